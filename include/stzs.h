@@ -1,0 +1,259 @@
+/*
+ * libstzs_hip.so — C-ABI of the MI355X-native StyleTTS-ZS synthesis hot path (gfx950).
+ *
+ * The upstream reference exposes NO interface for this path: `/root/reference/README.md:15-16`
+ * reads "## Inference / ### Under construction".  The entry points below are the operator
+ * boundary pinned by SURVEY.md §8(b) (L1 "torch ops" -> this C-ABI), one per hot-path function
+ * of SURVEY.md §8(a); each declaration names the row it implements.  INTEGRATION.md shows the
+ * ctypes binding (stzs/_lib.py) a maintainer would add on the reference side.
+ *
+ * Contract:
+ *   - plain pointers + element strides, no framework types; every tensor is caller-owned device
+ *     memory (the library never allocates on the hot path);
+ *   - channels-last ("NTC") activations: element (b, t, c) at b*bs + t*ld + c;
+ *   - every call is asynchronous on `stream` (a hipStream_t passed as void*), never syncs the
+ *     host, and is safe to capture into a hipGraph;
+ *   - returns STZS_OK (0) or a negative code; no exception crosses the ABI; stzs_strerror()
+ *     names it.  Shape/dtype violations are rejected before any launch.
+ */
+#ifndef STZS_H
+#define STZS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STZS_OK 0
+#define STZS_EINVAL (-1)  /* null pointer / bad enum / misaligned */
+#define STZS_ESHAPE (-2)  /* shape or stride violation */
+#define STZS_EDTYPE (-3)  /* unsupported dtype combination */
+#define STZS_EHIP (-4)    /* HIP runtime error on launch */
+
+enum { STZS_F32 = 0, STZS_BF16 = 1, STZS_I32 = 2 };
+enum { STZS_ACT_NONE = 0, STZS_ACT_LEAKY = 1, STZS_ACT_SNAKE = 2, STZS_ACT_GELU = 3, STZS_ACT_SILU = 4 };
+enum { STZS_PRO_NONE = 0, STZS_PRO_ADAIN = 1 };
+
+/* ---- library ---- */
+int stzs_init(int device);
+const char* stzs_strerror(int code);
+int stzs_version(void);
+
+/* ---- §8(a) a2/a9/a11/a12/a13-conv: the universal MFMA conv1d / linear -------------------
+ * y[b, t, co] = epi( sum_{k, ci} W[k, co, ci] * pro(x)[b, t*stride + k*dil - pad, ci] )
+ *   pro(x) = act_pro(x * sc[b,ci] + sh[b,ci]);  NONE: sc = pro_cscale, sh = 0;
+ *            ADAIN: sc = (1 + gamma) * rstd, sh = beta - mean * sc   (AdaIN1d, InstanceNorm)
+ *   epi(v) = ((act_epi(v + bias) * gate[b,co] + res[b, t/res_tdiv, co]) * alpha) + beta * acc_in
+ * Weights are pre-packed bf16 [ks][co_pad][ci_pad] (stzs/weights.py).  ups > 0 selects the
+ * polyphase ConvTranspose1d form (ks = 2, pad = 1, co = ups * Co): output row q, phase p lands at
+ * t = q*ups + p - ups_pad (+refl, with row 1 mirrored to row 0 for ReflectionPad(1,0)).
+ * Replaces: the decoder/predictor convs and every denoiser linear (SURVEY §8(a) a2,a9,a11,a12). */
+typedef struct stzs_conv_args {
+    const void* x;
+    const void* w;
+    const float* bias;
+    void* y;
+    const void* res;
+    const void* acc_in;
+    const float* gate;
+    const float* pro_mean;
+    const float* pro_rstd;
+    const float* pro_gb;
+    const float* pro_alpha;
+    int64_t ldx, bsx, ldy, bsy, ldr, bsr, lda, bsa;
+    int64_t gate_bs, stat_bs, gb_bs, gb_beta_off;
+    int32_t B, T_in, T_out, Ci, Co, ks, dil, stride, pad;
+    int32_t ci_pad, co_pad, cic;
+    int32_t ups, ups_pad, T_final, refl, res_tdiv;
+    int32_t in_dtype, out_dtype;
+    int32_t pro_mode, pro_act, epi_act, flags;
+    float pro_cscale, pro_slope, epi_slope, alpha, beta, pad_f;
+} stzs_conv_args;
+int stzs_conv1d(const stzs_conv_args* a, void* stream);
+
+/* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------
+ * x [B, T, ld] (bf16|f32), channels [0, C).  `partial` is caller workspace of
+ * stzs_chan_stats_workspace(B, T, C) bytes.  (SURVEY §8(a) a9/a12 AdaIN statistics) */
+typedef struct stzs_stats_args {
+    const void* x;
+    float* mean;
+    float* rstd;
+    void* partial;
+    int64_t ld, bs, stat_bs;
+    int32_t B, T, C, dtype;
+    float eps, pad_f;
+} stzs_stats_args;
+size_t stzs_chan_stats_workspace(int B, int T, int C);
+int stzs_chan_stats(const stzs_stats_args* a, void* stream);
+
+/* ---- row LayerNorm + modulation (+activation), one wave per row -------------------------
+ * y[r, c] = act((x - mu_r) * rstd_r * (gadd + G[(r/gdiv)*gs + c]) + Bt[(r/gdiv)*bs + c])
+ * (AdaLN / adaLN-single modulate / affine LayerNorm) */
+typedef struct stzs_rowln_args {
+    const void* x;
+    void* y;
+    const float* G;
+    const float* Bt;
+    int64_t ldx, ldy, gs, bs;
+    int32_t R, C, gdiv, in_dtype, out_dtype, act;
+    float gadd, eps, slope, pad_f;
+} stzs_rowln_args;
+int stzs_row_layernorm(const stzs_rowln_args* a, void* stream);
+
+/* ---- multi-head attention, softmax(q k^T / sqrt(dh)) v, rows independent ----------------
+ * q [R, Lq, ldq], k/v [R, Lk, ldk/ldv], o [R, Lq, ldo]; bf16; heads x dh = D.
+ * (denoiser self-attention over L_s codes, cross-attention to context) */
+typedef struct stzs_attn_args {
+    const void* q;
+    const void* k;
+    const void* v;
+    void* o;
+    int64_t ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso;
+    int32_t R, Lq, Lk, heads, dh, pad_i;
+} stzs_attn_args;
+int stzs_attention(const stzs_attn_args* a, void* stream);
+
+/* ---- LSTM recurrence (input projection done by stzs_conv1d) -----------------------------
+ * gx [B, T, ldg] f32 holds x W_ih^T + b_ih + b_hh for both directions (fwd 4H | rev 4H, gate
+ * order i,f,g,o); whhT [2][H][4H] f32; h written bf16 to y[b, t, dir*H + j].
+ * (DurationEncoder BiLSTMs, duration LSTM, shared LSTM) */
+typedef struct stzs_lstm_args {
+    const float* gx;
+    const float* whhT;
+    void* y;
+    int64_t ldg, bsg, ldy, bsy;
+    int32_t B, T, H, ndir;
+} stzs_lstm_args;
+int stzs_lstm(const stzs_lstm_args* a, void* stream);
+
+/* ---- predictor glue ---- */
+/* per-token style: linear resample of codes[:, :, c0:c0+Cs] (L_s rows) to T rows (F.interpolate
+ * linear, align_corners=False) into y[b, t, yc0 + c], plus copy of h[b, t, 0:Ch] to y[..., 0:Ch] */
+typedef struct stzs_prprep_args {
+    const float* codes;
+    const void* h;
+    void* y;
+    int64_t ldc, bsc, ldh, bsh, ldy, bsy;
+    int32_t B, L, T, c0, Cs, Ch, yc0, pad_i;
+} stzs_prprep_args;
+int stzs_predictor_prep(const stzs_prprep_args* a, void* stream);
+
+/* durations: round(sum_j sigmoid(logit_j)) (serial fp32 sum), clamp >= 1; override if given */
+typedef struct stzs_dur_args {
+    const float* logits;
+    const int32_t* override_dur;
+    int32_t* dur;
+    float* dsum;
+    int64_t ldl, bsl;
+    int32_t B, T, nbins, pad_i;
+} stzs_dur_args;
+int stzs_durations(const stzs_dur_args* a, void* stream);
+
+/* alignment: exclusive scan of dur -> token index per aligned frame idx[b, f], f < T40;
+ * frames beyond sum(dur) get -1; total[b] = sum(dur). */
+typedef struct stzs_align_args {
+    const int32_t* dur;
+    int32_t* idx;
+    int32_t* total;
+    int32_t B, T, T40, pad_i;
+} stzs_align_args;
+int stzs_alignment(const stzs_align_args* a, void* stream);
+
+/* row gather: y[b, f, yc0 + c] = x[b, idx[b, f], xc0 + c] for c < C (C % 8 == 0); idx<0 -> 0 */
+typedef struct stzs_gather_args {
+    const void* x;
+    const int32_t* idx;
+    void* y;
+    int64_t ldx, bsx, ldy, bsy;
+    int32_t B, Tsrc, Tdst, C, xc0, yc0, dtype, pad_i;
+} stzs_gather_args;
+int stzs_gather_rows(const stzs_gather_args* a, void* stream);
+
+/* AdaIN + LeakyReLU(0.2) + depthwise ConvTranspose1d(k3, s2, p1, op1): [B,T,C] -> [B,2T,C] */
+typedef struct stzs_dwup_args {
+    const void* x;
+    void* y;
+    const float* mean;
+    const float* rstd;
+    const float* gb;
+    const float* w;   /* [C][3] */
+    const float* wb;  /* [C] */
+    int64_t ldx, bsx, ldy, bsy, stat_bs, gb_bs, gb_beta_off;
+    int32_t B, T, C, pad_i;
+    float slope, pad_f;
+} stzs_dwup_args;
+int stzs_adain_dwup(const stzs_dwup_args* a, void* stream);
+
+/* Conv1d(1,1,k3,s2,p1) on F0 and N [B, T80] f32 -> bf16 channels of up to two destinations */
+typedef struct stzs_f0n_args {
+    const float* f0;
+    const float* n;
+    const float* wf; /* 4 floats: w0 w1 w2 bias */
+    const float* wn;
+    void* y0;
+    void* y1;
+    int64_t ldf, ldy0, bsy0, ldy1, bsy1;
+    int32_t B, T80, cf0, cn0, cf1, cn1;
+} stzs_f0n_args;
+int stzs_f0n_down(const stzs_f0n_args* a, void* stream);
+
+/* ---- decoder source + iSTFT ---- */
+/* harmonic source (SineGen, counter-RNG noise, Linear(9->1)+tanh) and its n_fft STFT
+ * (real | imag) -> har [B, Tf, ldh] bf16, Tf = T80*hop/hop_s + 1.  `prefix` is caller workspace
+ * [B][nh][T80] f32 (frame-rate phase prefix, computed in fp64 and wrapped every frame). */
+typedef struct stzs_source_args {
+    const float* f0;
+    const uint32_t* seeds;
+    const float* merge_w; /* nh weights + 1 bias */
+    float* prefix;
+    void* har;
+    int64_t ldf, ldh, bsh;
+    int32_t B, T80, hop, n_fft, hop_s, nh;
+    float sr, sine_amp, noise_std, voiced_thr;
+} stzs_source_args;
+int stzs_harmonic_source(const stzs_source_args* a, void* stream);
+
+/* iSTFT: post [B, Tf, ldp] f32 (n_bins log-mag | n_bins phase-arg) -> wav [B, (Tf-1)*hop_s]
+ * spec = exp(m) * exp(i sin(p)); hann window, center=True, window-square normalisation */
+typedef struct stzs_istft_args {
+    const float* post;
+    float* wav;
+    int64_t ldp, bsp, bsw;
+    int32_t B, Tf, n_fft, hop_s;
+} stzs_istft_args;
+int stzs_istft(const stzs_istft_args* a, void* stream);
+
+/* ---- sampler glue ---- */
+/* c[r, j] = silu(pool[r, j] + temb[j]) -> bf16 */
+int stzs_dn_cond(const float* pool, const float* temb, void* c, int R, int D, void* stream);
+/* out[l][r][j] = mod[r][j] + (table ? table[l][j] : 0) + ((j / D) in scale_mask ? 1 : 0) */
+int stzs_adaln_expand(const float* mod, const float* table, float* out, int R, int D, int nchunk,
+                      int nlayers, unsigned scale_mask, void* stream);
+/* fused CFG combine + Euler step on the duplicated state x [R, N] (R = B or 2B):
+ * Dg = cfg ? D_u + s (D_c - D_u) : D_c ;  x <- x + dsig (x - Dg) / s0 (both halves),
+ * dsig = sigma_{i+1} - sigma_i rounded once from fp64 on the host */
+int stzs_cfg_euler(float* x, const float* D, int B, int N, int cfg, float scale, float s0,
+                   float dsig, void* stream);
+/* x[r, :] = eps[b, :] * sigma for both halves (state init) */
+int stzs_state_init(float* x, const float* eps, int B, int N, int cfg, float sigma, void* stream);
+/* y[b, c] = mean_l x[b, l, c0 + c]  (pooled style / prompt vectors), f32 */
+int stzs_mean_rows(const float* x, float* y, int B, int L, int64_t ldx, int64_t bsx, int c0,
+                   int C, int64_t ldy, void* stream);
+/* generic strided 2-D copy with dtype conversion: R rows x C cols (row r of batch b) */
+typedef struct stzs_copy_args {
+    const void* x;
+    void* y;
+    int64_t ldx, bsx, ldy, bsy;
+    int32_t B, R, C, in_dtype, out_dtype, pad_i;
+} stzs_copy_args;
+int stzs_copy2d(const stzs_copy_args* a, void* stream);
+/* token embedding gather: y[b, t, :] = emb[tok[b, t], :] (f32 table -> bf16 rows) */
+int stzs_embed(const int32_t* tok, const float* emb, void* y, int B, int T, int D, int64_t ldy,
+               void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STZS_H */

@@ -1,0 +1,90 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of libstzs_hip.so.
+// Wave = 64 lanes everywhere; bf16 is stored as raw 16-bit words and converted with RNE.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/stzs.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef uint16_t bf16_t;
+
+#define STZS_DEV __device__ __forceinline__
+
+STZS_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+STZS_DEV bf16_t f2bf(float f) {
+    __bf16 h = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving on gfx950
+    return __builtin_bit_cast(bf16_t, h);
+}
+
+template <typename T> struct DT;
+template <> struct DT<float> {
+    static STZS_DEV float ld(const float* p) { return *p; }
+    static STZS_DEV void st(float* p, float v) { *p = v; }
+};
+template <> struct DT<bf16_t> {
+    static STZS_DEV float ld(const bf16_t* p) { return bf2f(*p); }
+    static STZS_DEV void st(bf16_t* p, float v) { *p = f2bf(v); }
+};
+
+// load 8 consecutive elements (16-B aligned for bf16, 32-B for f32) as floats
+STZS_DEV void load8(const bf16_t* p, float* v) {
+    uint4 u = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+}
+STZS_DEV void load8(const float* p, float* v) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+STZS_DEV uint4 pack8(const float* v) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+STZS_DEV void store8(bf16_t* p, const float* v) { *reinterpret_cast<uint4*>(p) = pack8(v); }
+STZS_DEV void store8(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+STZS_DEV float act_apply(int act, float x, float slope, float alpha) {
+    switch (act) {
+        case STZS_ACT_LEAKY: return x >= 0.f ? x : x * slope;
+        case STZS_ACT_SNAKE: {
+            float s = sinf(alpha * x);
+            return x + s * s / alpha;
+        }
+        case STZS_ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+        case STZS_ACT_SILU: return x / (1.f + expf(-x));
+        default: return x;
+    }
+}
+
+STZS_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+STZS_DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+#define STZS_LAUNCH_CHECK()                                          \
+    do {                                                             \
+        hipError_t e__ = hipGetLastError();                          \
+        if (e__ != hipSuccess) return STZS_EHIP;                     \
+    } while (0)
+
+static inline bool stzs_aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }

@@ -1,0 +1,179 @@
+// Normalisation statistics and row LayerNorm.
+//
+// stzs_chan_stats: InstanceNorm1d statistics per (b, c) over time for channels-last
+// activations.  Pass 1 streams the tensor once with 16-B loads (8 channels per lane, rows split
+// over the 8 row-lanes of a 256-thread block) and writes fp32 partial (sum, sumsq) per
+// 256-row chunk; pass 2 combines the chunks in a fixed order in fp64 -> deterministic,
+// bit-reproducible statistics (no float atomics).  HBM-bound: 1 read of the tensor.
+//
+// stzs_row_layernorm: one wave per row, values kept in registers, two-pass mean/variance
+// (as torch.layer_norm), fused modulation  (gadd + G) * x_hat + Bt  and activation.
+#include "common.hpp"
+
+namespace {
+
+constexpr int STAT_ROWS = 256;  // rows per partial chunk
+constexpr int STAT_CG = 32;     // 8-channel vectors per block (256 channels)
+
+template <typename T>
+__global__ __launch_bounds__(256) void chan_stats_partial(const stzs_stats_args a, int nchunk) {
+    __shared__ float red[8][STAT_CG * 8][2];
+    const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
+    const int chunk = blockIdx.x, b = blockIdx.y;
+    const int cv = blockIdx.z * STAT_CG + tx;
+    const int c = cv * 8;
+    float s[8], q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+    const int r0 = chunk * STAT_ROWS, r1 = min(a.T, r0 + STAT_ROWS);
+    const T* X = reinterpret_cast<const T*>(a.x) + (long)b * a.bs;
+    if (c < a.C) {
+        for (int r = r0 + ty; r < r1; r += 8) {
+            float v[8];
+            load8(X + (long)r * a.ld + c, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                s[j] += v[j];
+                q[j] += v[j] * v[j];
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        red[ty][tx * 8 + j][0] = s[j];
+        red[ty][tx * 8 + j][1] = q[j];
+    }
+    __syncthreads();
+    // 256 threads: one channel of the block's 256 each
+    const int cl = tid;
+    const int cg = blockIdx.z * STAT_CG * 8 + cl;
+    if (cg < a.C) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int y = 0; y < 8; ++y) {
+            ss += red[y][cl][0];
+            qq += red[y][cl][1];
+        }
+        float* P = reinterpret_cast<float*>(a.partial);
+        const long o = (((long)b * nchunk + chunk) * a.C + cg) * 2;
+        P[o] = ss;
+        P[o + 1] = qq;
+    }
+}
+
+__global__ __launch_bounds__(256) void chan_stats_final(const stzs_stats_args a, int nchunk) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)a.B * a.C) return;
+    const int b = (int)(i / a.C), c = (int)(i - (long)b * a.C);
+    const float* P = reinterpret_cast<const float*>(a.partial);
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < nchunk; ++k) {
+        const long o = (((long)b * nchunk + k) * a.C + c) * 2;
+        s += (double)P[o];
+        q += (double)P[o + 1];
+    }
+    const double mean = s / a.T;
+    double var = q / a.T - mean * mean;
+    if (var < 0.0) var = 0.0;
+    a.mean[(long)b * a.stat_bs + c] = (float)mean;
+    a.rstd[(long)b * a.stat_bs + c] = (float)(1.0 / sqrt(var + (double)a.eps));
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void row_ln(const stzs_rowln_args a) {
+    constexpr int MAXV = 4;
+    const int lane = threadIdx.x & 63;
+    const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= a.R) return;
+    const TI* X = reinterpret_cast<const TI*>(a.x) + r * a.ldx;
+    const int nv = a.C >> 3;
+    float v[MAXV][8];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        const int vi = lane + i * 64;
+        if (vi < nv) {
+            load8(X + vi * 8, v[i]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += v[i][j];
+        }
+    }
+    const float mu = wave_sum(s) / a.C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        const int vi = lane + i * 64;
+        if (vi < nv) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float d = v[i][j] - mu;
+                q += d * d;
+            }
+        }
+    }
+    const float rstd = 1.f / sqrtf(wave_sum(q) / a.C + a.eps);
+    const long grp = r / a.gdiv;
+    TO* Y = reinterpret_cast<TO*>(a.y) + r * a.ldy;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        const int vi = lane + i * 64;
+        if (vi < nv) {
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = vi * 8 + j;
+                float g = a.gadd + (a.G ? a.G[grp * a.gs + c] : 0.f);
+                float bt = a.Bt ? a.Bt[grp * a.bs + c] : 0.f;
+                o[j] = act_apply(a.act, (v[i][j] - mu) * rstd * g + bt, a.slope, 1.f);
+            }
+            store8(Y + vi * 8, o);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" size_t stzs_chan_stats_workspace(int B, int T, int C) {
+    const int nchunk = (T + STAT_ROWS - 1) / STAT_ROWS;
+    return (size_t)B * nchunk * C * 2 * sizeof(float);
+}
+
+extern "C" int stzs_chan_stats(const stzs_stats_args* a, void* stream) {
+    if (!a || !a->x || !a->mean || !a->rstd || !a->partial) return STZS_EINVAL;
+    if (a->B <= 0 || a->T <= 0 || a->C <= 0 || a->ld % 8 || a->bs % 8 || a->ld < a->C) return STZS_ESHAPE;
+    if (a->C % 8) return STZS_ESHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int nchunk = (a->T + STAT_ROWS - 1) / STAT_ROWS;
+    dim3 g1(nchunk, a->B, (a->C + STAT_CG * 8 - 1) / (STAT_CG * 8));
+    if (a->dtype == STZS_BF16)
+        hipLaunchKernelGGL(chan_stats_partial<bf16_t>, g1, dim3(256), 0, s, *a, nchunk);
+    else if (a->dtype == STZS_F32)
+        hipLaunchKernelGGL(chan_stats_partial<float>, g1, dim3(256), 0, s, *a, nchunk);
+    else
+        return STZS_EDTYPE;
+    STZS_LAUNCH_CHECK();
+    const long n = (long)a->B * a->C;
+    hipLaunchKernelGGL(chan_stats_final, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, *a, nchunk);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_row_layernorm(const stzs_rowln_args* a, void* stream) {
+    if (!a || !a->x || !a->y) return STZS_EINVAL;
+    if (a->R <= 0 || a->C <= 0 || a->C % 8 || a->C > 2048 || a->ldx % 8 || a->ldy % 8 || a->gdiv <= 0)
+        return STZS_ESHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    dim3 g((a->R + 3) / 4);
+    if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16)
+        hipLaunchKernelGGL((row_ln<bf16_t, bf16_t>), g, dim3(256), 0, s, *a);
+    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_BF16)
+        hipLaunchKernelGGL((row_ln<float, bf16_t>), g, dim3(256), 0, s, *a);
+    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32)
+        hipLaunchKernelGGL((row_ln<float, float>), g, dim3(256), 0, s, *a);
+    else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32)
+        hipLaunchKernelGGL((row_ln<bf16_t, float>), g, dim3(256), 0, s, *a);
+    else
+        return STZS_EDTYPE;
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}

@@ -1,0 +1,147 @@
+// Harmonic source of the iSTFT decoder: NSF SineGen from F0, counter-RNG
+// noise, Linear(9->1) + tanh merge, and its n_fft-point STFT (real | imag) feeding noise_convs.
+//
+// Phase accuracy (SURVEY §7 "SineGen phase cumsum drifts in fp32"): a per-(utterance, harmonic)
+// thread accumulates the frame-rate phase prefix in fp64 and wraps it every 80-fps frame; the
+// in-frame phase is then prefix + (j+1) * f/sr in fp32 (|arg| < 60 cycles, so < 4e-6 cycles of
+// error).  Every fp32/fp64 op that must agree bit-for-bit with the oracle uses explicit _rn
+// intrinsics (no FMA contraction).  Samples are generated once per workgroup into LDS
+// (reflect-padded at the ends, centre=True) and consumed by all frames that overlap them.
+#include "common.hpp"
+
+namespace {
+
+STZS_DEV uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+STZS_DEV uint32_t stream_key(uint32_t seed, uint32_t stream) {
+    return hash32(hash32(seed + 0x9E3779B9u) ^ stream);
+}
+STZS_DEV float counter_normal(uint32_t key, uint32_t idx) {
+    const uint32_t a = hash32(key ^ hash32(idx * 2u));
+    const uint32_t b = hash32(key ^ hash32(idx * 2u + 1u));
+    const double u1 = ((double)(a >> 8) + 1.0) * (1.0 / 16777216.0);
+    const double u2 = (double)(b >> 8) * (1.0 / 16777216.0);
+    return (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+}
+STZS_DEV float initial_phase(uint32_t key) {
+    return (float)((double)(hash32(key ^ 0xA5A5A5A5u) >> 8) * (1.0 / 16777216.0));
+}
+
+__global__ void phase_prefix_kernel(const stzs_source_args a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.B * a.nh) return;
+    const int b = i / a.nh, h = i - b * a.nh;
+    const float* F = a.f0 + (long)b * a.ldf;
+    float* P = a.prefix + (long)i * a.T80;
+    double acc = 0.0;
+    for (int k = 0; k < a.T80; ++k) {
+        P[k] = (float)acc;
+        const double inc = __ddiv_rn(__dmul_rn((double)F[k], (double)(h + 1)), (double)a.sr);
+        acc = __dadd_rn(acc, __dmul_rn((double)a.hop, inc));
+        acc = acc - floor(acc);
+    }
+}
+
+constexpr int FB = 256;  // STFT frames per workgroup
+
+__global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args a) {
+    extern __shared__ float sm[];
+    const int nfft = a.n_fft, hs = a.hop_s, nb = nfft / 2 + 1;
+    const int NS = hs * (FB - 1) + nfft;
+    float* sbuf = sm;                 // NS samples
+    float* twc = sbuf + NS;           // nfft cos
+    float* tws = twc + nfft;          // nfft sin
+    float* win = tws + nfft;          // nfft hann
+    uint32_t* keys = reinterpret_cast<uint32_t*>(win + nfft);  // nh
+    float* ph0 = reinterpret_cast<float*>(keys + a.nh);        // nh
+    const int b = blockIdx.y, f0i = blockIdx.x * FB, tid = threadIdx.x;
+    const int N = a.T80 * a.hop;
+    const int Tf = N / hs + 1;
+    if (tid < nfft) {
+        const double ang = 2.0 * 3.141592653589793 * tid / nfft;
+        twc[tid] = (float)cos(ang);
+        tws[tid] = (float)sin(ang);
+        win[tid] = (float)(0.5 - 0.5 * cos(ang));
+    }
+    if (tid < a.nh) {
+        const uint32_t key = stream_key(a.seeds[b], (uint32_t)tid);
+        keys[tid] = key;
+        ph0[tid] = tid == 0 ? 0.f : initial_phase(key);
+    }
+    __syncthreads();
+    const float* F = a.f0 + (long)b * a.ldf;
+    const float* P = a.prefix + (long)b * a.nh * a.T80;
+    const float amp = a.sine_amp, amp3 = __fdiv_rn(a.sine_amp, 3.0f), two_pi = 6.2831853071795864f;
+    const float wb = a.merge_w[a.nh];
+    for (int p = tid; p < NS; p += 256) {
+        int n = (f0i * hs + p) - nfft / 2;  // centre=True: padded index -> signal index
+        if (n < 0) n = -n;
+        if (n >= N) n = 2 * (N - 1) - n;
+        float v = 0.f;
+        if (n >= 0 && n < N) {
+            const int k = n / a.hop;
+            const float jj = (float)(n - k * a.hop + 1);
+            const float f0v = F[k];
+            const bool voiced = f0v > a.voiced_thr;
+            const float uv = voiced ? 1.f : 0.f;
+            const float namp = voiced ? a.noise_std : amp3;
+            float acc = 0.f;
+            for (int h = 0; h < a.nh; ++h) {
+                const float inc = __fdiv_rn(__fmul_rn(f0v, (float)(h + 1)), a.sr);
+                float t = __fadd_rn(P[(long)h * a.T80 + k], ph0[h]);
+                t = __fadd_rn(t, __fmul_rn(jj, inc));
+                const float th = __fsub_rn(t, floorf(t));
+                const float sine = __fmul_rn(amp, sinf(__fmul_rn(two_pi, th)));
+                const float z = counter_normal(keys[h], (uint32_t)n);
+                const float sw = __fadd_rn(__fmul_rn(sine, uv), __fmul_rn(namp, z));
+                acc = __fadd_rn(acc, __fmul_rn(a.merge_w[h], sw));
+            }
+            v = tanhf(__fadd_rn(acc, wb));
+        }
+        sbuf[p] = v;
+    }
+    __syncthreads();
+    const int f = f0i + tid;
+    if (tid < FB && f < Tf) {
+        const float* s = sbuf + tid * hs;
+        bf16_t* Hh = reinterpret_cast<bf16_t*>(a.har) + (long)b * a.bsh + (long)f * a.ldh;
+        for (int kb = 0; kb < nb; ++kb) {
+            float re = 0.f, im = 0.f;
+            for (int i = 0; i < nfft; ++i) {
+                const int m = (kb * i) % nfft;
+                const float x = s[i] * win[i];
+                re += x * twc[m];
+                im -= x * tws[m];
+            }
+            Hh[kb] = f2bf(re);
+            Hh[nb + kb] = f2bf(im);
+        }
+        for (int c = 2 * nb; c < a.ldh; ++c) Hh[c] = 0;
+    }
+}
+
+}  // namespace
+
+extern "C" int stzs_harmonic_source(const stzs_source_args* a, void* stream) {
+    if (!a || !a->f0 || !a->seeds || !a->merge_w || !a->prefix || !a->har) return STZS_EINVAL;
+    if (a->B <= 0 || a->T80 <= 0 || a->nh <= 0 || a->nh > 64 || a->n_fft <= 0 || a->n_fft > 64 || a->hop_s <= 0)
+        return STZS_ESHAPE;
+    if (a->ldh < 2 * (a->n_fft / 2 + 1)) return STZS_ESHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int n = a->B * a->nh;
+    hipLaunchKernelGGL(phase_prefix_kernel, dim3((n + 63) / 64), dim3(64), 0, s, *a);
+    STZS_LAUNCH_CHECK();
+    const int N = a->T80 * a->hop;
+    const int Tf = N / a->hop_s + 1;
+    const int NS = a->hop_s * (FB - 1) + a->n_fft;
+    const size_t lds = (size_t)(NS + 3 * a->n_fft) * 4 + (size_t)a->nh * 8;
+    hipLaunchKernelGGL(source_stft_kernel, dim3((Tf + FB - 1) / FB, a->B), dim3(256), lds, s, *a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}

@@ -1,0 +1,176 @@
+"""ctypes binding of libstzs_hip.so (the C-ABI declared in include/stzs.h).
+
+This is also the reference-side binding stub shown in INTEGRATION.md: the structures below
+mirror the header field-for-field.  The library is built in-tree by styletts-zs_amd/build.py;
+there is deliberately NO fallback — importing the product path without the library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("STZS_LIB", os.path.join(_HERE, "libstzs_hip.so"))
+
+F32, BF16, I32 = 0, 1, 2
+ACT_NONE, ACT_LEAKY, ACT_SNAKE, ACT_GELU, ACT_SILU = 0, 1, 2, 3, 4
+PRO_NONE, PRO_ADAIN = 0, 1
+
+vp = C.c_void_p
+i64 = C.c_int64
+i32 = C.c_int32
+f32 = C.c_float
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [(n, vp) for n in ("x", "w", "bias", "y", "res", "acc_in", "gate", "pro_mean", "pro_rstd",
+                                  "pro_gb", "pro_alpha")] + \
+               [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy", "ldr", "bsr", "lda", "bsa",
+                                   "gate_bs", "stat_bs", "gb_bs", "gb_beta_off")] + \
+               [(n, i32) for n in ("B", "T_in", "T_out", "Ci", "Co", "ks", "dil", "stride", "pad",
+                                   "ci_pad", "co_pad", "cic", "ups", "ups_pad", "T_final", "refl", "res_tdiv",
+                                   "in_dtype", "out_dtype", "pro_mode", "pro_act", "epi_act", "flags")] + \
+               [(n, f32) for n in ("pro_cscale", "pro_slope", "epi_slope", "alpha", "beta", "pad_f")]
+
+
+class StatsArgs(C.Structure):
+    _fields_ = [("x", vp), ("mean", vp), ("rstd", vp), ("partial", vp),
+                ("ld", i64), ("bs", i64), ("stat_bs", i64),
+                ("B", i32), ("T", i32), ("C", i32), ("dtype", i32), ("eps", f32), ("pad_f", f32)]
+
+
+class RowLNArgs(C.Structure):
+    _fields_ = [("x", vp), ("y", vp), ("G", vp), ("Bt", vp),
+                ("ldx", i64), ("ldy", i64), ("gs", i64), ("bs", i64),
+                ("R", i32), ("C", i32), ("gdiv", i32), ("in_dtype", i32), ("out_dtype", i32), ("act", i32),
+                ("gadd", f32), ("eps", f32), ("slope", f32), ("pad_f", f32)]
+
+
+class AttnArgs(C.Structure):
+    _fields_ = [("q", vp), ("k", vp), ("v", vp), ("o", vp)] + \
+               [(n, i64) for n in ("ldq", "ldk", "ldv", "ldo", "bsq", "bsk", "bsv", "bso")] + \
+               [(n, i32) for n in ("R", "Lq", "Lk", "heads", "dh", "pad_i")]
+
+
+class LstmArgs(C.Structure):
+    _fields_ = [("gx", vp), ("whhT", vp), ("y", vp),
+                ("ldg", i64), ("bsg", i64), ("ldy", i64), ("bsy", i64),
+                ("B", i32), ("T", i32), ("H", i32), ("ndir", i32)]
+
+
+class PrPrepArgs(C.Structure):
+    _fields_ = [("codes", vp), ("h", vp), ("y", vp)] + \
+               [(n, i64) for n in ("ldc", "bsc", "ldh", "bsh", "ldy", "bsy")] + \
+               [(n, i32) for n in ("B", "L", "T", "c0", "Cs", "Ch", "yc0", "pad_i")]
+
+
+class DurArgs(C.Structure):
+    _fields_ = [("logits", vp), ("override_dur", vp), ("dur", vp), ("dsum", vp),
+                ("ldl", i64), ("bsl", i64), ("B", i32), ("T", i32), ("nbins", i32), ("pad_i", i32)]
+
+
+class AlignArgs(C.Structure):
+    _fields_ = [("dur", vp), ("idx", vp), ("total", vp), ("B", i32), ("T", i32), ("T40", i32), ("pad_i", i32)]
+
+
+class GatherArgs(C.Structure):
+    _fields_ = [("x", vp), ("idx", vp), ("y", vp)] + \
+               [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy")] + \
+               [(n, i32) for n in ("B", "Tsrc", "Tdst", "C", "xc0", "yc0", "dtype", "pad_i")]
+
+
+class DwupArgs(C.Structure):
+    _fields_ = [(n, vp) for n in ("x", "y", "mean", "rstd", "gb", "w", "wb")] + \
+               [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy", "stat_bs", "gb_bs", "gb_beta_off")] + \
+               [("B", i32), ("T", i32), ("C", i32), ("pad_i", i32), ("slope", f32), ("pad_f", f32)]
+
+
+class F0nArgs(C.Structure):
+    _fields_ = [(n, vp) for n in ("f0", "n", "wf", "wn", "y0", "y1")] + \
+               [(n, i64) for n in ("ldf", "ldy0", "bsy0", "ldy1", "bsy1")] + \
+               [(n, i32) for n in ("B", "T80", "cf0", "cn0", "cf1", "cn1")]
+
+
+class SourceArgs(C.Structure):
+    _fields_ = [(n, vp) for n in ("f0", "seeds", "merge_w", "prefix", "har")] + \
+               [(n, i64) for n in ("ldf", "ldh", "bsh")] + \
+               [(n, i32) for n in ("B", "T80", "hop", "n_fft", "hop_s", "nh")] + \
+               [(n, f32) for n in ("sr", "sine_amp", "noise_std", "voiced_thr")]
+
+
+class IstftArgs(C.Structure):
+    _fields_ = [("post", vp), ("wav", vp), ("ldp", i64), ("bsp", i64), ("bsw", i64),
+                ("B", i32), ("Tf", i32), ("n_fft", i32), ("hop_s", i32)]
+
+
+class CopyArgs(C.Structure):
+    _fields_ = [("x", vp), ("y", vp)] + [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy")] + \
+               [(n, i32) for n in ("B", "R", "C", "in_dtype", "out_dtype", "pad_i")]
+
+
+# every exported symbol of include/stzs.h (tests check the .so exports exactly these)
+EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_chan_stats_workspace",
+           "stzs_chan_stats", "stzs_row_layernorm", "stzs_attention", "stzs_lstm", "stzs_predictor_prep",
+           "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
+           "stzs_harmonic_source", "stzs_istft", "stzs_dn_cond", "stzs_adaln_expand", "stzs_cfg_euler",
+           "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed"]
+
+_lib = None
+
+
+class StzsError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library (raises if it was not built — no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise StzsError(f"libstzs_hip.so not found at {LIB_PATH}: run `python styletts-zs_amd/build.py` "
+                        "(the product path has no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    sig = {
+        "stzs_init": ([i32], i32),
+        "stzs_strerror": ([i32], C.c_char_p),
+        "stzs_version": ([], i32),
+        "stzs_conv1d": ([P(ConvArgs), vp], i32),
+        "stzs_chan_stats_workspace": ([i32, i32, i32], C.c_size_t),
+        "stzs_chan_stats": ([P(StatsArgs), vp], i32),
+        "stzs_row_layernorm": ([P(RowLNArgs), vp], i32),
+        "stzs_attention": ([P(AttnArgs), vp], i32),
+        "stzs_lstm": ([P(LstmArgs), vp], i32),
+        "stzs_predictor_prep": ([P(PrPrepArgs), vp], i32),
+        "stzs_durations": ([P(DurArgs), vp], i32),
+        "stzs_alignment": ([P(AlignArgs), vp], i32),
+        "stzs_gather_rows": ([P(GatherArgs), vp], i32),
+        "stzs_adain_dwup": ([P(DwupArgs), vp], i32),
+        "stzs_f0n_down": ([P(F0nArgs), vp], i32),
+        "stzs_harmonic_source": ([P(SourceArgs), vp], i32),
+        "stzs_istft": ([P(IstftArgs), vp], i32),
+        "stzs_dn_cond": ([vp, vp, vp, i32, i32, vp], i32),
+        "stzs_adaln_expand": ([vp, vp, vp, i32, i32, i32, i32, C.c_uint32, vp], i32),
+        "stzs_cfg_euler": ([vp, vp, i32, i32, i32, f32, f32, f32, vp], i32),
+        "stzs_state_init": ([vp, vp, i32, i32, i32, f32, vp], i32),
+        "stzs_mean_rows": ([vp, vp, i32, i32, i64, i64, i32, i32, i64, vp], i32),
+        "stzs_copy2d": ([P(CopyArgs), vp], i32),
+        "stzs_embed": ([vp, vp, vp, i32, i32, i32, i64, vp], i32),
+    }
+    for name, (argt, rest) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = argt
+        fn.restype = rest
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = load().stzs_strerror(rc).decode()
+        raise StzsError(f"{what}: {msg} (rc={rc})")
+
+
+def strerror(rc: int) -> str:
+    return load().stzs_strerror(rc).decode()

@@ -1,0 +1,648 @@
+"""StyleTTS-ZS synthesis engine on MI355X: the L4 host pipeline over libstzs_hip.so.
+
+API (the upstream inference API is "Under construction",
+`/root/reference/README.md:15-16`, so this pins it in the StyleTTS2-family shape
+`inference(text, ref_s, diffusion_steps, embedding_scale)`):
+
+    eng = StyleTTSZS(spec, params, device="cuda:0")
+    out = eng.synth(tokens, ref_wav, steps=2, cfg_scale=5.0, noise=eps, durations=dur)
+    codes = eng.sample_style(h_txt, prompt, eps, steps, cfg_scale)     # (a) style diffusion
+    pro   = eng.predict_prosody(h_txt, codes, durations)               # (b) duration/prosody
+    wav   = eng.decode(pro, codes, seeds)                              # (c) iSTFT decoder
+
+Every hot-path FLOP runs in a hand-written gfx950 kernel reached through the C-ABI; PyTorch only
+provides device memory (caching allocator), the stream, and hosts the front ends that SURVEY §8(f)
+lists as "next" (log-mel + prompt encoder).  Buffers are cached per shape so a whole synth() can
+be captured into one HIP graph (`capture()`), which removes all host launch overhead.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+from .frontend import log_mel, mel_filterbank
+from .spec import Spec
+from .weights import ConvW, PackedModel
+
+_DT = {torch.float32: L.F32, torch.bfloat16: L.BF16}
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class Act:
+    """channels-last activation view: buffer [B, T, ld], logical channels [c0, c0 + C)."""
+    t: torch.Tensor
+    c0: int = 0
+    C: int = -1
+
+    def __post_init__(self):
+        if self.C < 0:
+            self.C = self.t.shape[-1] - self.c0
+
+    @property
+    def B(self):
+        return self.t.shape[0]
+
+    @property
+    def T(self):
+        return self.t.shape[1]
+
+    @property
+    def ld(self):
+        return self.t.shape[2]
+
+    @property
+    def bs(self):
+        return self.t.shape[1] * self.t.shape[2]
+
+    @property
+    def ptr(self):
+        return self.t.data_ptr() + self.c0 * self.t.element_size()
+
+    @property
+    def dt(self):
+        return _DT[self.t.dtype]
+
+    def sl(self, c0, C):
+        return Act(self.t, self.c0 + c0, C)
+
+    def rows(self, b0, nb):
+        return Act(self.t[b0:b0 + nb], self.c0, self.C)
+
+
+def sigma_schedule(spec: Spec, steps: int):
+    """Distilled pins 1: [smax, 0], 2: [smax, 0.5, 0]; otherwise Karras(rho) + trailing 0 (a1)."""
+    if steps == 1:
+        return [spec.sigma_max, 0.0]
+    if steps == 2:
+        return [spec.sigma_max, 0.5, 0.0]
+    lo, hi = spec.sigma_min ** (1 / spec.rho), spec.sigma_max ** (1 / spec.rho)
+    return [(hi + i / (steps - 1) * (lo - hi)) ** spec.rho for i in range(steps)] + [0.0]
+
+
+def edm_coeffs(spec: Spec, sigma: float):
+    sd = spec.sigma_data
+    return dict(c_in=1.0 / math.sqrt(sigma ** 2 + sd ** 2), c_skip=sd ** 2 / (sigma ** 2 + sd ** 2),
+                c_out=sigma * sd / math.sqrt(sigma ** 2 + sd ** 2), c_noise=math.log(sigma) / 4.0)
+
+
+def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
+    half = spec.dn_fourier // 2
+    f = np.exp(-math.log(10000.0) * np.arange(half) / half)
+    arg = 1000.0 * c_noise * f
+    return np.concatenate([np.cos(arg), np.sin(arg)]).astype(np.float32)
+
+
+class StyleTTSZS:
+    def __init__(self, spec: Spec, params, device="cuda:0", fill=True):
+        self.spec = spec
+        self.device = torch.device(device)
+        self.lib = L.load()
+        L.check(self.lib.stzs_init(self.device.index or 0), "stzs_init")
+        self.W = PackedModel(spec, params, self.device, fill=fill)
+        # hosted front end (log-mel + prompt encoder), fp32 torch on the device
+        self.fe = {k: v.to(self.device).float() for k, v in params.items() if k.startswith("pe.")}
+        self.mel_fb = mel_filterbank(spec.n_mels, spec.mel_nfft, spec.sr).to(self.device)
+        self._bufs = {}
+        self._ws = None
+        self.launches = 0
+
+    # ------------------------------------------------------------------ plumbing
+    def stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def buf(self, key, shape, dtype=torch.bfloat16, zero=False):
+        """cached device buffer (stable address across calls -> graph-capturable)."""
+        k = (key, tuple(shape), dtype)
+        t = self._bufs.get(k)
+        if t is None:
+            t = torch.zeros(shape, dtype=dtype, device=self.device) if zero else \
+                torch.empty(shape, dtype=dtype, device=self.device)
+            self._bufs[k] = t
+        return t
+
+    def act(self, key, B, T, C, dtype=torch.bfloat16):
+        return Act(self.buf(key, (B, T, _rup(C, 8)), dtype, zero=True), 0, C)
+
+    def _t(self, x):
+        """weight reference -> device tensor (arena name, or an already-resolved tensor)."""
+        return x if isinstance(x, torch.Tensor) else self.W.t(x)
+
+    def _call(self, fn, arg, what):
+        self.launches += 1
+        L.check(fn(C.byref(arg), self.stream()), what)
+
+    # ------------------------------------------------------------------ ops
+    def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
+             pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
+             alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
+             T_final=0, refl=0, what="conv"):
+        W = self.W
+        a = L.ConvArgs()
+        a.x, a.w, a.y = x.ptr, self._t(cw.w).data_ptr(), y.ptr
+        a.bias = self._t(cw.b).data_ptr() if cw.b is not None else None
+        a.ldx, a.bsx, a.ldy, a.bsy = x.ld, x.bs, y.ld, y.bs
+        a.B, a.T_in, a.Ci, a.Co, a.ks, a.dil, a.stride, a.pad = x.B, x.T, cw.Ci, cw.Co, cw.ks, dil, stride, pad
+        assert x.C == cw.Ci, (what, x.C, cw.Ci)
+        if cw.ups:
+            a.T_out = x.T + 1
+            a.ups, a.ups_pad, a.T_final, a.refl = cw.ups, ups_pad, T_final, refl
+            a.pad = 1
+        else:
+            a.T_out = T_out if T_out is not None else (x.T + 2 * pad - dil * (cw.ks - 1) - 1) // stride + 1
+        a.ci_pad, a.co_pad, a.cic = cw.ci_pad, cw.co_pad, cw.cic
+        a.in_dtype, a.out_dtype = x.dt, y.dt
+        if pro is not None:  # AdaIN: (mean, rstd, stat_bs, gb_ptr, gb_bs, beta_off)
+            mean, rstd, stat_bs, gbp, gb_bs, boff = pro
+            a.pro_mode = L.PRO_ADAIN
+            a.pro_mean, a.pro_rstd, a.stat_bs = mean.data_ptr(), rstd.data_ptr(), stat_bs
+            a.pro_gb, a.gb_bs, a.gb_beta_off = gbp, gb_bs, boff
+        a.pro_act, a.pro_slope, a.pro_cscale = pro_act, pro_slope, cscale
+        a.pro_alpha = self._t(pro_alpha).data_ptr() if pro_alpha is not None else None
+        if res is not None:
+            assert res.t.dtype == y.t.dtype
+            a.res, a.ldr, a.bsr = res.ptr, res.ld, (res.bs if res.B > 1 or res.B == y.B else 0)
+        a.res_tdiv = res_tdiv
+        if acc_in is not None:
+            a.acc_in, a.lda, a.bsa = acc_in.ptr, acc_in.ld, acc_in.bs
+        if gate is not None:
+            a.gate, a.gate_bs = gate, gate_bs
+        a.alpha, a.beta, a.epi_act, a.epi_slope = alpha, beta, epi_act, epi_slope
+        self._call(self.lib.stzs_conv1d, a, what)
+        return y
+
+    def stats(self, x: Act, key):
+        """InstanceNorm statistics of x over time -> (mean, rstd, stat_bs)."""
+        Cc = _rup(x.C, 8)
+        mean = self.buf(key + ".m", (x.B, Cc), torch.float32)
+        rstd = self.buf(key + ".r", (x.B, Cc), torch.float32)
+        need = self.lib.stzs_chan_stats_workspace(x.B, x.T, Cc) // 4 + 1
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=self.device)
+        ws = self._ws
+        a = L.StatsArgs()
+        a.x, a.mean, a.rstd, a.partial = x.ptr, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr()
+        a.ld, a.bs, a.stat_bs, a.B, a.T, a.C, a.dtype, a.eps = x.ld, x.bs, Cc, x.B, x.T, Cc, x.dt, 1e-5
+        self._call(self.lib.stzs_chan_stats, a, "chan_stats")
+        return mean, rstd, Cc
+
+    def rowln(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=1.0, act=L.ACT_NONE, slope=0.0,
+              R=None, what="rowln"):
+        a = L.RowLNArgs()
+        a.x, a.y, a.G, a.Bt = x.ptr, y.ptr, G, Bt
+        a.ldx, a.ldy, a.gs, a.bs = x.ld, y.ld, gs, bs
+        a.R = R if R is not None else x.B * x.T
+        a.C, a.gdiv, a.in_dtype, a.out_dtype, a.act = x.C, gdiv, x.dt, y.dt, act
+        a.gadd, a.eps, a.slope = gadd, 1e-5, slope
+        assert x.ld * x.T == x.bs and y.ld * y.T == y.bs
+        self._call(self.lib.stzs_row_layernorm, a, what)
+
+    def attention(self, q: Act, k: Act, v: Act, o: Act):
+        S = self.spec
+        a = L.AttnArgs()
+        a.q, a.k, a.v, a.o = q.ptr, k.ptr, v.ptr, o.ptr
+        a.ldq, a.ldk, a.ldv, a.ldo = q.ld, k.ld, v.ld, o.ld
+        a.bsq, a.bsk, a.bsv, a.bso = q.bs, k.bs, v.bs, o.bs
+        a.R, a.Lq, a.Lk, a.heads, a.dh = q.B, q.T, k.T, S.dn_heads, S.dn_head_dim
+        self._call(self.lib.stzs_attention, a, "attention")
+
+    def lstm(self, lw, x: Act, y: Act, key):
+        gx = self.act(key + ".gx", x.B, x.T, 8 * lw.H, torch.float32)
+        self.conv(lw.ih, x, gx, what=key + ".ih")
+        a = L.LstmArgs()
+        a.gx, a.whhT, a.y = gx.ptr, self._t(lw.whhT).data_ptr(), y.ptr
+        a.ldg, a.bsg, a.ldy, a.bsy = gx.ld, gx.bs, y.ld, y.bs
+        a.B, a.T, a.H, a.ndir = x.B, x.T, lw.H, 2
+        self._call(self.lib.stzs_lstm, a, key + ".rec")
+        return y
+
+    def copy2d(self, x: Act, y: Act, R, Cn, bsx=None):
+        a = L.CopyArgs()
+        a.x, a.y, a.ldx, a.bsx, a.ldy, a.bsy = x.ptr, y.ptr, x.ld, x.bs if bsx is None else bsx, y.ld, y.bs
+        a.B, a.R, a.C, a.in_dtype, a.out_dtype = y.B, R, Cn, x.dt, y.dt
+        self._call(self.lib.stzs_copy2d, a, "copy2d")
+
+    def mean_rows(self, x: torch.Tensor, c0, Cn, key):
+        y = self.buf(key, (x.shape[0], Cn), torch.float32)
+        self.launches += 1
+        L.check(self.lib.stzs_mean_rows(x.data_ptr(), y.data_ptr(), x.shape[0], x.shape[1], x.shape[2],
+                                        x.shape[1] * x.shape[2], c0, Cn, Cn, self.stream()), "mean_rows")
+        return y
+
+    # ------------------------------------------------------------------ front ends
+    def text_encode(self, tokens: torch.Tensor) -> Act:
+        """tokens int32 [B, T] (device) -> h_txt bf16 [B, T, d_txt]; HIP (embed + conv + LN)."""
+        S, W = self.spec, self.W
+        B, T = tokens.shape
+        e = self.act("te.e", B, T, S.d_txt)
+        c = self.act("te.c", B, T, S.d_txt)
+        self.launches += 1
+        L.check(self.lib.stzs_embed(tokens.data_ptr(), W.t(W.te_emb).data_ptr(), e.ptr, B, T, S.d_txt, e.ld,
+                                    self.stream()), "embed")
+        for i in range(S.te_layers):
+            self.conv(W.te_conv[i], e, c, pad=S.te_kernel // 2, what=f"te.conv{i}")
+            g, b = W.te_ln[i]
+            self.rowln(c, e, G=W.t(g).data_ptr(), gs=0, Bt=W.t(b).data_ptr(), bs=0, gadd=0.0,
+                       act=L.ACT_LEAKY, slope=0.2, what=f"te.ln{i}")
+        return e
+
+    def prompt_encode(self, ref_wav: torch.Tensor) -> torch.Tensor:
+        """hosted front end (torch fp32): ref wav [B, N] -> codes [B, L_s, code]."""
+        S, P = self.spec, self.fe
+        mel = log_mel(ref_wav.float(), S, self.mel_fb)
+        x = F.leaky_relu(F.conv1d(mel, P["pe.conv0.w"], P["pe.conv0.b"], padding=2), 0.2)
+        x = F.leaky_relu(F.conv1d(x, P["pe.conv1.w"], P["pe.conv1.b"], padding=2), 0.2)
+        x = F.adaptive_avg_pool1d(x, S.L_s).transpose(1, 2)
+        out = self.buf("prompt", (x.shape[0], S.L_s, S.code_dim), torch.float32)
+        torch.addmm(P["pe.proj.b"], x.reshape(-1, x.shape[-1]), P["pe.proj.w"].t(), out=out.view(-1, S.code_dim))
+        return out
+
+    # ------------------------------------------------------------------ (a) style diffusion
+    def sample_style(self, h_txt: Act, prompt: torch.Tensor, eps: torch.Tensor, steps: int,
+                     cfg_scale: float = 1.0) -> torch.Tensor:
+        S, W = self.spec, self.W
+        B, T = h_txt.B, h_txt.T
+        cfg = cfg_scale != 1.0
+        R = 2 * B if cfg else B
+        Ls, d, cd = S.L_s, S.dn_d, S.code_dim
+        Lc = T + Ls
+        # context (once per batch): [ctx_txt(h) ; ctx_prm(prompt | null)]
+        ctx = self.act("dn.ctx", R, Lc, d)
+        # ctx_txt rows: the conv writes T rows per utterance into a buffer of Lc rows per utterance
+        self._conv_rows(W.dn_ctx_txt, h_txt, ctx.t, 0, 0, "dn.ctx_txt")
+        pa = Act(prompt)
+        self._conv_rows(W.dn_ctx_prm, pa, ctx.t, 0, T, "dn.ctx_prm")
+        if cfg:
+            self._conv_rows(W.dn_ctx_txt, h_txt, ctx.t, B, 0, "dn.ctx_txt.u")
+            nul = Act(W.t(W.dn_ctx_null)[None])
+            dst = Act(ctx.t[B:]).rows(0, B)
+            a = L.CopyArgs()
+            a.x, a.y = nul.ptr, dst.t.data_ptr() + T * ctx.ld * 2
+            a.ldx, a.bsx, a.ldy, a.bsy = d, 0, ctx.ld, Lc * ctx.ld
+            a.B, a.R, a.C, a.in_dtype, a.out_dtype = B, Ls, d, L.BF16, L.BF16
+            self._call(self.lib.stzs_copy2d, a, "ctx_null")
+        pm = self.mean_rows(prompt, 0, cd, "dn.pm")
+        pool = self.buf("dn.pool", (R, d), torch.float32)
+        self.conv(W.dn_pool, Act(pm[:, None]), Act(pool[:B, None]), what="dn.pool")
+        if cfg:
+            a = L.CopyArgs()
+            a.x, a.y = W.t(W.dn_pool_null).data_ptr(), pool[B:].data_ptr()
+            a.ldx, a.bsx, a.ldy, a.bsy = d, 0, d, d
+            a.B, a.R, a.C, a.in_dtype, a.out_dtype = B, 1, d, L.F32, L.F32
+            self._call(self.lib.stzs_copy2d, a, "pool_null")
+        kv = []
+        for l, lw in enumerate(W.dn_layers):
+            kvl = self.act(f"dn.kv{l}", R, Lc, 2 * d)
+            self.conv(lw["kv"], ctx, kvl, what=f"dn.kv{l}")
+            kv.append(kvl)
+        # sigma embeddings for all steps
+        sig = sigma_schedule(S, steps)
+        four = np.stack([fourier_features(S, edm_coeffs(S, s)["c_noise"]) for s in sig[:steps]])
+        fo = self.buf(f"dn.four{steps}", (1, steps, S.dn_fourier), torch.float32)
+        fo.copy_(torch.from_numpy(four)[None], non_blocking=False)
+        t0 = self.act("dn.t0", 1, steps, d, torch.float32)
+        temb = self.act("dn.temb", 1, steps, d, torch.float32)
+        self.conv(W.dn_t0, Act(fo), t0, epi_act=L.ACT_SILU, what="dn.t0")
+        self.conv(W.dn_t1, t0, temb, what="dn.t1")
+        # state
+        x = self.buf("dn.x", (R, Ls, cd), torch.float32)
+        N = Ls * cd
+        self.launches += 1
+        L.check(self.lib.stzs_state_init(x.data_ptr(), eps.data_ptr(), B, N, int(cfg), float(sig[0]), self.stream()),
+                "state_init")
+        cb = self.buf("dn.cb", (R, d), torch.bfloat16)
+        mod = self.buf("dn.mod", (R, 6 * d), torch.float32)
+        fmod = self.buf("dn.fmod", (R, 2 * d), torch.float32)
+        modx = self.buf("dn.modx", (S.dn_layers, R, 6 * d), torch.float32)
+        fmodx = self.buf("dn.fmodx", (1, R, 2 * d), torch.float32)
+        h = self.act("dn.h", R, Ls, d, torch.float32)
+        an = self.act("dn.a", R, Ls, d)
+        qkv = self.act("dn.qkv", R, Ls, 3 * d)
+        o = self.act("dn.o", R, Ls, d)
+        q = self.act("dn.q", R, Ls, d)
+        ff = self.act("dn.ff", R, Ls, S.dn_ffn)
+        D = self.act("dn.D", R, Ls, cd, torch.float32)
+        xa = Act(x)
+        pos = Act(W.t(W.dn_pos)[None])
+        fsz = 4
+        for i in range(steps):
+            s0 = sig[i]
+            co = edm_coeffs(S, s0)
+            self.launches += 1
+            L.check(self.lib.stzs_dn_cond(pool.data_ptr(), temb.t.data_ptr() + i * d * fsz, cb.data_ptr(), R, d,
+                                          self.stream()), "dn_cond")
+            self.conv(W.dn_ada, Act(cb[:, None]), Act(mod[:, None]), what="dn.ada")
+            self.conv(W.dn_final_ada, Act(cb[:, None]), Act(fmod[:, None]), what="dn.final_ada")
+            self.launches += 2
+            L.check(self.lib.stzs_adaln_expand(mod.data_ptr(), W.t(W.dn_table).data_ptr(), modx.data_ptr(), R, d, 6,
+                                               S.dn_layers, 0b010010, self.stream()), "adaln_expand")
+            L.check(self.lib.stzs_adaln_expand(fmod.data_ptr(), None, fmodx.data_ptr(), R, d, 2, 1, 0b10,
+                                               self.stream()), "adaln_expand.f")
+            self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, what="dn.in")
+            for l, lw in enumerate(W.dn_layers):
+                mb = modx[l].data_ptr()
+                self.rowln(h, an, G=mb + d * fsz, gs=6 * d, Bt=mb, bs=6 * d, gdiv=Ls, gadd=0.0, what="ln1")
+                self.conv(lw["qkv"], an, qkv, what="qkv")
+                self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
+                self.conv(lw["o"], o, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, what="sa_o")
+                self.rowln(h, an, G=W.t(lw["ln_g"]).data_ptr(), gs=0, Bt=W.t(lw["ln_b"]).data_ptr(), bs=0,
+                           gadd=0.0, what="ca_ln")
+                self.conv(lw["q"], an, q, what="ca_q")
+                self.attention(q, kv[l].sl(0, d), kv[l].sl(d, d), o)
+                self.conv(lw["co"], o, h, res=h, what="ca_o")
+                self.rowln(h, an, G=mb + 4 * d * fsz, gs=6 * d, Bt=mb + 3 * d * fsz, bs=6 * d, gdiv=Ls, gadd=0.0,
+                           what="ln2")
+                self.conv(lw["ff1"], an, ff, epi_act=L.ACT_GELU, what="ff1")
+                self.conv(lw["ff2"], ff, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, what="ff2")
+            fb = fmodx.data_ptr()
+            self.rowln(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls, gadd=0.0, what="lnf")
+            self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], what="dn.out")
+            self.launches += 1
+            L.check(self.lib.stzs_cfg_euler(x.data_ptr(), D.t.data_ptr(), B, N, int(cfg), float(cfg_scale),
+                                            float(s0), float(sig[i + 1] - s0), self.stream()), "cfg_euler")
+        return x[:B]
+
+    def _conv_rows(self, cw, x: Act, dst: torch.Tensor, b0, t0, what):
+        """linear over x [B, T, C] written to dst[b0 + b, t0 + t, :] (dst rows have a larger T)."""
+        B, T = x.B, x.T
+        y = Act(dst[b0:b0 + B])
+        a_y = Act(y.t, 0, cw.Co)
+        # shift the output base by t0 rows; the batch stride stays that of dst
+        view = _OffsetAct(a_y, t0 * dst.shape[2])
+        self.conv(cw, x, view, T_out=T, what=what)
+
+    # ------------------------------------------------------------------ (b) prosody predictor
+    def predict_prosody(self, h_txt: Act, codes: torch.Tensor, durations=None):
+        """durations: optional int tensor [B, T_txt] (host or device).  Returns dict of device tensors."""
+        S, W = self.spec, self.W
+        B, T = h_txt.B, h_txt.T
+        pin = S.pr_in
+        xin = self.act("pr.xin", B, T, pin)
+        a = L.PrPrepArgs()
+        a.codes, a.h, a.y = codes.data_ptr(), h_txt.ptr, xin.ptr
+        a.ldc, a.bsc, a.ldh, a.bsh, a.ldy, a.bsy = codes.shape[2], codes.shape[1] * codes.shape[2], h_txt.ld, \
+            h_txt.bs, xin.ld, xin.bs
+        a.B, a.L, a.T, a.c0, a.Cs, a.Ch, a.yc0 = B, S.L_s, T, S.style_ac, S.style_pr, S.d_txt, S.d_txt
+        self._call(self.lib.stzs_predictor_prep, a, "pr_prep")
+        hout = self.act("pr.hout", B, T, S.pr_hid)
+        gb = self.act("pr.gb", B, T, 2 * S.pr_hid, torch.float32)
+        for i in range(S.pr_layers):
+            self.lstm(W.pr_de[i], xin, hout, f"pr.de{i}")
+            self.conv(W.pr_aln[i], xin.sl(S.d_txt, S.style_pr), gb, what=f"pr.aln{i}")
+            self.rowln(hout, Act(xin.t, 0, S.pr_hid), G=gb.ptr, gs=2 * S.pr_hid, Bt=gb.ptr + S.pr_hid * 4,
+                       bs=2 * S.pr_hid, gdiv=1, gadd=1.0, what=f"pr.adaln{i}")
+        d = xin
+        hd = self.act("pr.hd", B, T, S.pr_hid)
+        self.lstm(W.pr_dur_lstm, d, hd, "pr.dur_lstm")
+        logits = self.act("pr.logits", B, T, S.dur_bins, torch.float32)
+        self.conv(W.pr_dur_proj, hd, Act(logits.t, 0, S.dur_bins), what="pr.dur_proj")
+        dur = self.buf("pr.dur", (B, T), torch.int32)
+        dsum = self.buf("pr.dsum", (B, T), torch.float32)
+        ov = None
+        if durations is not None:
+            ov = self.buf("pr.dur_ov", (B, T), torch.int32)
+            if durations.device.type == "cpu":
+                ov.copy_(durations.to(torch.int32))
+            elif durations.data_ptr() != ov.data_ptr():
+                ov.copy_(durations)
+        a = L.DurArgs()
+        a.logits, a.override_dur, a.dur, a.dsum = logits.ptr, (ov.data_ptr() if ov is not None else None), \
+            dur.data_ptr(), dsum.data_ptr()
+        a.ldl, a.bsl, a.B, a.T, a.nbins = logits.ld, logits.bs, B, T, S.dur_bins
+        self._call(self.lib.stzs_durations, a, "durations")
+        if durations is not None and durations.device.type == "cpu":
+            tot = durations.to(torch.int64).sum(1)
+        else:
+            tot = dur.to(torch.int64).sum(1).cpu()  # host sync: frame count sizes every later buffer
+        assert int(tot.min()) == int(tot.max()), "one batch must share its total frame count (§8(f) bucketing)"
+        T40 = int(tot[0])
+        idx = self.buf("pr.idx", (B, T40), torch.int32)
+        total = self.buf("pr.total", (B,), torch.int32)
+        a = L.AlignArgs()
+        a.dur, a.idx, a.total, a.B, a.T, a.T40 = dur.data_ptr(), idx.data_ptr(), total.data_ptr(), B, T, T40
+        self._call(self.lib.stzs_alignment, a, "alignment")
+        en = self.act("pr.en", B, T40, pin)
+        self.gather(d, idx, en, pin)
+        enc_in = self.act("dec.enc_in", B, T40, S.d_txt + 2)
+        self.gather(h_txt, idx, enc_in, S.d_txt)
+        xs = self.act("pr.xs", B, T40, S.pr_hid)
+        self.lstm(W.pr_shared, en, xs, "pr.shared")
+        sg = self.mean_rows(codes, S.style_ac, S.style_pr, "pr.sg")
+        ng = W.pr_norm
+        gbp = self.buf("pr.gbn", (B, ng.total), torch.float32)
+        self.conv(ng.lin, Act(sg[:, None]), Act(gbp[:, None]), what="pr.norms")
+        T80 = 2 * T40
+        F0 = self.buf("pr.F0", (B, T80, 1), torch.float32)
+        Nn = self.buf("pr.N", (B, T80, 1), torch.float32)
+        c0, c1, c2 = S.f0n_ch
+        for br, out in (("f0", F0), ("n", Nn)):
+            y0 = self.act(f"pr.{br}.y0", B, T40, c0)
+            y1 = self.act(f"pr.{br}.y1", B, T80, c1)
+            y2 = self.act(f"pr.{br}.y2", B, T80, c2)
+            self.blk(W.pr_blk[f"pr.{br}0"], xs, y0, ng, gbp, f"pr.{br}0")
+            self.blk(W.pr_blk[f"pr.{br}1"], y0, y1, ng, gbp, f"pr.{br}1")
+            self.blk(W.pr_blk[f"pr.{br}2"], y1, y2, ng, gbp, f"pr.{br}2")
+            self.conv(W.pr_blk[f"pr.{br}_proj"], y2, Act(out, 0, 1), what=f"pr.{br}_proj")
+        return dict(dur=dur, dsum=dsum, logits=logits, idx=idx, T40=T40, en=en, asr_buf=enc_in, d=d,
+                    F0=F0[:, :, 0], N=Nn[:, :, 0])
+
+    def gather(self, x: Act, idx, y: Act, Cn):
+        a = L.GatherArgs()
+        a.x, a.idx, a.y = x.t.data_ptr(), idx.data_ptr(), y.t.data_ptr()
+        a.ldx, a.bsx, a.ldy, a.bsy = x.ld, x.bs, y.ld, y.bs
+        a.B, a.Tsrc, a.Tdst, a.C, a.xc0, a.yc0, a.dtype = x.B, x.T, y.T, Cn, x.c0, y.c0, x.dt
+        self._call(self.lib.stzs_gather_rows, a, "gather")
+
+    def blk(self, bw, x: Act, out: Act, ng, gb: torch.Tensor, key):
+        """AdainResBlk1d: out = (conv2(act(AdaIN(conv1(up(act(AdaIN(x))))))) + sc(x)) / sqrt 2."""
+        B, T = x.B, x.T
+        off1, c1 = ng.offsets[bw.name + ".norm1"]
+        off2, c2 = ng.offsets[bw.name + ".norm2"]
+        gbase, gbs = gb.data_ptr(), ng.total
+        m1, r1, sb1 = self.stats(x, key + ".s1")
+        To = 2 * T if bw.up else T
+        r = self.act(key + ".r", B, To, bw.dout)
+        if bw.up:
+            u = self.act(key + ".u", B, To, bw.din)
+            a = L.DwupArgs()
+            a.x, a.y, a.mean, a.rstd, a.gb = x.ptr, u.ptr, m1.data_ptr(), r1.data_ptr(), gbase + off1 * 4
+            a.w, a.wb = self.W.t(bw.pool_w).data_ptr(), self.W.t(bw.pool_b).data_ptr()
+            a.ldx, a.bsx, a.ldy, a.bsy, a.stat_bs, a.gb_bs, a.gb_beta_off = x.ld, x.bs, u.ld, u.bs, sb1, gbs, c1
+            a.B, a.T, a.C, a.slope = B, T, bw.din, 0.2
+            self._call(self.lib.stzs_adain_dwup, a, key + ".dwup")
+            self.conv(bw.conv1, u, r, pad=1, what=key + ".conv1")
+        else:
+            self.conv(bw.conv1, x, r, pad=1, pro=(m1, r1, sb1, gbase + off1 * 4, gbs, c1), pro_act=L.ACT_LEAKY,
+                      pro_slope=0.2, what=key + ".conv1")
+        m2, r2, sb2 = self.stats(r, key + ".s2")
+        if bw.sc is not None:
+            scb = self.act(key + ".sc", B, T, bw.dout)
+            self.conv(bw.sc, x, scb, what=key + ".sc")
+            res = scb
+        else:
+            res = x
+        self.conv(bw.conv2, r, out, pad=1, pro=(m2, r2, sb2, gbase + off2 * 4, gbs, c2), pro_act=L.ACT_LEAKY,
+                  pro_slope=0.2, res=res, res_tdiv=2 if bw.up else 1, alpha=1.0 / math.sqrt(2.0), what=key + ".conv2")
+        return out
+
+    # ------------------------------------------------------------------ (c) decoder
+    def decode(self, pro: dict, codes: torch.Tensor, seeds) -> torch.Tensor:
+        S, W = self.spec, self.W
+        enc_in, F0, Nn, T40 = pro["asr_buf"], pro["F0"], pro["N"], pro["T40"]
+        B = enc_in.B
+        T80 = 2 * T40
+        sa = self.mean_rows(codes, 0, S.style_ac, "dec.sa")
+        ng = W.dec_norm
+        gbd = self.buf("dec.gbn", (B, ng.total), torch.float32)
+        self.conv(ng.lin, Act(sa[:, None]), Act(gbd[:, None]), what="dec.norms")
+        dcat = S.dec_enc + 2 + S.dec_asr_res
+        cats = [self.act("dec.catA", B, T40, dcat), self.act("dec.catB", B, T40, dcat)]
+        cF, cN = S.dec_enc + S.dec_asr_res, S.dec_enc + S.dec_asr_res + 1
+        for j, cat in enumerate(cats):
+            a = L.F0nArgs()
+            a.f0, a.n = F0.data_ptr(), Nn.data_ptr()
+            a.wf, a.wn = W.t(W.dec_f0).data_ptr(), W.t(W.dec_n).data_ptr()
+            a.y0, a.y1 = cat.t.data_ptr(), (enc_in.t.data_ptr() if j == 0 else None)
+            a.ldf, a.ldy0, a.bsy0, a.ldy1, a.bsy1 = F0.stride(0), cat.ld, cat.bs, enc_in.ld, enc_in.bs
+            a.B, a.T80, a.cf0, a.cn0, a.cf1, a.cn1 = B, T80, cF, cN, S.d_txt, S.d_txt + 1
+            self._call(self.lib.stzs_f0n_down, a, "f0n_down")
+            self.conv(W.dec_asr_res, Act(enc_in.t, 0, S.d_txt), cat.sl(S.dec_enc, S.dec_asr_res), what="asr_res")
+        self.blk(W.dec_blk["dec.encode"], Act(enc_in.t, 0, S.d_txt + 2), cats[0].sl(0, S.dec_enc), ng, gbd, "dec.encode")
+        src = 0
+        for i in range(3):
+            self.blk(W.dec_blk[f"dec.decode{i}"], Act(cats[src].t, 0, dcat), cats[1 - src].sl(0, S.dec_enc), ng, gbd,
+                     f"dec.decode{i}")
+            src = 1 - src
+        gen_in = self.act("dec.gen_in", B, T80, S.dec_out)
+        self.blk(W.dec_blk["dec.decode3"], Act(cats[src].t, 0, dcat), gen_in, ng, gbd, "dec.decode3")
+        return self.generator(gen_in, F0, seeds, gbd)
+
+    def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None):
+        S, W = self.spec, self.W
+        B, T80 = x.B, x.T
+        ng = W.dec_norm
+        N = T80 * S.hop
+        Tf = N // S.istft_hop + 1
+        nh = S.harmonic_num + 1
+        sd = self.buf("gen.seeds", (B,), torch.int32)
+        if isinstance(seeds, torch.Tensor) and seeds.device.type != "cpu":
+            sd.copy_(seeds.to(torch.int32))
+        else:
+            sd.copy_(torch.as_tensor(np.asarray(seeds, dtype=np.uint32).astype(np.int64)).to(torch.int32))
+        pref = self.buf("gen.pref", (B, nh, T80), torch.float32)
+        har = self.act("gen.har", B, Tf, S.har_ch)
+        a = L.SourceArgs()
+        a.f0, a.seeds, a.merge_w, a.prefix, a.har = F0.data_ptr(), sd.data_ptr(), W.t(W.src_merge).data_ptr(), \
+            pref.data_ptr(), har.ptr
+        a.ldf, a.ldh, a.bsh = F0.stride(0), har.ld, har.bs
+        a.B, a.T80, a.hop, a.n_fft, a.hop_s, a.nh = B, T80, S.hop, S.n_fft, S.istft_hop, nh
+        a.sr, a.sine_amp, a.noise_std, a.voiced_thr = float(S.sr), S.sine_amp, S.noise_std, S.voiced_threshold
+        self._call(self.lib.stzs_harmonic_source, a, "harmonic_source")
+        if trace is not None:
+            trace["har"] = har
+        n_up = len(S.up_rates)
+        Tcur = T80
+        for i, (r, k) in enumerate(zip(S.up_rates, S.up_kernels)):
+            c = S.gen_ch[i]
+            last = i == n_up - 1
+            Tn = Tcur * r + (1 if last else 0)
+            xsrc = self.act(f"gen.xsrc{i}", B, Tn, c)
+            if not last:
+                sf0 = int(np.prod(S.up_rates[i + 1:]))
+                self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, stride=sf0, pad=(sf0 + 1) // 2,
+                          what=f"noise_conv{i}")
+            else:
+                self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, what=f"noise_conv{i}")
+            xu = self.act(f"gen.x{i}", B, Tn, c)
+            self.conv(W.ups[i], x, xu, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=(k - r) // 2, T_final=Tcur * r,
+                      refl=1 if last else 0, res=xsrc, what=f"ups{i}")
+            if trace is not None:
+                trace[f"mrf_in{i}"] = xu
+            x = self.mrf(xu, i, gbd, ng)
+            if trace is not None:
+                trace[f"mrf_out{i}"] = x
+            Tcur = Tn
+        post = self.act("gen.post", B, Tcur, S.har_ch, torch.float32)
+        self.conv(W.conv_post, x, Act(post.t, 0, S.har_ch), pad=3, pro_act=L.ACT_LEAKY, pro_slope=0.01,
+                  what="conv_post")
+        if trace is not None:
+            trace["post"] = post
+        Nout = (Tcur - 1) * S.istft_hop
+        wav = self.buf("gen.wav", (B, Nout), torch.float32)
+        a = L.IstftArgs()
+        a.post, a.wav, a.ldp, a.bsp, a.bsw = post.ptr, wav.data_ptr(), post.ld, post.bs, Nout
+        a.B, a.Tf, a.n_fft, a.hop_s = B, Tcur, S.n_fft, S.istft_hop
+        self._call(self.lib.stzs_istft, a, "istft")
+        return wav
+
+    def mrf(self, x: Act, i, gbd, ng):
+        S, W = self.spec, self.W
+        B, T, c = x.B, x.T, x.C
+        gbase, gbs = gbd.data_ptr(), ng.total
+        xs = self.act(f"gen.xs{i}", B, T, c)
+        bufA = self.act(f"gen.ba{i}", B, T, c)
+        bufB = self.act(f"gen.bb{i}", B, T, c)
+        t1 = self.act(f"gen.t1_{i}", B, T, c)
+        mx, rx, sb = self.stats(x, f"gen.sx{i}")
+        nk = len(S.rb_kernels)
+        for j, res in enumerate(W.rb[i]):
+            cur, cm, cr = x, mx, rx
+            for m, lw in enumerate(res):
+                k, dil = lw["k"], lw["dil"]
+                o1, c1 = ng.offsets[lw["n1"]]
+                o2, c2 = ng.offsets[lw["n2"]]
+                self.conv(lw["c1"], cur, t1, pad=dil * (k - 1) // 2, dil=dil, pro=(cm, cr, sb, gbase + o1 * 4, gbs, c1),
+                          pro_act=L.ACT_SNAKE, pro_alpha=lw["a1"], what="rb.c1")
+                tm, tr, _ = self.stats(t1, f"gen.st{i}")
+                last = m == len(res) - 1
+                out = xs if last else (bufA if cur is not bufA else bufB)
+                self.conv(lw["c2"], t1, out, pad=(k - 1) // 2, pro=(tm, tr, sb, gbase + o2 * 4, gbs, c2),
+                          pro_act=L.ACT_SNAKE, pro_alpha=lw["a2"], res=cur, alpha=(1.0 / nk) if last else 1.0,
+                          acc_in=(xs if (last and j > 0) else None), beta=1.0, what="rb.c2")
+                if not last:
+                    cm, cr, _ = self.stats(out, f"gen.sc{i}.{m % 2}")
+                    cur = out
+        return xs
+
+    # ------------------------------------------------------------------ end to end
+    def synth(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None, codes=None):
+        """tokens int [B, T_txt]; ref_wav fp32 [B|1, N]; noise fp32 [B, L_s, code]; durations int [B, T_txt]
+        (host tensor: no device sync); seeds: per-utterance source-noise seeds.  -> dict(wav=[B, 600*T40])"""
+        S = self.spec
+        dev = self.device
+        tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
+        B = tokens.shape[0]
+        h = self.text_encode(tokens)
+        prompt = self.prompt_encode(ref_wav.to(dev))
+        if prompt.shape[0] == 1 and B > 1:
+            pe = self.buf("prompt.bc", (B, S.L_s, S.code_dim), torch.float32)
+            pe.copy_(prompt.expand(B, -1, -1))
+            prompt = pe
+        if codes is None:
+            eps = noise.to(dev, torch.float32)
+            codes = self.sample_style(h, prompt, eps, steps, cfg_scale)
+        pro = self.predict_prosody(h, codes, durations)
+        seeds = list(range(B)) if seeds is None else seeds
+        wav = self.decode(pro, codes, seeds)
+        return dict(wav=wav, codes=codes, h_txt=h, prompt=prompt, **pro)
+
+
+class _OffsetAct(Act):
+    """Act whose base pointer is shifted by `off` elements (writes into a row window of a larger buffer)."""
+
+    def __init__(self, base: Act, off: int):
+        super().__init__(base.t, base.c0, base.C)
+        self._off = off
+
+    @property
+    def ptr(self):
+        return self.t.data_ptr() + (self.c0 + self._off) * self.t.element_size()

@@ -1,0 +1,269 @@
+"""Weight packing: torch-native parameter dict -> one contiguous device arena of kernel layouts.
+
+Layouts (see include/stzs.h):
+  * conv / linear : bf16 [ks][co_pad][ci_pad]  (ci chunk cic = 32|64, co padded to the tile)
+  * ConvTranspose1d(k = 2s): polyphase bf16 [2][s*Co][ci_pad]  W'[0][p*Co+co] = W[:, co, p+s],
+                             W'[1][p*Co+co] = W[:, co, p]
+  * LSTM          : W_ih of both directions as one linear [8H, in] with bias b_ih + b_hh, and
+                    W_hh^T fp32 [2][H][4H]
+  * AdaIN fcs     : every norm fc of a stage concatenated into ONE linear (style -> sum 2C), so
+                    all gamma/beta of a stage come from one GEMM per utterance batch
+The arena is a single uint8 tensor (256-B aligned sub-buffers) so that multi-GPU runs move all
+weights with ONE RCCL broadcast; its layout depends only on the spec, so every
+rank can build the views before receiving the bytes.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from .spec import Spec
+
+ALIGN = 256
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class ConvW:
+    w: object            # name in arena (resolved to a tensor view)
+    b: Optional[object]
+    Ci: int
+    Co: int
+    ks: int
+    ci_pad: int
+    co_pad: int
+    cic: int
+    ups: int = 0
+
+
+class Arena:
+    """Collects CPU tensors, lays them out in one buffer, uploads once."""
+
+    def __init__(self):
+        self.items: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        self.views = {}
+        self.buf = None
+
+    def add(self, name, t: torch.Tensor):
+        assert name not in self.items, name
+        self.items[name] = t.contiguous()
+        return name
+
+    def layout(self):
+        off = 0
+        lay = OrderedDict()
+        for k, t in self.items.items():
+            nb = t.numel() * t.element_size()
+            lay[k] = (off, nb)
+            off = _rup(off + nb, ALIGN)
+        return lay, off
+
+    def finalize(self, device, fill=True):
+        lay, total = self.layout()
+        host = torch.zeros(total, dtype=torch.uint8)
+        if fill:
+            for k, t in self.items.items():
+                o, nb = lay[k]
+                host[o:o + nb] = t.reshape(-1).view(torch.uint8)
+        self.buf = host.to(device)
+        for k, t in self.items.items():
+            o, nb = lay[k]
+            self.views[k] = self.buf[o:o + nb].view(t.dtype).view(t.shape)
+        self.items = OrderedDict((k, None) for k in self.items)  # drop host copies
+        return self
+
+    def __getitem__(self, k):
+        return self.views[k]
+
+
+def pack_conv(A: Arena, name, w, b=None, ups=0) -> ConvW:
+    """w: Conv1d [Co, Ci, k] / Linear [Co, Ci] / ConvTranspose1d [Ci, Co, 2*ups] (ups > 0)."""
+    if ups:
+        Ci, Co, k = w.shape
+        assert k == 2 * ups
+        ncol = ups * Co
+        wk = torch.empty(2, ncol, Ci)
+        for p in range(ups):
+            wk[0, p * Co:(p + 1) * Co] = w[:, :, p + ups].t()
+            wk[1, p * Co:(p + 1) * Co] = w[:, :, p].t()
+        ks = 2
+    else:
+        if w.dim() == 2:
+            w = w[:, :, None]
+        Co, Ci, ks = w.shape
+        ncol = Co
+        wk = w.permute(2, 0, 1)
+    cic = 32 if Ci <= 32 else 64
+    ci_pad = _rup(Ci, cic)
+    co_pad = _rup(ncol, 128) if ncol >= 128 else _rup(ncol, 64)
+    wp = torch.zeros(ks, co_pad, ci_pad)
+    wp[:, :ncol, :Ci] = wk
+    wn = A.add(name + ".wpk", wp.to(torch.bfloat16))
+    bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
+    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups)
+
+
+@dataclass
+class NormGroup:
+    """all AdaIN fc layers of one stage, packed as one linear; offsets per norm name."""
+    lin: ConvW
+    offsets: dict
+    total: int
+
+
+def pack_norm_group(A: Arena, name, P, norm_names, style_dim) -> NormGroup:
+    ws, bs, offs, off = [], [], {}, 0
+    for n in norm_names:
+        w, b = P[n + ".w"], P[n + ".b"]
+        offs[n] = (off, w.shape[0] // 2)
+        off += w.shape[0]
+        ws.append(w)
+        bs.append(b)
+    W = torch.cat(ws, 0)
+    Bv = torch.cat(bs, 0)
+    return NormGroup(pack_conv(A, name, W, Bv), offs, off)
+
+
+@dataclass
+class LstmW:
+    ih: ConvW
+    whhT: str
+    H: int
+
+
+def pack_lstm(A: Arena, name, P) -> LstmW:
+    H = P[name + ".w_hh"].shape[1]
+    wih = torch.cat([P[name + ".w_ih"], P[name + ".w_ih_rev"]], 0)
+    bias = torch.cat([P[name + ".b_ih"] + P[name + ".b_hh"], P[name + ".b_ih_rev"] + P[name + ".b_hh_rev"]], 0)
+    ih = pack_conv(A, name + ".ih", wih, bias)
+    whhT = torch.stack([P[name + ".w_hh"].t(), P[name + ".w_hh_rev"].t()], 0).contiguous().float()
+    return LstmW(ih, A.add(name + ".whhT", whhT), H)
+
+
+def blk_norms(prefix):
+    return [prefix + ".norm1", prefix + ".norm2"]
+
+
+@dataclass
+class BlkW:
+    """AdainResBlk1d"""
+    name: str
+    din: int
+    dout: int
+    up: bool
+    conv1: ConvW
+    conv2: ConvW
+    sc: Optional[ConvW]
+    pool_w: Optional[str]
+    pool_b: Optional[str]
+
+
+def pack_blk(A: Arena, P, name, up=False) -> BlkW:
+    c1 = pack_conv(A, name + ".conv1", P[name + ".conv1.w"], P[name + ".conv1.b"])
+    c2 = pack_conv(A, name + ".conv2", P[name + ".conv2.w"], P[name + ".conv2.b"])
+    sc = pack_conv(A, name + ".sc", P[name + ".sc.w"]) if name + ".sc.w" in P else None
+    pw = pb = None
+    if up:
+        pw = A.add(name + ".poolw", P[name + ".pool.w"].reshape(-1, 3).float())
+        pb = A.add(name + ".poolb", P[name + ".pool.b"].float())
+    din = P[name + ".conv1.w"].shape[1]
+    dout = P[name + ".conv1.w"].shape[0]
+    return BlkW(name, din, dout, up, c1, c2, sc, pw, pb)
+
+
+class PackedModel:
+    """All hot-path weights of spec v0 in kernel layouts, resident in one device arena."""
+
+    def __init__(self, spec: Spec, P, device, fill=True):
+        S = self.spec = spec
+        A = self.arena = Arena()
+        d = S.dn_d
+        # --- text encoder ---
+        self.te_emb = A.add("te.emb", P["te.emb"].float())
+        self.te_conv = [pack_conv(A, f"te.conv{i}", P[f"te.conv{i}.w"], P[f"te.conv{i}.b"]) for i in range(S.te_layers)]
+        self.te_ln = [(A.add(f"te.ln{i}.g", P[f"te.ln{i}.g"]), A.add(f"te.ln{i}.b", P[f"te.ln{i}.b"])) for i in range(S.te_layers)]
+        # --- denoiser ---
+        L = lambda n: pack_conv(A, n, P[n + ".w"], P[n + ".b"])
+        self.dn_in = L("dn.in_proj")
+        self.dn_pos = A.add("dn.pos", P["dn.pos"].float())
+        self.dn_t0, self.dn_t1 = L("dn.t_mlp0"), L("dn.t_mlp1")
+        self.dn_pool = L("dn.pool_proj")
+        self.dn_ctx_txt, self.dn_ctx_prm = L("dn.ctx_txt"), L("dn.ctx_prm")
+        self.dn_ada = L("dn.ada")
+        self.dn_table = A.add("dn.ada_table", P["dn.ada_table"].float())
+        self.dn_final_ada = L("dn.final_ada")
+        self.dn_out = L("dn.out")
+        # constant unconditional-branch context: null codes through ctx_prm / pool_proj (fp32, once)
+        null = P["dn.null_codes"].float()
+        ctx_null = null @ P["dn.ctx_prm.w"].t() + P["dn.ctx_prm.b"]
+        pool_null = null.mean(0) @ P["dn.pool_proj.w"].t() + P["dn.pool_proj.b"]
+        self.dn_ctx_null = A.add("dn.ctx_null", ctx_null.to(torch.bfloat16))
+        self.dn_pool_null = A.add("dn.pool_null", pool_null.float())
+        self.dn_layers = []
+        for l in range(S.dn_layers):
+            p = f"dn.l{l}"
+            self.dn_layers.append(dict(
+                qkv=L(p + ".sa_qkv"), o=L(p + ".sa_o"), q=L(p + ".ca_q"), kv=L(p + ".ca_kv"), co=L(p + ".ca_o"),
+                ff1=L(p + ".ff1"), ff2=L(p + ".ff2"),
+                ln_g=A.add(p + ".ca_ln.g", P[p + ".ca_ln.g"]), ln_b=A.add(p + ".ca_ln.b", P[p + ".ca_ln.b"])))
+        # --- predictor ---
+        self.pr_de = [pack_lstm(A, f"pr.de{i}", P) for i in range(S.pr_layers)]
+        self.pr_aln = [L(f"pr.de{i}.aln") for i in range(S.pr_layers)]
+        self.pr_dur_lstm = pack_lstm(A, "pr.dur_lstm", P)
+        self.pr_dur_proj = L("pr.dur_proj")
+        self.pr_shared = pack_lstm(A, "pr.shared", P)
+        pr_norms = []
+        self.pr_blk = {}
+        for br in ("f0", "n"):
+            for i in range(3):
+                nm = f"pr.{br}{i}"
+                self.pr_blk[nm] = pack_blk(A, P, nm, up=(i == 1))
+                pr_norms += blk_norms(nm)
+            self.pr_blk[f"pr.{br}_proj"] = pack_conv(A, f"pr.{br}_proj", P[f"pr.{br}_proj.w"], P[f"pr.{br}_proj.b"])
+        self.pr_norm = pack_norm_group(A, "pr.norms", P, pr_norms, S.style_pr)
+        # --- decoder ---
+        self.dec_f0 = A.add("dec.f0c", torch.cat([P["dec.f0_conv.w"].reshape(-1), P["dec.f0_conv.b"]]).float())
+        self.dec_n = A.add("dec.nc", torch.cat([P["dec.n_conv.w"].reshape(-1), P["dec.n_conv.b"]]).float())
+        self.dec_asr_res = pack_conv(A, "dec.asr_res", P["dec.asr_res.w"], P["dec.asr_res.b"])
+        dec_norms = []
+        self.dec_blk = {}
+        for nm, up in [("dec.encode", False), ("dec.decode0", False), ("dec.decode1", False),
+                       ("dec.decode2", False), ("dec.decode3", True)]:
+            self.dec_blk[nm] = pack_blk(A, P, nm, up=up)
+            dec_norms += blk_norms(nm)
+        self.src_merge = A.add("gen.src_merge", torch.cat([P["gen.src_merge.w"].reshape(-1), P["gen.src_merge.b"]]).float())
+        self.noise_conv, self.ups, self.rb = [], [], []
+        for i, (r, k) in enumerate(zip(S.up_rates, S.up_kernels)):
+            self.noise_conv.append(pack_conv(A, f"gen.noise_conv{i}", P[f"gen.noise_conv{i}.w"], P[f"gen.noise_conv{i}.b"]))
+            self.ups.append(pack_conv(A, f"gen.ups{i}", P[f"gen.ups{i}.w"], P[f"gen.ups{i}.b"], ups=r))
+            stage = []
+            for j, kr in enumerate(S.rb_kernels):
+                res = []
+                for m, dil in enumerate(S.rb_dils):
+                    p = f"gen.rb{i}.{j}.{m}"
+                    res.append(dict(
+                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"]),
+                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"]),
+                        a1=A.add(p + ".a1", P[p + ".alpha1"].float()), a2=A.add(p + ".a2", P[p + ".alpha2"].float()),
+                        n1=p + ".n1", n2=p + ".n2", k=kr, dil=dil))
+                    dec_norms += [p + ".n1", p + ".n2"]
+                stage.append(res)
+            self.rb.append(stage)
+        self.conv_post = pack_conv(A, "gen.conv_post", P["gen.conv_post.w"], P["gen.conv_post.b"])
+        self.dec_norm = pack_norm_group(A, "dec.norms", P, dec_norms, S.style_ac)
+        A.finalize(device, fill=fill)
+        self.device = device
+
+    def t(self, name):
+        return self.arena[name]
+
+    @property
+    def nbytes(self):
+        return self.arena.buf.numel()

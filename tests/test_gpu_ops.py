@@ -1,0 +1,305 @@
+"""Kernel-level parity: each HIP op (through the C-ABI) against a plain-torch fp32 restatement of
+the op on identical bf16-representable inputs.  Tolerances are stated per test."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from refops import bf, conv_ref, convT_ref, max_rel, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(gpu_device, tiny, tiny_params):
+    from stzs.engine import StyleTTSZS
+    return StyleTTSZS(tiny, tiny_params, device=gpu_device)
+
+
+def _pack(w, b, ups=0):
+    from stzs.weights import Arena, pack_conv
+    A = Arena()
+    cw = pack_conv(A, "t", w, b, ups=ups)
+    A.finalize("cuda:0")
+    cw.w = A[cw.w]
+    cw.b = A[cw.b] if cw.b is not None else None
+    return cw, A
+
+
+def _act(t, C=None):
+    from stzs.engine import Act
+    return Act(t, 0, t.shape[-1] if C is None else C)
+
+
+def _dev_ntc(x, ld, dtype=torch.bfloat16):
+    B, T, Cc = x.shape
+    t = torch.zeros(B, T, ld, dtype=dtype, device="cuda:0")
+    t[:, :, :Cc] = x.to(dtype).cuda()
+    return t
+
+
+CONV_CASES = [
+    # B, T, Ci, Co, k, dil, stride
+    (2, 300, 96, 80, 3, 1, 1),
+    (2, 1000, 128, 128, 11, 5, 1),
+    (1, 257, 64, 256, 7, 3, 1),
+    (2, 2401, 22, 32, 12, 1, 6),
+    (3, 50, 514, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_adain_snake(eng, case):
+    """AdaIN prologue + Snake + dilated conv + residual/alpha/acc epilogue (MRF c2 form); bf16 out.
+    tolerance: max-abs error <= 1.5e-2 of max|ref| (one bf16 ulp of the output + fp32 reorder)."""
+    B, T, Ci, Co, k, dil, stride = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    pad = dil * (k - 1) // 2 if stride == 1 else (stride + 1) // 2
+    x = bf(torch.randn(B, T, Ci, generator=g))
+    w = torch.randn(Co, Ci, k, generator=g) / math.sqrt(Ci * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    mean = torch.randn(B, Ci, generator=g) * 0.1
+    rstd = torch.rand(B, Ci, generator=g) + 0.5
+    gb = torch.randn(B, 2 * Ci, generator=g) * 0.2
+    alpha = torch.rand(Ci, generator=g) + 0.5
+    T_out = (T + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    res = bf(torch.randn(B, T_out, Co, generator=g))
+    acc = bf(torch.randn(B, T_out, Co, generator=g))
+    sc = (1 + gb[:, :Ci]) * rstd
+    sh = gb[:, Ci:] - mean * sc
+    ref = conv_ref(x, w, b, pad=pad, dil=dil, stride=stride, sc=sc, sh=sh, pro_act="snake", alpha=alpha,
+                   res=res, out_scale=1 / 3, acc_in=acc, beta=1.0)
+    cw, _A = _pack(w, b)
+    ld = (Ci + 7) // 8 * 8
+    xd = _act(_dev_ntc(x, ld), Ci)
+    yd = _act(torch.zeros(B, T_out, Co, dtype=torch.bfloat16, device="cuda:0"))
+    from stzs import _lib as L
+    stat_bs = Ci
+    al = alpha.cuda()
+    gbd = gb.cuda()  # keep alive: the kernel reads it asynchronously
+    eng.conv(cw, xd, yd, pad=pad, dil=dil, stride=stride,
+             pro=(mean.cuda(), rstd.cuda(), stat_bs, gbd.data_ptr(), 2 * Ci, Ci),
+             pro_act=L.ACT_SNAKE, pro_alpha=al, res=_act(res.to(torch.bfloat16).cuda()), alpha=1 / 3,
+             acc_in=_act(acc.to(torch.bfloat16).cuda()), beta=1.0)
+    out = yd.t.float().cpu()
+    e = max_rel(out, ref)
+    print(case, "max_rel", e, "rel_l2", rel_err(out, ref))
+    assert e < 1.5e-2
+
+
+@pytest.mark.parametrize("dt_in,dt_out", [(torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32),
+                                          (torch.bfloat16, torch.float32), (torch.float32, torch.bfloat16)])
+def test_linear_flat(eng, dt_in, dt_out):
+    """ks=1 'flat' GEMM over rows spanning utterances: cscale prologue, GELU, per-(row-group) gate,
+    batch-broadcast residual; tolerance 1e-2 (bf16 out) / 2e-3 (f32 out) of max|ref|."""
+    g = torch.Generator().manual_seed(7)
+    R, Lr, Ci, Co = 6, 50, 512, 384
+    x = bf(torch.randn(R, Lr, Ci, generator=g))
+    w = torch.randn(Co, Ci, generator=g) / math.sqrt(Ci)
+    b = torch.randn(Co, generator=g) * 0.1
+    gate = torch.randn(R, Co, generator=g)
+    pos = bf(torch.randn(1, Lr, Co, generator=g)) if dt_out == torch.bfloat16 else torch.randn(1, Lr, Co, generator=g)
+    cs = 0.7
+    xs = bf(x * cs) if dt_in == torch.bfloat16 else bf(x * cs)
+    ref = F.gelu(xs @ bf(w).t() + b) * gate[:, None, :] + pos
+    cw, _A = _pack(w, b)
+    xd = _act(x.to(dt_in).cuda())
+    yd = _act(torch.zeros(R, Lr, Co, dtype=dt_out, device="cuda:0"))
+    from stzs import _lib as L
+    gated = gate.cuda()
+    eng.conv(cw, xd, yd, cscale=cs, epi_act=L.ACT_GELU, gate=gated.data_ptr(), gate_bs=Co,
+             res=_act(pos.to(dt_out).cuda()))
+    out = yd.t.float().cpu()
+    e = max_rel(out, ref)
+    print(dt_in, dt_out, e)
+    assert e < (1e-2 if dt_out == torch.bfloat16 else 2e-3)
+
+
+@pytest.mark.parametrize("Ci,Co,s,refl", [(64, 32, 10, 0), (32, 16, 6, 1), (512, 256, 10, 0), (256, 128, 6, 1)])
+def test_convtranspose_polyphase(eng, Ci, Co, s, refl):
+    """polyphase ConvTranspose1d(k=2s) + LeakyReLU(0.1) prologue + ReflectionPad(1,0) + residual."""
+    g = torch.Generator().manual_seed(Ci + s)
+    B, T = 2, 40
+    k, pad = 2 * s, s // 2
+    x = bf(torch.randn(B, T, Ci, generator=g))
+    w = torch.randn(Ci, Co, k, generator=g) / math.sqrt(Co * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    Tn = T * s + refl
+    res = bf(torch.randn(B, Tn, Co, generator=g))
+    ref = convT_ref(x, w, b, stride=s, pad=pad, refl=refl, pro_act="leaky", slope=0.1, res=res)
+    cw, _A = _pack(w, b, ups=s)
+    from stzs import _lib as L
+    yd = _act(torch.zeros(B, Tn, Co, dtype=torch.bfloat16, device="cuda:0"))
+    eng.conv(cw, _act(x.to(torch.bfloat16).cuda()), yd, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=pad,
+             T_final=T * s, refl=refl, res=_act(res.to(torch.bfloat16).cuda()))
+    out = yd.t.float().cpu()
+    e = max_rel(out, ref)
+    print(Ci, Co, s, refl, e)
+    assert e < 1.5e-2
+
+
+def test_chan_stats(eng):
+    """InstanceNorm statistics: fp32 partials + fixed-order fp64 combine; 1e-5 relative."""
+    g = torch.Generator().manual_seed(3)
+    B, T, C = 3, 24001, 128
+    x = bf(torch.randn(B, T, C, generator=g) * 2 + 0.5)
+    from stzs.engine import Act
+    m, r, _ = eng.stats(Act(x.to(torch.bfloat16).cuda()), "t.stats")
+    mr = x.double().mean(1)
+    vr = x.double().var(1, unbiased=False)
+    assert max_rel(m.cpu(), mr) < 1e-5
+    assert max_rel(r.cpu(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
+
+
+def test_row_layernorm(eng):
+    g = torch.Generator().manual_seed(4)
+    R, Lr, C = 4, 50, 512
+    x = torch.randn(R * Lr, C, generator=g) * 3 + 1
+    G = torch.randn(R, 3 * C, generator=g)
+    ref = F.layer_norm(x, (C,)).view(R, Lr, C) * G[:, None, C:2 * C] + G[:, None, :C]
+    from stzs.engine import Act
+    xd = Act(x.view(R, Lr, C).cuda())
+    yd = Act(torch.zeros(R, Lr, C, device="cuda:0"))
+    Gd = G.cuda()
+    eng.rowln(xd, yd, G=Gd.data_ptr() + C * 4, gs=3 * C, Bt=Gd.data_ptr(), bs=3 * C, gdiv=Lr, gadd=0.0)
+    assert max_rel(yd.t.cpu(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("Lk", [50, 130, 530])
+def test_attention(eng, Lk):
+    """online-softmax MHA (fp32 math, bf16 I/O); tolerance 1e-2 of max|ref|."""
+    S = eng.spec
+    g = torch.Generator().manual_seed(Lk)
+    R, Lq, D = 3, 50, S.dn_d
+    H, dh = S.dn_heads, S.dn_head_dim
+    q = bf(torch.randn(R, Lq, D, generator=g))
+    k = bf(torch.randn(R, Lk, 2 * D, generator=g))
+    qh = q.view(R, Lq, H, dh).transpose(1, 2)
+    kh = k[..., :D].reshape(R, Lk, H, dh).transpose(1, 2)
+    vh = k[..., D:].reshape(R, Lk, H, dh).transpose(1, 2)
+    ref = (torch.softmax(qh @ kh.transpose(-1, -2) / math.sqrt(dh), -1) @ vh).transpose(1, 2).reshape(R, Lq, D)
+    from stzs.engine import Act
+    kd = Act(k.to(torch.bfloat16).cuda())
+    od = Act(torch.zeros(R, Lq, D, dtype=torch.bfloat16, device="cuda:0"))
+    eng.attention(Act(q.to(torch.bfloat16).cuda()), kd.sl(0, D), kd.sl(D, D), od)
+    assert max_rel(od.t.float().cpu(), ref) < 1e-2
+
+
+def test_lstm(eng, tiny_params):
+    """bidirectional LSTM (GEMM input projection + recurrent kernel) vs torch.nn.LSTM."""
+    from oracle.stzs_ref import bilstm
+    from stzs.engine import Act
+    P = tiny_params
+    g = torch.Generator().manual_seed(5)
+    B, T = 3, 37
+    x = bf(torch.randn(B, T, eng.spec.pr_in, generator=g))
+    ref = bilstm(x, P, "pr.de0")
+    y = Act(torch.zeros(B, T, eng.spec.pr_hid, dtype=torch.bfloat16, device="cuda:0"))
+    eng.lstm(eng.W.pr_de[0], Act(x.to(torch.bfloat16).cuda()), y, "t.lstm")
+    e = max_rel(y.t.float().cpu(), ref)
+    print("lstm", e)
+    assert e < 2e-2
+
+
+def test_durations_alignment_gather_exact(eng):
+    """integer path is bit-exact: round(serial sum sigmoid) clamp>=1, scan, row gather."""
+    from oracle.stzs_ref import alignment_index, durations_from_logits
+    from stzs import _lib as L
+    g = torch.Generator().manual_seed(6)
+    B, T, nb = 4, 33, 50
+    logits = torch.randn(B, T, nb, generator=g) * 2 - 1
+    dur_ref, dsum = durations_from_logits(logits)
+    ld = torch.zeros(B, T, nb, device="cuda:0")
+    ld.copy_(logits)
+    dur = torch.zeros(B, T, dtype=torch.int32, device="cuda:0")
+    ds = torch.zeros(B, T, device="cuda:0")
+    a = L.DurArgs()
+    a.logits, a.override_dur, a.dur, a.dsum = ld.data_ptr(), None, dur.data_ptr(), ds.data_ptr()
+    a.ldl, a.bsl, a.B, a.T, a.nbins = nb, T * nb, B, T, nb
+    eng._call(eng.lib.stzs_durations, a, "dur")
+    tie = ((dsum - dsum.floor() - 0.5).abs() < 1e-4)
+    ok = (dur.cpu() == dur_ref) | tie
+    assert bool(ok.all())
+    # alignment on equal-total durations
+    dd = torch.tensor([[3, 2] * 8 + [1]] * B, dtype=torch.int32)
+    dd[:, -1] = 0
+    dd[:, 0] += 1
+    idx_ref = alignment_index(dd)
+    T40 = idx_ref.shape[1]
+    idx = torch.zeros(B, T40, dtype=torch.int32, device="cuda:0")
+    tot = torch.zeros(B, dtype=torch.int32, device="cuda:0")
+    a = L.AlignArgs()
+    ddd = dd.cuda()
+    a.dur, a.idx, a.total, a.B, a.T, a.T40 = ddd.data_ptr(), idx.data_ptr(), tot.data_ptr(), B, dd.shape[1], T40
+    eng._call(eng.lib.stzs_alignment, a, "align")
+    assert torch.equal(idx.cpu(), idx_ref)
+    assert torch.equal(tot.cpu(), dd.sum(1).int())
+    src = torch.randn(B, dd.shape[1], 64, generator=g).to(torch.bfloat16)
+    from stzs.engine import Act
+    y = Act(torch.zeros(B, T40, 72, dtype=torch.bfloat16, device="cuda:0"), 8, 64)
+    eng.gather(Act(src.cuda()), idx, y, 64)
+    ref = torch.stack([src[b, idx_ref[b].long()] for b in range(B)])
+    assert torch.equal(y.t[:, :, 8:].cpu(), ref)
+
+
+def test_harmonic_source_vs_oracle(eng, tiny_params):
+    """SineGen + counter-RNG noise + merge + STFT (real|imag) vs the oracle; bf16 output."""
+    from oracle.stzs_ref import source_features
+    S = eng.spec
+    g = torch.Generator().manual_seed(8)
+    B, T80 = 2, 40
+    F0 = 120 + 80 * torch.rand(B, T80, generator=g)
+    F0[:, 5:9] = 0.0  # unvoiced stretch
+    seeds = [11, 12345]
+    ref, _ = source_features(tiny_params, S, F0, seeds)   # [B, 22, Tf]
+    from stzs.engine import Act
+    pre = eng.buf("t.pref", (B, S.harmonic_num + 1, T80), torch.float32)
+    Fd = F0.cuda()
+    from stzs import _lib as L
+    Tf = T80 * S.hop // S.istft_hop + 1
+    h = Act(torch.zeros(B, Tf, 24, dtype=torch.bfloat16, device="cuda:0"))
+    sd = torch.tensor(seeds, dtype=torch.int32, device="cuda:0")
+    a = L.SourceArgs()
+    a.f0, a.seeds, a.merge_w, a.prefix, a.har = Fd.data_ptr(), sd.data_ptr(), eng.W.t(eng.W.src_merge).data_ptr(), \
+        pre.data_ptr(), h.ptr
+    a.ldf, a.ldh, a.bsh = T80, 24, Tf * 24
+    a.B, a.T80, a.hop, a.n_fft, a.hop_s, a.nh = B, T80, S.hop, S.n_fft, S.istft_hop, S.harmonic_num + 1
+    a.sr, a.sine_amp, a.noise_std, a.voiced_thr = float(S.sr), S.sine_amp, S.noise_std, S.voiced_threshold
+    eng._call(eng.lib.stzs_harmonic_source, a, "src")
+    har = h.t[:, :, :22].float().cpu().transpose(1, 2)
+    e = max_rel(har, ref)
+    print("source", e, rel_err(har, ref))
+    assert e < 1e-2
+
+
+def test_istft(eng):
+    """exp/sin spectrum + irfft + Hann OLA + envelope vs torch.istft; fp32, 1e-5."""
+    from stzs import _lib as L
+    g = torch.Generator().manual_seed(9)
+    B, Tf = 2, 2401
+    post = torch.randn(B, Tf, 24, generator=g) * 0.5
+    spec = torch.exp(post[:, :, :11]) * torch.exp(1j * torch.sin(post[:, :, 11:22]))
+    ref = torch.istft(spec.transpose(1, 2), 20, hop_length=5, win_length=20, window=torch.hann_window(20))
+    pd = post.cuda()
+    wav = torch.zeros(B, (Tf - 1) * 5, device="cuda:0")
+    a = L.IstftArgs()
+    a.post, a.wav, a.ldp, a.bsp, a.bsw = pd.data_ptr(), wav.data_ptr(), 24, Tf * 24, (Tf - 1) * 5
+    a.B, a.Tf, a.n_fft, a.hop_s = B, Tf, 20, 5
+    eng._call(eng.lib.stzs_istft, a, "istft")
+    assert max_rel(wav.cpu(), ref) < 1e-5
+
+
+def test_abi_rejects_bad_shapes(eng):
+    """invalid arguments return a negative code before any launch (no fault)."""
+    from stzs import _lib as L
+    import ctypes as C
+    a = L.ConvArgs()
+    assert eng.lib.stzs_conv1d(C.byref(a), None) == -1  # null pointers
+    t = torch.zeros(64, device="cuda:0", dtype=torch.bfloat16)
+    a.x = a.w = a.y = t.data_ptr()
+    a.cic = 64
+    a.B, a.T_in, a.T_out, a.Ci, a.Co, a.ks, a.dil, a.stride = 1, 4, 4, 8, 8, 1, 1, 1
+    a.ci_pad, a.co_pad, a.ldx, a.bsx = 64, 64, 7, 28  # ld not a multiple of 8
+    assert eng.lib.stzs_conv1d(C.byref(a), None) == -2

