@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X StyleTTS-ZS synthesis hot path (BASELINE.json metric).
+
+metric  : synthesized audio-seconds per wall-second (whole job, all GPUs) + p50 utterance latency,
+          3-s reference -> 5-s target.
+workload: one "step" = one synth() of a batch of 64 utterances per GPU (BASELINE.json configs[2],
+          "batch=64, 2-step distilled diffusion, bf16" -- the throughput config whose 8-GPU form is
+          configs[3]), CFG scale 5, HOTPATH spec v0 dims, seeded random-init weights, synthetic
+          fixed-length inputs (16 tokens/s, durations forced to [3,2] -> exactly 5.000 s).
+latency : configs[1] (batch 1, 10-step CFG-5 sampling) timed per utterance; p50/p90 reported.
+timing  : W warm-up steps, then K steps bracketed by barrier + synchronize, max over ranks.
+          The synth() of a step is replayed from one captured HIP graph (all ~1000 launches).
+roofline: the dominant kernel (conv_mfma on the generator MRF convs, 89% of decoder FLOPs) timed
+          per launch with HIP events on its own stream in an instrumented eager pass right after
+          the timed region; achieved = algorithmic FLOP / average launch time (bound: MFMA).
+cpu     : the CPU oracle (oracle/stzs_ref.py, torch fp32) on a bounded sample of the same
+          workload (rank 0, N=1 only), threads = min(16, affinity).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "styletts-zs_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+TARGET_S = 5.0
+TOK_PER_S = 16
+REF_S = 3.0
+B_THROUGHPUT = 64
+STEPS_THROUGHPUT = 2
+CFG = 5.0
+STEPS_LATENCY = 10
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+PEAK_HBM_GBS = 8000.0
+
+
+def make_inputs(S, B, seed):
+    g = torch.Generator().manual_seed(1234 + seed)
+    T = int(TOK_PER_S * TARGET_S)
+    tok = torch.randint(1, S.n_symbols, (B, T), generator=g, dtype=torch.int64).to(torch.int32)
+    ref = torch.randn(B, int(REF_S * S.sr), generator=torch.Generator().manual_seed(4321 + seed)) * 0.1
+    eps = torch.randn(B, S.L_s, S.code_dim, generator=torch.Generator().manual_seed(seed))
+    dur = torch.tensor([[3, 2] * (T // 2)] * B, dtype=torch.int32)
+    return tok, ref, eps, dur
+
+
+def cpu_baseline(S, P, budget_s=12.0):
+    from oracle import stzs_ref as R
+    nthr = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(nthr)
+    tok, ref, eps, dur = make_inputs(S, 1, 0)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        R.synth(P, S, tok, ref, STEPS_THROUGHPUT, CFG, eps, dur, seeds=[0])
+        n += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or n >= 8:
+            break
+    return dict(value=n * TARGET_S / el, unit="audio-s/s", cores=nthr, kind="port",
+                sample=f"{n} x 1 utterance of the bench workload (5-s target, {STEPS_THROUGHPUT}-step CFG-{CFG:g}), "
+                       f"CPU oracle torch fp32, {el:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=B_THROUGHPUT)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from stzs.engine import StyleTTSZS
+    from stzs.params import init_params
+    from stzs.spec import SPEC_V0
+    S = SPEC_V0
+    # rank 0 owns the weights; every other rank receives them with ONE RCCL broadcast of the arena
+    P = init_params(S, seed=0 if rank == 0 else 1)
+    eng = StyleTTSZS(S, P, device=dev)
+    bcast_ms = 0.0
+    if world > 1:
+        from stzs.dist import broadcast_weights
+        bcast_ms = broadcast_weights(eng, src=0)
+
+    B = args.batch
+    tok, ref, eps, dur = make_inputs(S, B, seed=rank)
+    tok_d, ref_d, eps_d, dur_d = (t.to(dev) for t in (tok, ref, eps, dur))
+    n_frames = int(dur[0].sum())
+    seeds = [rank * B + i for i in range(B)]
+
+    def step():
+        return eng.synth(tok_d, ref_d, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps_d, durations=dur_d,
+                         seeds=seeds, n_frames=n_frames)
+
+    out = step()  # eager warm-up: allocates every cached buffer
+    torch.cuda.synchronize()
+    audio_s = out["wav"].shape[1] / S.sr
+    graph = None
+    if not args.no_graph:
+        try:
+            graph, out = eng.capture(step)
+        except Exception as e:  # capture failure -> eager replay, reported in the JSON
+            print(f"[bench] graph capture failed ({type(e).__name__}: {e}); eager", file=sys.stderr)
+            graph = None
+    run = graph.replay if graph is not None else step
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total_audio = world * B * audio_s * args.steps
+    value = total_audio / el
+
+    # ---- roofline of the dominant kernel: instrumented eager pass, events on the kernel's stream ----
+    eng.start_timer({"rb.c1", "rb.c2"})
+    step()
+    rec = eng.stop_timer()
+    tsum = sum(r[1] for r in rec)
+    fsum = sum(r[2] for r in rec)
+    bsum = sum(r[3] for r in rec)
+    nl = max(len(rec), 1)
+    achieved = (fsum / nl) / (tsum / nl) / 1e12 if tsum > 0 else 0.0
+    roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=None,
+                kernel="conv_mfma (generator MRF convs)", launches=len(rec),
+                avg_launch_us=round(tsum / nl * 1e6, 2), alg_gflop_per_launch=round(fsum / nl / 1e9, 3),
+                alg_hbm_gbs=round(bsum / tsum / 1e9, 1) if tsum > 0 else None)
+
+    # ---- p50 latency, configs[1]: batch 1, 10-step CFG-5 ----
+    lat = None
+    if not args.no_latency:
+        tok1, ref1, eps1, dur1 = (t.to(dev) for t in make_inputs(S, 1, seed=1000 + rank))
+
+        def one():
+            return eng.synth(tok1, ref1, steps=STEPS_LATENCY, cfg_scale=CFG, noise=eps1, durations=dur1, seeds=[7],
+                             n_frames=n_frames)
+        one()
+        g1 = None
+        if graph is not None:
+            try:
+                g1, _ = eng.capture(one)
+            except Exception:
+                g1 = None
+        r1 = g1.replay if g1 is not None else one
+        ts = []
+        for i in range(25):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            r1()
+            torch.cuda.synchronize()
+            if i >= 5:
+                ts.append((time.perf_counter() - a) * 1e3)
+        lat = dict(p50_ms=round(float(np.percentile(ts, 50)), 3), p90_ms=round(float(np.percentile(ts, 90)), 3),
+                   config="batch 1, 10-step sampling, CFG 5, 5-s target, 3-s reference")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(S, P)
+
+    if rank == 0:
+        line = {
+            "metric": "synthesized audio-sec/sec/GPU + p50 utterance latency, 3-s ref -> 5-s target",
+            "value": round(value, 2),
+            "unit": "audio-s/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (seeded tokens 16/s, 3-s noise reference, forced [3,2] durations); random-init weights",
+            "config": {"workload": "configs[2]: batch 64/GPU, 5-s targets, 2-step distilled style diffusion, CFG 5",
+                       "global_batch": world * B, "seq_len": n_frames, "parallelism": f"dp{world} (utterance shards)",
+                       "spec": S.name, "graph": graph is not None},
+            "audio_s_per_s_per_gpu": round(value / world, 2),
+            "p50_latency_ms": lat["p50_ms"] if lat else None,
+            "latency": lat,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "weight_broadcast_ms": round(bcast_ms, 3),
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -113,6 +113,7 @@ class StyleTTSZS:
         self.fe = {k: v.to(self.device).float() for k, v in params.items() if k.startswith("pe.")}
         self.mel_fb = mel_filterbank(spec.n_mels, spec.mel_nfft, spec.sr).to(self.device)
         self._bufs = {}
+        self._consts = {}
         self._ws = None
         self.launches = 0
 
@@ -177,8 +178,33 @@ class StyleTTSZS:
         if gate is not None:
             a.gate, a.gate_bs = gate, gate_bs
         a.alpha, a.beta, a.epi_act, a.epi_slope = alpha, beta, epi_act, epi_slope
-        self._call(self.lib.stzs_conv1d, a, what)
+        tm = self.timer
+        if tm is not None and what in tm["tags"]:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self._call(self.lib.stzs_conv1d, a, what)
+            e1.record()
+            flops = 2.0 * y.B * a.T_out * (cw.ups or 1) * cw.Co * cw.Ci * cw.ks
+            # algorithmic bytes: input tile once + output once (+ residual/acc reads), bf16/f32 as stored
+            byt = x.B * x.T * x.C * x.t.element_size() + y.B * a.T_out * (cw.ups or 1) * cw.Co * y.t.element_size() * (
+                1 + (res is not None) + (acc_in is not None))
+            tm["rec"].append((what, e0, e1, flops, byt))
+        else:
+            self._call(self.lib.stzs_conv1d, a, what)
         return y
+
+    timer = None
+
+    def start_timer(self, tags):
+        """record HIP events around every conv launch whose tag is in `tags` (same stream as the kernel)."""
+        self.timer = dict(tags=set(tags), rec=[])
+
+    def stop_timer(self):
+        tm, self.timer = self.timer, None
+        torch.cuda.synchronize(self.device)
+        out = [(w, e0.elapsed_time(e1) * 1e-3, f, b) for (w, e0, e1, f, b) in tm["rec"]]
+        return out
 
     def stats(self, x: Act, key):
         """InstanceNorm statistics of x over time -> (mean, rstd, stat_bs)."""
@@ -306,9 +332,11 @@ class StyleTTSZS:
             kv.append(kvl)
         # sigma embeddings for all steps
         sig = sigma_schedule(S, steps)
-        four = np.stack([fourier_features(S, edm_coeffs(S, s)["c_noise"]) for s in sig[:steps]])
-        fo = self.buf(f"dn.four{steps}", (1, steps, S.dn_fourier), torch.float32)
-        fo.copy_(torch.from_numpy(four)[None], non_blocking=False)
+        fkey = ("dn.four", steps)
+        fo = self._consts.get(fkey)
+        if fo is None:  # host constant, uploaded once (never inside a graph capture)
+            four = np.stack([fourier_features(S, edm_coeffs(S, s)["c_noise"]) for s in sig[:steps]])
+            fo = self._consts[fkey] = torch.from_numpy(four)[None].to(self.device)
         t0 = self.act("dn.t0", 1, steps, d, torch.float32)
         temb = self.act("dn.temb", 1, steps, d, torch.float32)
         self.conv(W.dn_t0, Act(fo), t0, epi_act=L.ACT_SILU, what="dn.t0")
@@ -381,8 +409,9 @@ class StyleTTSZS:
         self.conv(cw, x, view, T_out=T, what=what)
 
     # ------------------------------------------------------------------ (b) prosody predictor
-    def predict_prosody(self, h_txt: Act, codes: torch.Tensor, durations=None):
-        """durations: optional int tensor [B, T_txt] (host or device).  Returns dict of device tensors."""
+    def predict_prosody(self, h_txt: Act, codes: torch.Tensor, durations=None, n_frames=None):
+        """durations: optional int tensor [B, T_txt] (host or device); n_frames: their per-utterance sum if
+        known (avoids the device->host sync, e.g. under graph capture).  Returns dict of device tensors."""
         S, W = self.spec, self.W
         B, T = h_txt.B, h_txt.T
         pin = S.pr_in
@@ -419,12 +448,15 @@ class StyleTTSZS:
             dur.data_ptr(), dsum.data_ptr()
         a.ldl, a.bsl, a.B, a.T, a.nbins = logits.ld, logits.bs, B, T, S.dur_bins
         self._call(self.lib.stzs_durations, a, "durations")
-        if durations is not None and durations.device.type == "cpu":
-            tot = durations.to(torch.int64).sum(1)
+        if n_frames is not None:
+            T40 = int(n_frames)
         else:
-            tot = dur.to(torch.int64).sum(1).cpu()  # host sync: frame count sizes every later buffer
-        assert int(tot.min()) == int(tot.max()), "one batch must share its total frame count (§8(f) bucketing)"
-        T40 = int(tot[0])
+            if durations is not None and durations.device.type == "cpu":
+                tot = durations.to(torch.int64).sum(1)
+            else:
+                tot = dur.to(torch.int64).sum(1).cpu()  # host sync: the frame count sizes every later buffer
+            assert int(tot.min()) == int(tot.max()), "one batch must share its total frame count (§8(f) bucketing)"
+            T40 = int(tot[0])
         idx = self.buf("pr.idx", (B, T40), torch.int32)
         total = self.buf("pr.total", (B,), torch.int32)
         a = L.AlignArgs()
@@ -533,11 +565,14 @@ class StyleTTSZS:
         N = T80 * S.hop
         Tf = N // S.istft_hop + 1
         nh = S.harmonic_num + 1
-        sd = self.buf("gen.seeds", (B,), torch.int32)
         if isinstance(seeds, torch.Tensor) and seeds.device.type != "cpu":
-            sd.copy_(seeds.to(torch.int32))
+            sd = seeds.to(torch.int32)
         else:
-            sd.copy_(torch.as_tensor(np.asarray(seeds, dtype=np.uint32).astype(np.int64)).to(torch.int32))
+            skey = ("seeds", tuple(int(s) for s in seeds))
+            sd = self._consts.get(skey)
+            if sd is None:  # uploaded once per distinct seed list (graph-capture safe afterwards)
+                host = torch.as_tensor(np.asarray(seeds, dtype=np.uint32).view(np.int32).copy())
+                sd = self._consts[skey] = host.to(self.device)
         pref = self.buf("gen.pref", (B, nh, T80), torch.float32)
         har = self.act("gen.har", B, Tf, S.har_ch)
         a = L.SourceArgs()
@@ -614,9 +649,26 @@ class StyleTTSZS:
         return xs
 
     # ------------------------------------------------------------------ end to end
-    def synth(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None, codes=None):
+    def capture(self, fn):
+        """Capture `fn()` into one HIP graph.  fn must be replay-safe: device-resident inputs, cached
+        buffers (a warm-up call on a side stream allocates them), no host syncs.  -> (graph, fn's output)"""
+        cur = torch.cuda.current_stream(self.device)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            fn()
+        cur.wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = fn()
+        return g, out
+
+    def synth(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None, codes=None,
+              n_frames=None):
         """tokens int [B, T_txt]; ref_wav fp32 [B|1, N]; noise fp32 [B, L_s, code]; durations int [B, T_txt]
-        (host tensor: no device sync); seeds: per-utterance source-noise seeds.  -> dict(wav=[B, 600*T40])"""
+        (host tensor, or device tensor + n_frames: no device sync); seeds: per-utterance source-noise
+        seeds.  -> dict(wav=[B, 600*T40], ...)"""
         S = self.spec
         dev = self.device
         tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
@@ -630,7 +682,7 @@ class StyleTTSZS:
         if codes is None:
             eps = noise.to(dev, torch.float32)
             codes = self.sample_style(h, prompt, eps, steps, cfg_scale)
-        pro = self.predict_prosody(h, codes, durations)
+        pro = self.predict_prosody(h, codes, durations, n_frames)
         seeds = list(range(B)) if seeds is None else seeds
         wav = self.decode(pro, codes, seeds)
         return dict(wav=wav, codes=codes, h_txt=h, prompt=prompt, **pro)
