@@ -1,44 +1,74 @@
 // The universal MFMA conv1d / linear of the hot path.
 //
-// Implicit GEMM on gfx950 matrix cores: M = output time rows, N = output channels,
-// K = taps x input channels.  One 256-thread workgroup (4 waves, 2x2) owns a BT x BCO output
-// tile; each wave a (BT/2) x (BCO/2) sub-tile of 16x16 accumulators fed by
-// v_mfma_f32_16x16x32_bf16 (bf16 operands, fp32 accumulate).
+// Implicit GEMM on gfx950 matrix cores: M = output time rows, N = output channels, K = taps x
+// input channels.  One 256-thread workgroup (4 waves as 2x2) owns a 128 x 128 output tile; each
+// wave a 64 x 64 sub-tile = 4 x 4 accumulators of v_mfma_f32_16x16x32_bf16 (bf16 operands, fp32
+// accumulate).  Two workgroups fit per CU (<= 80 KB LDS each), so one's staging/epilogue VALU
+// overlaps the other's MFMAs.
 //
-// Per input-channel chunk (cic = 32|64 channels):
-//   1. the input rows of the tile INCLUDING the dilation halo are staged ONCE into LDS
-//      (channels-last rows, 16-B padded pitch), with the AdaIN / cscale prologue and the
-//      activation (LeakyReLU / Snake) applied on the way in -> no separate norm/activation pass;
-//   2. the taps re-read that LDS tile at row offset tap*dil (the halo is never re-fetched);
-//   3. per-tap weight tiles [BCO][cic] are double-buffered in LDS with register prefetch of the
-//      next tap issued before the MFMAs of the current one (T14 split: issue early, write late).
-// The epilogue fuses bias, activation, DiT gate, residual (optionally read at t/res_tdiv, i.e.
-// a nearest-x2 shortcut), scaling and an fp32/bf16 accumulate-input (MRF sum, EDM c_skip*x),
-// and the polyphase ConvTranspose1d scatter (+ ReflectionPad(1,0)) when `ups` > 0.
+//  * INPUT: per input-channel chunk (cic = 32|64|128) the tile's rows INCLUDING the dilation halo
+//    are staged ONCE into LDS through registers, with the AdaIN/cscale prologue and the
+//    activation (LeakyReLU / Snake with the hardware v_sin) applied on the way in.  Rows use a
+//    16-B padded pitch (conflict-light ds_read_b128 for the A fragments).  Every tap re-reads that
+//    tile at row offset tap*dil: the halo is fetched once, no separate norm/activation pass exists.
+//  * WEIGHTS: pre-packed per 128-column tile as a stream of K-steps, each [128 co][32 ci] bf16 =
+//    8 KB, already XOR-swizzled into the LDS image order (stzs/weights.py) so that a lane-linear
+//    LDS-DMA copy (global_load_lds_dwordx4, 1 KB per wave instruction) lands a conflict-free
+//    B-fragment layout.  A 3-slot ring keeps two K-steps in flight: counted s_waitcnt vmcnt + one
+//    raw s_barrier per K-step, never a vmcnt(0) drain inside the K loop.
+//  * EPILOGUE: accumulators go through LDS (fp32, padded rows) and leave as 16-B vectors per lane:
+//    bias, activation, DiT gate, residual (optionally at t/res_tdiv = nearest-x2 shortcut), scale,
+//    fp32/bf16 accumulate-input (MRF sum, EDM c_skip*x), the polyphase ConvTranspose1d scatter and
+//    ReflectionPad(1,0) when ups > 0.
 #include "common.hpp"
 
 namespace {
 
 constexpr int NTHR = 256;
+constexpr int BT = 128, BCO = 128;
+constexpr int NSLOT = 3;
+constexpr int SLOT_BYTES = BCO * 32 * 2;  // one K-step of weights
+constexpr int EP_PITCH = BCO + 4;         // fp32 epilogue row pitch (floats)
 
-template <typename TIn, typename TOut, int BT, int BCO, bool FLAT>
-__global__ __launch_bounds__(NTHR) void conv_mfma(const stzs_conv_args a) {
+STZS_DEV int gswz(int r) { return (0x1320 >> (((r >> 2) & 3) * 4)) & 3; }
+
+template <int PACT>
+STZS_DEV float pro_act(float x, float slope, float alpha, float ialpha) {
+    if constexpr (PACT == STZS_ACT_SNAKE) {
+        const float s = __sinf(alpha * x);  // v_sin_f32 (hardware, revolutions)
+        return x + s * s * ialpha;
+    } else if constexpr (PACT == STZS_ACT_LEAKY) {
+        return x >= 0.f ? x : x * slope;
+    } else {
+        return x;
+    }
+}
+
+template <typename T> STZS_DEV void store8v(T* p, const float* v) { store8(p, v); }
+
+STZS_DEV void waitcnt_vm(int n) {
+    if (n >= 2)
+        __builtin_amdgcn_s_waitcnt(0x0F70 | 2);
+    else
+        __builtin_amdgcn_s_waitcnt(0x0F70 | 0);
+}
+
+template <typename TIn, typename TOut, bool FLAT, int PACT>
+__global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int WT = BT / 2, WC = BCO / 2, MT = WT / 16, NT = WC / 16;
-    constexpr int WV_MAX = BCO * 8 / NTHR;  // 16-B weight vectors per thread at cic = 64
     const int cic = a.cic;
-    const int lrow = cic + 8;
+    const int pitch = cic * 2 + 16;
     const int ks = FLAT ? 1 : a.ks;
     const int rows_in = FLAT ? BT : (BT - 1) * a.stride + (ks - 1) * a.dil + 1;
-    bf16_t* in_lds = reinterpret_cast<bf16_t*>(smem);
-    bf16_t* w_lds = in_lds + rows_in * lrow;
-    float* c_sc = reinterpret_cast<float*>(w_lds + 2 * BCO * lrow);
-    float* c_sh = c_sc + 64;
-    float* c_al = c_sh + 64;
+    unsigned char* in_lds = smem;
+    unsigned char* ring = smem + ((rows_in * pitch + 15) & ~15);
+    float* c_sc = reinterpret_cast<float*>(ring + NSLOT * SLOT_BYTES);
+    float* c_sh = c_sc + 128;
+    float* c_al = c_sh + 128;
+    float* c_ia = c_al + 128;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
-    const int n0 = blockIdx.y * BCO;
     int bq = 0, t0 = 0;
     long row0 = 0;
     if (FLAT) {
@@ -48,43 +78,40 @@ __global__ __launch_bounds__(NTHR) void conv_mfma(const stzs_conv_args a) {
         bq = blockIdx.x / tpb;
         t0 = (blockIdx.x - bq * tpb) * BT;
     }
+    const int nchunk = a.ci_pad / cic;
+    const int kpc = cic >> 5;
+    const int NK = nchunk * ks * kpc;
+    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
 
-    f32x4 acc[MT][NT];
+    auto fill = [&](int k) {
+        const bf16_t* src = Wt + (long)k * (BCO * 32) + wave * 1024 + lane * 8;
+        unsigned char* dst = ring + (k % NSLOT) * SLOT_BYTES + wave * 2048;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 512),
+                                         (__attribute__((address_space(3))) void*)(dst + 1024), 16, 0, 0);
+    };
+
+    f32x4 acc[4][4];
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const TIn* X = reinterpret_cast<const TIn*>(a.x);
-    const bf16_t* W = reinterpret_cast<const bf16_t*>(a.w);
-    const int nchunk = a.ci_pad / cic;
     const int vpr = cic >> 3;
-    const int wvec = BCO * vpr;
-    uint4 wreg[WV_MAX];
-
-    auto load_w = [&](int tap, int cc) {
+    const int rstr = FLAT ? 1 : a.stride;
+    // B-fragment LDS byte offsets inside a slot (fixed per lane): row rr, chunk (lane>>4) swizzled
+    int boff[4];
 #pragma unroll
-        for (int i = 0; i < WV_MAX; ++i) {
-            const int v = tid + i * NTHR;
-            if (v < wvec) {
-                const int r = v / vpr, cv = v - r * vpr;
-                wreg[i] = *reinterpret_cast<const uint4*>(
-                    W + ((long)tap * a.co_pad + n0 + r) * a.ci_pad + cc * cic + cv * 8);
-            }
-        }
-    };
-    auto store_w = [&](int buf) {
-        bf16_t* dst = w_lds + buf * BCO * lrow;
-#pragma unroll
-        for (int i = 0; i < WV_MAX; ++i) {
-            const int v = tid + i * NTHR;
-            if (v < wvec) {
-                const int r = v / vpr, cv = v - r * vpr;
-                *reinterpret_cast<uint4*>(dst + r * lrow + cv * 8) = wreg[i];
-            }
-        }
-    };
+    for (int nt = 0; nt < 4; ++nt) {
+        const int rr = wc * 64 + nt * 16 + (lane & 15);
+        boff[nt] = rr * 64 + (((lane >> 4) ^ gswz(rr)) << 4);
+    }
 
+    fill(0);
+    if (NK > 1) fill(1);
+    int k = 0;
     for (int cc = 0; cc < nchunk; ++cc) {
         __syncthreads();
         if (tid < cic) {
@@ -106,8 +133,8 @@ __global__ __launch_bounds__(NTHR) void conv_mfma(const stzs_conv_args a) {
             c_sc[tid] = sc;
             c_sh[tid] = sh;
             c_al[tid] = al;
+            c_ia[tid] = 1.f / al;
         }
-        load_w(0, cc);
         __syncthreads();
         const int nv = rows_in * vpr;
         for (int v = tid; v < nv; v += NTHR) {
@@ -120,8 +147,7 @@ __global__ __launch_bounds__(NTHR) void conv_mfma(const stzs_conv_args a) {
                 const long R = row0 + r;
                 ok = R < (long)a.B * a.T_in;
                 const long bb = R / a.T_in;
-                const long tt = R - bb * a.T_in;
-                src = X + bb * a.bsx + tt * a.ldx + ci;
+                src = X + bb * a.bsx + (R - bb * a.T_in) * a.ldx + ci;
             } else {
                 const int tin = t0 * a.stride - a.pad + r;
                 ok = tin >= 0 && tin < a.T_in;
@@ -131,157 +157,171 @@ __global__ __launch_bounds__(NTHR) void conv_mfma(const stzs_conv_args a) {
             if (ok) {
                 load8(src, f);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float y = f[j] * c_sc[cv * 8 + j] + c_sh[cv * 8 + j];
-                    f[j] = act_apply(a.pro_act, y, a.pro_slope, c_al[cv * 8 + j]);
-                }
+                for (int j = 0; j < 8; ++j)
+                    f[j] = pro_act<PACT>(f[j] * c_sc[cv * 8 + j] + c_sh[cv * 8 + j], a.pro_slope, c_al[cv * 8 + j],
+                                         c_ia[cv * 8 + j]);
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) f[j] = 0.f;
             }
-            *reinterpret_cast<uint4*>(in_lds + r * lrow + cv * 8) = pack8(f);
+            *reinterpret_cast<uint4*>(in_lds + r * pitch + cv * 16) = pack8(f);
         }
-        store_w(0);
         __syncthreads();
         for (int tap = 0; tap < ks; ++tap) {
-            const int buf = tap & 1;
-            if (tap + 1 < ks) load_w(tap + 1, cc);
-            const bf16_t* wl = w_lds + buf * BCO * lrow;
             const int roff = FLAT ? 0 : tap * a.dil;
-            const int rstr = FLAT ? 1 : a.stride;
-            for (int kk = 0; kk < cic; kk += 32) {
-                const int kc = kk + 8 * (lane >> 4);
-                bf16x8 af[MT], bw[NT];
+            for (int kq = 0; kq < kpc; ++kq, ++k) {
+                waitcnt_vm(k + 1 < NK ? 2 : 0);
+                __builtin_amdgcn_s_barrier();
+                if (k + 2 < NK) fill(k + 2);
+                const unsigned char* wl = ring + (k % NSLOT) * SLOT_BYTES;
+                const int kb = (kq * 32 + 8 * (lane >> 4)) * 2;
+                bf16x8 af[4], bw[4];
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    const int r = (wt * WT + mt * 16 + (lane & 15)) * rstr + roff;
-                    af[mt] = *reinterpret_cast<const bf16x8*>(in_lds + r * lrow + kc);
+                for (int mt = 0; mt < 4; ++mt) {
+                    const int r = (wt * 64 + mt * 16 + (lane & 15)) * rstr + roff;
+                    af[mt] = *reinterpret_cast<const bf16x8*>(in_lds + r * pitch + kb);
                 }
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt) {
-                    const int c = wc * WC + nt * 16 + (lane & 15);
-                    bw[nt] = *reinterpret_cast<const bf16x8*>(wl + c * lrow + kc);
-                }
+                for (int nt = 0; nt < 4; ++nt) bw[nt] = *reinterpret_cast<const bf16x8*>(wl + boff[nt]);
+                __builtin_amdgcn_sched_barrier(0);  // issue all 8 fragment reads before the first MFMA
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
+                for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
+                    for (int nt = 0; nt < 4; ++nt)
                         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bw[nt], acc[mt][nt], 0, 0, 0);
             }
-            if (tap + 1 < ks) store_w(buf ^ 1);
-            __syncthreads();
         }
     }
 
-    // ---- epilogue ----
+    // ---- epilogue through LDS ----
+    __syncthreads();
+    float* ep = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                ep[(wt * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
+    __syncthreads();
+
     const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
     const TOut* AI = reinterpret_cast<const TOut*>(a.acc_in);
     TOut* Y = reinterpret_cast<TOut*>(a.y);
     const int ncol = a.ups > 0 ? a.ups * a.Co : a.Co;
     const long nrows_flat = (long)a.B * a.T_out;
+    const bool vec = (a.Co % 8 == 0) && (a.ldy % 8 == 0) && (!Rp || a.ldr % 8 == 0) && (!AI || a.lda % 8 == 0) &&
+                     (a.bsy % 8 == 0) && (!Rp || a.bsr % 8 == 0) && (!AI || a.bsa % 8 == 0);
+    for (int v = tid; v < BT * (BCO / 8); v += NTHR) {
+        const int tl = v >> 4, cv = v & 15;
+        const int n = blockIdx.y * BCO + cv * 8;
+        if (n >= ncol) continue;
+        long bb, t;
+        if (FLAT) {
+            const long Rr = row0 + tl;
+            if (Rr >= nrows_flat) continue;
+            bb = Rr / a.T_out;
+            t = Rr - bb * a.T_out;
+        } else {
+            bb = bq;
+            t = t0 + tl;
+            if (t >= a.T_out) continue;
+        }
+        int co = n;
+        if (a.ups > 0) {
+            const int p = n / a.Co;
+            co = n - p * a.Co;
+            t = t * a.ups + p - a.ups_pad;
+            if (t < 0 || t >= a.T_final) continue;
+            t += a.refl;
+        }
+        float u[8];
+        const float* er = ep + tl * EP_PITCH + cv * 8;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+        for (int j = 0; j < 8; ++j) {
+            float x = er[j];
+            if (a.bias) x += (co + j < a.Co || a.ups) ? a.bias[min(co + j, a.Co - 1)] : 0.f;
+            x = act_apply(a.epi_act, x, a.epi_slope, 1.f);
+            if (a.gate) x *= a.gate[bb * a.gate_bs + min(co + j, a.Co - 1)];
+            u[j] = x;
+        }
+        const int ntgt = (a.ups > 0 && a.refl && t == 2) ? 2 : 1;
+        for (int q = 0; q < ntgt; ++q) {
+            const long tt = q == 0 ? t : 0;
+            float o[8];
+            if (vec && co + 8 <= a.Co) {
+                float rr[8], ai[8];
+                if (Rp) load8(Rp + bb * a.bsr + (tt / a.res_tdiv) * a.ldr + co, rr);
+                if (AI) load8(AI + bb * a.bsa + tt * a.lda + co, ai);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int tl = wt * WT + mt * 16 + (lane >> 4) * 4 + r;
-                const int n = n0 + wc * WC + nt * 16 + (lane & 15);
-                if (n >= ncol) continue;
-                long bb, t;
-                if (FLAT) {
-                    const long Rr = row0 + tl;
-                    if (Rr >= nrows_flat) continue;
-                    bb = Rr / a.T_out;
-                    t = Rr - bb * a.T_out;
-                } else {
-                    bb = bq;
-                    t = t0 + tl;
-                    if (t >= a.T_out) continue;
+                for (int j = 0; j < 8; ++j) {
+                    float x = u[j];
+                    if (Rp) x += rr[j];
+                    x *= a.alpha;
+                    if (AI) x += a.beta * ai[j];
+                    o[j] = x;
                 }
-                int co = n;
-                if (a.ups > 0) {
-                    const int p = n / a.Co;
-                    co = n - p * a.Co;
-                    t = t * a.ups + p - a.ups_pad;
-                    if (t < 0 || t >= a.T_final) continue;
-                    t += a.refl;
-                }
-                float u = acc[mt][nt][r];
-                if (a.bias) u += a.bias[co];
-                u = act_apply(a.epi_act, u, a.epi_slope, 1.f);
-                if (a.gate) u *= a.gate[bb * a.gate_bs + co];
-                const int ntgt = (a.ups > 0 && a.refl && t == 2) ? 2 : 1;
-                for (int q = 0; q < ntgt; ++q) {
-                    const long tt = q == 0 ? t : 0;
-                    float v = u;
-                    if (Rp) v += DT<TOut>::ld(Rp + bb * a.bsr + (tt / a.res_tdiv) * a.ldr + co);
-                    v *= a.alpha;
-                    if (AI) v += a.beta * DT<TOut>::ld(AI + bb * a.bsa + tt * a.lda + co);
-                    DT<TOut>::st(Y + bb * a.bsy + tt * a.ldy + co, v);
+                store8v(Y + bb * a.bsy + tt * a.ldy + co, o);
+            } else {
+                for (int j = 0; j < 8 && co + j < a.Co; ++j) {
+                    float x = u[j];
+                    if (Rp) x += DT<TOut>::ld(Rp + bb * a.bsr + (tt / a.res_tdiv) * a.ldr + co + j);
+                    x *= a.alpha;
+                    if (AI) x += a.beta * DT<TOut>::ld(AI + bb * a.bsa + tt * a.lda + co + j);
+                    DT<TOut>::st(Y + bb * a.bsy + tt * a.ldy + co + j, x);
                 }
             }
-}
-
-size_t lds_bytes(int BT, int BCO, int rows_in, int cic) {
-    const int lrow = cic + 8;
-    return (size_t)rows_in * lrow * 2 + (size_t)2 * BCO * lrow * 2 + 3 * 64 * 4;
-}
-
-template <typename TIn, typename TOut, int BT, int BCO>
-int launch_cfg(const stzs_conv_args& a, hipStream_t s, bool flat) {
-    const int rows_in = flat ? BT : (BT - 1) * a.stride + (a.ks - 1) * a.dil + 1;
-    const size_t lds = lds_bytes(BT, BCO, rows_in, a.cic);
-    if (lds > 160 * 1024) return STZS_ESHAPE;
-    unsigned gx = flat ? (unsigned)(((long)a.B * a.T_out + BT - 1) / BT)
-                       : (unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT);
-    dim3 grid(gx, a.co_pad / BCO);
-    if (flat) {
-        auto k = conv_mfma<TIn, TOut, BT, BCO, true>;
-        if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, a);
-    } else {
-        auto k = conv_mfma<TIn, TOut, BT, BCO, false>;
-        if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, a);
+        }
     }
-    STZS_LAUNCH_CHECK();
-    return STZS_OK;
+}
+
+size_t lds_bytes(int rows_in, int cic) {
+    const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + NSLOT * SLOT_BYTES + 4 * 128 * 4;
+    const size_t epi = (size_t)BT * EP_PITCH * 4;
+    return main > epi ? main : epi;
 }
 
 template <typename TIn, typename TOut>
 int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     const bool flat = (a.ks == 1 && a.stride == 1 && a.pad == 0 && a.ups == 0 && a.pro_mode == STZS_PRO_NONE &&
-                       a.T_in == a.T_out);
-    const int BCO = (a.co_pad % 128 == 0) ? 128 : 64;
-    int BT = 128;
-    if (!flat) {
-        const int rows128 = 127 * a.stride + (a.ks - 1) * a.dil + 1;
-        if (a.T_out <= 64 || lds_bytes(128, BCO, rows128, a.cic) > 64 * 1024) BT = 64;
-    } else if ((long)a.B * a.T_out <= 64) {
-        BT = 64;
-    }
-    if (BT == 128 && BCO == 128) return launch_cfg<TIn, TOut, 128, 128>(a, s, flat);
-    if (BT == 128 && BCO == 64) return launch_cfg<TIn, TOut, 128, 64>(a, s, flat);
-    if (BT == 64 && BCO == 128) return launch_cfg<TIn, TOut, 64, 128>(a, s, flat);
-    return launch_cfg<TIn, TOut, 64, 64>(a, s, flat);
+                       a.pro_act == STZS_ACT_NONE && a.T_in == a.T_out);
+    const int rows_in = flat ? BT : (BT - 1) * a.stride + (a.ks - 1) * a.dil + 1;
+    const size_t lds = lds_bytes(rows_in, a.cic);
+    if (lds > 160 * 1024) return STZS_ESHAPE;
+    const unsigned gx = flat ? (unsigned)(((long)a.B * a.T_out + BT - 1) / BT)
+                             : (unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT);
+    dim3 grid(gx, a.co_pad / BCO);
+    void (*k)(stzs_conv_args);
+    if (flat)
+        k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE>;
+    else if (a.pro_act == STZS_ACT_SNAKE)
+        k = conv_mfma<TIn, TOut, false, STZS_ACT_SNAKE>;
+    else if (a.pro_act == STZS_ACT_LEAKY)
+        k = conv_mfma<TIn, TOut, false, STZS_ACT_LEAKY>;
+    else
+        k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE>;
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
 }
 
 }  // namespace
 
 extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
     if (!a || !a->x || !a->w || !a->y) return STZS_EINVAL;
-    if (a->cic != 32 && a->cic != 64) return STZS_EINVAL;
+    if (a->cic != 32 && a->cic != 64 && a->cic != 128) return STZS_EINVAL;
     if (a->B <= 0 || a->T_in <= 0 || a->T_out <= 0 || a->Ci <= 0 || a->Co <= 0 || a->ks <= 0 || a->dil <= 0 ||
         a->stride <= 0)
         return STZS_ESHAPE;
-    if (a->ci_pad % a->cic || a->ci_pad < a->Ci || a->co_pad % 64) return STZS_ESHAPE;
+    if (a->ci_pad % a->cic || a->ci_pad < a->Ci || a->co_pad % BCO) return STZS_ESHAPE;
     const int ncol = a->ups > 0 ? a->ups * a->Co : a->Co;
     if (a->co_pad < ncol) return STZS_ESHAPE;
     if (a->ldx % 8 || a->bsx % 8 || a->ldx < ((a->Ci + 7) / 8) * 8) return STZS_ESHAPE;
-    if (!stzs_aligned(a->x, 32) || !stzs_aligned(a->w, 16)) return STZS_EINVAL;
+    if (!stzs_aligned(a->x, 16) || !stzs_aligned(a->w, 16)) return STZS_EINVAL;
     if (a->ups > 0) {
         if (a->ks != 2 || a->pad != 1 || a->stride != 1 || a->dil != 1 || a->T_out != a->T_in + 1) return STZS_ESHAPE;
+        if (a->Co % 8) return STZS_ESHAPE;
         if (a->refl && a->T_final < 2) return STZS_ESHAPE;
     } else if (a->refl) {
         return STZS_EINVAL;
@@ -289,9 +329,6 @@ extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
     if (a->res && a->res_tdiv <= 0) return STZS_EINVAL;
     if (a->pro_mode == STZS_PRO_ADAIN && (!a->pro_mean || !a->pro_rstd || !a->pro_gb)) return STZS_EINVAL;
     if (a->pro_act == STZS_ACT_SNAKE && !a->pro_alpha) return STZS_EINVAL;
-    // the output row range the kernel may address must be non-negative and consistent
-    const long t_last = a->ups > 0 ? (long)a->T_final + a->refl : a->T_out;
-    if (t_last <= 0) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) return launch_dt<bf16_t, bf16_t>(*a, s);
     if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) return launch_dt<bf16_t, float>(*a, s);

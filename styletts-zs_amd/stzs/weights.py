@@ -83,6 +83,25 @@ class Arena:
         return self.views[k]
 
 
+_GSWZ = (0, 2, 3, 1)
+
+
+def kstep_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
+    """[ks, co_pad, ci_pad] -> [co_pad/128, NK, 128, 32] K-step stream in the kernel's loop order
+    (ci chunk, tap, 32-wide k-step), each 8-KB K-step already in its LDS image order: the 16-B
+    chunk c of row r sits at position c ^ g((r >> 2) & 3), g = (0, 2, 3, 1) -- the XOR swizzle
+    that makes the 16x16x32 B-fragment ds_read_b128 conflict-free (csrc/conv.hip)."""
+    ks, co_pad, ci_pad = wp.shape
+    ncot, nchunk, kpc = co_pad // 128, ci_pad // cic, cic // 32
+    t = wp.view(ks, ncot, 128, nchunk, kpc, 4, 8).permute(1, 3, 0, 4, 2, 5, 6)  # cot, cc, tap, kq, r, c, 8
+    r = torch.arange(128)
+    g = torch.tensor(_GSWZ)[(r >> 2) & 3]
+    p = torch.arange(4)
+    src_c = p[None, :] ^ g[:, None]                                            # [128, 4]: position -> chunk
+    t = t[:, :, :, :, r[:, None], src_c, :]
+    return t.reshape(ncot, nchunk * ks * kpc, 128, 32).contiguous()
+
+
 def pack_conv(A: Arena, name, w, b=None, ups=0) -> ConvW:
     """w: Conv1d [Co, Ci, k] / Linear [Co, Ci] / ConvTranspose1d [Ci, Co, 2*ups] (ups > 0)."""
     if ups:
@@ -100,12 +119,12 @@ def pack_conv(A: Arena, name, w, b=None, ups=0) -> ConvW:
         Co, Ci, ks = w.shape
         ncol = Co
         wk = w.permute(2, 0, 1)
-    cic = 32 if Ci <= 32 else 64
+    cic = 32 if Ci <= 32 else (64 if Ci <= 64 else 128)
     ci_pad = _rup(Ci, cic)
-    co_pad = _rup(ncol, 128) if ncol >= 128 else _rup(ncol, 64)
+    co_pad = _rup(ncol, 128)
     wp = torch.zeros(ks, co_pad, ci_pad)
     wp[:, :ncol, :Ci] = wk
-    wn = A.add(name + ".wpk", wp.to(torch.bfloat16))
+    wn = A.add(name + ".wpk", kstep_stream(wp, cic).to(torch.bfloat16))
     bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
     return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups)
 
