@@ -117,7 +117,8 @@ int stzs_attention(const stzs_attn_args* a, void* stream);
 
 /* ---- LSTM recurrence (input projection done by stzs_conv1d) -----------------------------
  * gx [B, T, ldg] f32 holds x W_ih^T + b_ih + b_hh for both directions (fwd 4H | rev 4H, gate
- * order i,f,g,o); whhT [2][H][4H] f32; h written bf16 to y[b, t, dir*H + j].
+ * order i,f,g,o); whhT = W_hh^T as bf16 16x16x32 B fragments [2][4H/16][H/32][64][8]
+ * (stzs/weights.py lstm_frags); H % 32 == 0, H <= 256; h written bf16 to y[b, t, dir*H + j].
  * (DurationEncoder BiLSTMs, duration LSTM, shared LSTM) */
 typedef struct stzs_lstm_args {
     const float* gx;

@@ -53,6 +53,114 @@ STZS_DEV void waitcnt_vm(int n) {
         __builtin_amdgcn_s_waitcnt(0x0F70 | 0);
 }
 
+// Epilogue pass: EB 8-channel output vectors per thread; residual / accumulate loads are issued
+// unconditionally from clamped addresses (all in flight) before any is consumed.
+template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA>
+STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_bias, const float* c_gate, int bq,
+                       int t0, long row0, int tid) {
+    const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
+    const TOut* AI = reinterpret_cast<const TOut*>(a.acc_in);
+    TOut* Y = reinterpret_cast<TOut*>(a.y);
+    const int ncol = a.ups > 0 ? a.ups * a.Co : a.Co;
+    const long nrows_flat = (long)a.B * a.T_out;
+    const long t_hi = a.ups > 0 ? (long)a.T_final + a.refl - 1 : (long)a.T_out - 1;
+    constexpr int EB = 4;
+    for (int v0 = 0; v0 < BT * (BCO / 8); v0 += EB * NTHR) {
+        long pb[EB], pt[EB];
+        int pco[EB];
+        bool pv[EB];
+        float rr[EB][8], ai[EB][8];
+#pragma unroll
+        for (int i = 0; i < EB; ++i) {
+            const int v = v0 + tid + i * NTHR;
+            const int tl = v >> 4, cv = v & 15;
+            const int n = blockIdx.y * BCO + cv * 8;
+            bool ok = n < ncol;
+            long bb, t;
+            if (FLAT) {
+                const long Rr = row0 + tl;
+                ok = ok && Rr < nrows_flat;
+                bb = Rr / a.T_out;
+                t = Rr - bb * a.T_out;
+            } else {
+                bb = bq;
+                t = t0 + tl;
+                ok = ok && t < a.T_out;
+            }
+            int co = n;
+            if (a.ups > 0) {
+                const int p = n / a.Co;
+                co = n - p * a.Co;
+                t = t * a.ups + p - a.ups_pad;
+                ok = ok && t >= 0 && t < a.T_final;
+                t += a.refl;
+            }
+            // clamp to a valid element so the loads below need no condition
+            const long tc = t < 0 ? 0 : (t > t_hi ? t_hi : t);
+            const long bc = bb < a.B ? bb : a.B - 1;
+            const int cc = ok ? co : 0;
+            pb[i] = bb;
+            pt[i] = t;
+            pco[i] = co;
+            pv[i] = ok;
+            if constexpr (VEC) {
+                if constexpr (HR) load8(Rp + bc * a.bsr + (tc / a.res_tdiv) * a.ldr + cc, rr[i]);
+                if constexpr (HA) load8(AI + bc * a.bsa + tc * a.lda + cc, ai[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < EB; ++i) {
+            if (!pv[i]) continue;
+            const int v = v0 + tid + i * NTHR;
+            const int tl = v >> 4, cv = v & 15;
+            const long bb = pb[i], t = pt[i];
+            const int co = pco[i];
+            float u[8];
+            const float* er = ep + tl * EP_PITCH + cv * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float x = er[j] + c_bias[cv * 8 + j];
+                x = act_apply(a.epi_act, x, a.epi_slope, 1.f);
+                if (FLAT) {
+                    if (a.gate) x *= a.gate[bb * a.gate_bs + min(co + j, a.Co - 1)];
+                } else {
+                    x *= c_gate[cv * 8 + j];
+                }
+                u[j] = x;
+            }
+            if constexpr (VEC) {
+                float o[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float x = u[j];
+                    if constexpr (HR) x += rr[i][j];
+                    x *= a.alpha;
+                    if constexpr (HA) x += a.beta * ai[i][j];
+                    o[j] = x;
+                }
+                store8(Y + bb * a.bsy + t * a.ldy + co, o);
+            } else {
+                for (int j = 0; j < 8 && co + j < a.Co; ++j) {
+                    float x = u[j];
+                    if (Rp) x += DT<TOut>::ld(Rp + bb * a.bsr + (t / a.res_tdiv) * a.ldr + co + j);
+                    x *= a.alpha;
+                    if (AI) x += a.beta * DT<TOut>::ld(AI + bb * a.bsa + t * a.lda + co + j);
+                    DT<TOut>::st(Y + bb * a.bsy + t * a.ldy + co + j, x);
+                }
+            }
+            if (a.ups > 0 && a.refl && t == 2) {  // ReflectionPad(1,0): row 0 mirrors source row 1
+                for (int j = 0; j < 8 && co + j < a.Co; ++j) {
+                    float x = u[j];
+                    if (Rp) x += DT<TOut>::ld(Rp + bb * a.bsr + co + j);
+                    x *= a.alpha;
+                    if (AI) x += a.beta * DT<TOut>::ld(AI + bb * a.bsa + co + j);
+                    DT<TOut>::st(Y + bb * a.bsy + co + j, x);
+                }
+            }
+        }
+    }
+}
+
 template <typename TIn, typename TOut, bool FLAT, int PACT>
 __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -136,38 +244,57 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
             c_ia[tid] = 1.f / al;
         }
         __syncthreads();
-        const int nv = rows_in * vpr;
-        for (int v = tid; v < nv; v += NTHR) {
-            const int r = v / vpr, cv = v - r * vpr;
-            const int ci = cc * cic + cv * 8;
-            float f[8];
-            bool ok;
-            const TIn* src;
-            if (FLAT) {
-                const long R = row0 + r;
-                ok = R < (long)a.B * a.T_in;
-                const long bb = R / a.T_in;
-                src = X + bb * a.bsx + (R - bb * a.T_in) * a.ldx + ci;
-            } else {
-                const int tin = t0 * a.stride - a.pad + r;
-                ok = tin >= 0 && tin < a.T_in;
-                src = X + (long)bq * a.bsx + (long)tin * a.ldx + ci;
-            }
-            ok = ok && (ci < a.Ci);
-            if (ok) {
-                load8(src, f);
+        const int nv = (a.flags & 1) ? 0 : rows_in * vpr;
+        // batched staging: SB independent 16-B loads in flight per thread before any is consumed.
+        // Loads are UNCONDITIONAL from clamped (always valid) addresses and masked afterwards: a
+        // runtime-conditioned load makes hipcc drain vmcnt(0) per element (serialised round trips).
+        constexpr int SB = sizeof(TIn) == 2 ? 8 : 4;
+        for (int v0 = 0; v0 < nv; v0 += SB * NTHR) {
+            float f[SB][8];
+            bool okv[SB];
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    f[j] = pro_act<PACT>(f[j] * c_sc[cv * 8 + j] + c_sh[cv * 8 + j], a.pro_slope, c_al[cv * 8 + j],
-                                         c_ia[cv * 8 + j]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) f[j] = 0.f;
+            for (int i = 0; i < SB; ++i) {
+                int v = v0 + tid + i * NTHR;
+                bool ok = v < nv;
+                v = ok ? v : 0;
+                const int r = v / vpr, cv = v - r * vpr;
+                int ci = cc * cic + cv * 8;
+                ok = ok && ci < a.Ci;
+                ci = ci < a.Ci ? ci : 0;
+                long off;
+                if (FLAT) {
+                    long R = row0 + r;
+                    const long nR = (long)a.B * a.T_in;
+                    ok = ok && R < nR;
+                    R = R < nR ? R : nR - 1;
+                    const long bb = R / a.T_in;
+                    off = bb * a.bsx + (R - bb * a.T_in) * a.ldx + ci;
+                } else {
+                    int tin = t0 * a.stride - a.pad + r;
+                    ok = ok && tin >= 0 && tin < a.T_in;
+                    tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+                    off = (long)bq * a.bsx + (long)tin * a.ldx + ci;
+                }
+                okv[i] = ok;
+                load8(X + off, f[i]);
             }
-            *reinterpret_cast<uint4*>(in_lds + r * pitch + cv * 16) = pack8(f);
+#pragma unroll
+            for (int i = 0; i < SB; ++i) {
+                const int v = v0 + tid + i * NTHR;
+                if (v >= nv) break;
+                const int r = v / vpr, cv = v - r * vpr;
+                float o[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float y = pro_act<PACT>(f[i][j] * c_sc[cv * 8 + j] + c_sh[cv * 8 + j], a.pro_slope,
+                                                  c_al[cv * 8 + j], c_ia[cv * 8 + j]);
+                    o[j] = okv[i] ? y : 0.f;
+                }
+                *reinterpret_cast<uint4*>(in_lds + r * pitch + cv * 16) = pack8(o);
+            }
         }
         __syncthreads();
-        for (int tap = 0; tap < ks; ++tap) {
+        for (int tap = 0; tap < ((a.flags & 2) ? 0 : ks); ++tap) {
             const int roff = FLAT ? 0 : tap * a.dil;
             for (int kq = 0; kq < kpc; ++kq, ++k) {
                 waitcnt_vm(k + 1 < NK ? 2 : 0);
@@ -205,79 +332,31 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
                 ep[(wt * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
     __syncthreads();
 
-    const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
-    const TOut* AI = reinterpret_cast<const TOut*>(a.acc_in);
-    TOut* Y = reinterpret_cast<TOut*>(a.y);
-    const int ncol = a.ups > 0 ? a.ups * a.Co : a.Co;
-    const long nrows_flat = (long)a.B * a.T_out;
-    const bool vec = (a.Co % 8 == 0) && (a.ldy % 8 == 0) && (!Rp || a.ldr % 8 == 0) && (!AI || a.lda % 8 == 0) &&
-                     (a.bsy % 8 == 0) && (!Rp || a.bsr % 8 == 0) && (!AI || a.bsa % 8 == 0);
-    for (int v = tid; v < BT * (BCO / 8); v += NTHR) {
-        const int tl = v >> 4, cv = v & 15;
-        const int n = blockIdx.y * BCO + cv * 8;
-        if (n >= ncol) continue;
-        long bb, t;
-        if (FLAT) {
-            const long Rr = row0 + tl;
-            if (Rr >= nrows_flat) continue;
-            bb = Rr / a.T_out;
-            t = Rr - bb * a.T_out;
-        } else {
-            bb = bq;
-            t = t0 + tl;
-            if (t >= a.T_out) continue;
-        }
-        int co = n;
-        if (a.ups > 0) {
-            const int p = n / a.Co;
-            co = n - p * a.Co;
-            t = t * a.ups + p - a.ups_pad;
-            if (t < 0 || t >= a.T_final) continue;
-            t += a.refl;
-        }
-        float u[8];
-        const float* er = ep + tl * EP_PITCH + cv * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float x = er[j];
-            if (a.bias) x += (co + j < a.Co || a.ups) ? a.bias[min(co + j, a.Co - 1)] : 0.f;
-            x = act_apply(a.epi_act, x, a.epi_slope, 1.f);
-            if (a.gate) x *= a.gate[bb * a.gate_bs + min(co + j, a.Co - 1)];
-            u[j] = x;
-        }
-        const int ntgt = (a.ups > 0 && a.refl && t == 2) ? 2 : 1;
-        for (int q = 0; q < ntgt; ++q) {
-            const long tt = q == 0 ? t : 0;
-            float o[8];
-            if (vec && co + 8 <= a.Co) {
-                float rr[8], ai[8];
-                if (Rp) load8(Rp + bb * a.bsr + (tt / a.res_tdiv) * a.ldr + co, rr);
-                if (AI) load8(AI + bb * a.bsa + tt * a.lda + co, ai);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    float x = u[j];
-                    if (Rp) x += rr[j];
-                    x *= a.alpha;
-                    if (AI) x += a.beta * ai[j];
-                    o[j] = x;
-                }
-                store8v(Y + bb * a.bsy + tt * a.ldy + co, o);
-            } else {
-                for (int j = 0; j < 8 && co + j < a.Co; ++j) {
-                    float x = u[j];
-                    if (Rp) x += DT<TOut>::ld(Rp + bb * a.bsr + (tt / a.res_tdiv) * a.ldr + co + j);
-                    x *= a.alpha;
-                    if (AI) x += a.beta * DT<TOut>::ld(AI + bb * a.bsa + tt * a.lda + co + j);
-                    DT<TOut>::st(Y + bb * a.bsy + tt * a.ldy + co + j, x);
-                }
-            }
-        }
+    if (a.flags & 4) return;
+    float* c_bias = ep + BT * EP_PITCH;       // [BCO] bias, [BCO] gate (conv mode: one utterance)
+    float* c_gate = c_bias + BCO;
+    if (tid < BCO) {
+        const int n = blockIdx.y * BCO + tid;
+        const int co = a.ups > 0 ? n % a.Co : min(n, a.Co - 1);
+        c_bias[tid] = a.bias ? a.bias[co] : 0.f;
+        c_gate[tid] = (!FLAT && a.gate) ? a.gate[(long)bq * a.gate_bs + co] : 1.f;
+    }
+    __syncthreads();
+    const bool vec = (a.Co % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0) && (!a.acc_in || a.lda % 8 == 0) &&
+                     (a.bsy % 8 == 0) && (!a.res || a.bsr % 8 == 0) && (!a.acc_in || a.bsa % 8 == 0);
+    if (vec) {
+        if (a.res && a.acc_in) epilogue<TOut, FLAT, true, true, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else if (a.res) epilogue<TOut, FLAT, true, true, false>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else if (a.acc_in) epilogue<TOut, FLAT, true, false, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else epilogue<TOut, FLAT, true, false, false>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+    } else {
+        epilogue<TOut, FLAT, false, true, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
     }
 }
 
 size_t lds_bytes(int rows_in, int cic) {
     const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + NSLOT * SLOT_BYTES + 4 * 128 * 4;
-    const size_t epi = (size_t)BT * EP_PITCH * 4;
+    const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4;
     return main > epi ? main : epi;
 }
 

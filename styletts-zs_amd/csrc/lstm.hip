@@ -2,69 +2,98 @@
 // BiLSTMs, the duration LSTM and the shared F0/N LSTM — 520 dependent steps per 5-s utterance.
 //
 // The input projection x W_ih^T + b is one MFMA GEMM over all steps (stzs_conv1d, ks = 1); this
-// kernel runs only the sequential part.  One workgroup per (direction, BB-utterance group);
-// thread j owns hidden unit j: it accumulates its 4 gate rows against h_{t-1} (broadcast from
-// LDS) with the transposed recurrent weights W_hh^T[k][4H] read coalesced across units (the
-// 1 MB fp32 matrix stays L2-resident across steps), updates c and h in registers and publishes
-// h_t to LDS.  One barrier per step; no inter-workgroup traffic.
+// kernel runs only the sequential part.  One workgroup (4 waves) per (direction, 16 utterances):
+// per step gates[16 x 4H] = h_{t-1}[16 x H] W_hh^T on v_mfma_f32_16x16x32_bf16 — h_{t-1} from LDS
+// (A fragments, loaded once per step), W_hh^T streamed from L2 in fragment order (one 1-KB fully
+// coalesced load per 16x32 tile, prefetched one column tile ahead, bf16: 512 KB per step at H=256).
+// Gates go through LDS; each thread updates 16 (utterance, unit) cells with c in registers and
+// publishes h_t (bf16) to LDS and to the output.  Two barriers per step, no inter-workgroup traffic.
 #include "common.hpp"
 
 namespace {
 
-template <int BB>
-__global__ __launch_bounds__(256) void lstm_rec(const stzs_lstm_args a) {
-    __shared__ float hs[2][BB][256];
-    const int j = threadIdx.x;
-    const int dir = blockIdx.y;
-    const int b0 = blockIdx.x * BB;
+constexpr int MB = 16;  // utterances per workgroup (MFMA M)
+
+__global__ __launch_bounds__(256) void lstm_mfma(const stzs_lstm_args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.H, G4 = 4 * a.H;
-    const bool unit = j < H;
-    float c[BB];
-#pragma unroll
-    for (int bb = 0; bb < BB; ++bb) {
-        c[bb] = 0.f;
-        hs[0][bb][j] = 0.f;
-    }
-    const float* Wt = a.whhT + (long)dir * H * G4;
+    const int hp = H + 8;                                    // bf16 pitch of the h tile
+    bf16_t* hs = reinterpret_cast<bf16_t*>(smem);            // [MB][hp]
+    float* gs = reinterpret_cast<float*>(smem + ((MB * hp * 2 + 15) & ~15));  // [MB][G4 + 4]
+    const int gp = G4 + 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int dir = blockIdx.y;
+    const int b0 = blockIdx.x * MB;
+    const int nks = H / 32, nct = G4 / 16;
+    const bf16_t* Wd = reinterpret_cast<const bf16_t*>(a.whhT) + (long)dir * nct * nks * 512;
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
+
+    // cells owned by this thread: (row = e / H, unit = e % H) for e = tid + 256 * i
+    const int ncell = MB * H;
+    const int cpt = (ncell + 255) / 256;
+    float c[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c[i] = 0.f;
+    for (int e = tid; e < MB * hp; e += 256) hs[e] = 0;
     __syncthreads();
+
     for (int s = 0; s < a.T; ++s) {
         const int t = dir == 0 ? s : a.T - 1 - s;
-        const int cur = s & 1;
-        float acc[4][BB];
+        // A fragments of h_{t-1}: row = lane & 15, k = ks*32 + 8*(lane>>4)
+        bf16x8 af[8];
 #pragma unroll
-        for (int bb = 0; bb < BB; ++bb) {
-            const int b = b0 + bb;
+        for (int ks = 0; ks < 8; ++ks)
+            if (ks < nks) af[ks] = *reinterpret_cast<const bf16x8*>(hs + (lane & 15) * hp + ks * 32 + 8 * (lane >> 4));
+        // column tiles of this wave: ct = wave + 4 * i
+        bf16x8 bcur[8], bnxt[8];
+        int ct = wave;
+        if (ct < nct) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-                acc[g][bb] = (unit && b < a.B) ? a.gx[(long)b * a.bsg + (long)t * a.ldg + dir * G4 + g * H + j] : 0.f;
+            for (int ks = 0; ks < 8; ++ks)
+                if (ks < nks) bcur[ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)ct * nks + ks) * 512 + lane * 8);
         }
-        if (unit) {
-#pragma unroll 4
-            for (int k = 0; k < H; ++k) {
-                const float* wr = Wt + (long)k * G4 + j;
-                const float w0 = wr[0], w1 = wr[H], w2 = wr[2 * H], w3 = wr[3 * H];
+        for (; ct < nct; ct += 4) {
+            const int cn = ct + 4;
+            if (cn < nct) {
 #pragma unroll
-                for (int bb = 0; bb < BB; ++bb) {
-                    const float hk = hs[cur][bb][k];
-                    acc[0][bb] += w0 * hk;
-                    acc[1][bb] += w1 * hk;
-                    acc[2][bb] += w2 * hk;
-                    acc[3][bb] += w3 * hk;
-                }
+                for (int ks = 0; ks < 8; ++ks)
+                    if (ks < nks) bnxt[ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)cn * nks + ks) * 512 + lane * 8);
             }
-        }
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int bb = 0; bb < BB; ++bb) {
-            const float ig = 1.f / (1.f + expf(-acc[0][bb]));
-            const float fg = 1.f / (1.f + expf(-acc[1][bb]));
-            const float gg = tanhf(acc[2][bb]);
-            const float og = 1.f / (1.f + expf(-acc[3][bb]));
-            c[bb] = fg * c[bb] + ig * gg;
-            const float h = og * tanhf(c[bb]);
-            hs[cur ^ 1][bb][j] = unit ? h : 0.f;
-            const int b = b0 + bb;
-            if (unit && b < a.B) Y[(long)b * a.bsy + (long)t * a.ldy + dir * H + j] = f2bf(h);
+            for (int ks = 0; ks < 8; ++ks)
+                if (ks < nks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bcur[ks], acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gs[((lane >> 4) * 4 + r) * gp + ct * 16 + (lane & 15)] = acc[r];
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) bcur[ks] = bnxt[ks];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (i >= cpt) break;
+            const int e = tid + 256 * i;
+            if (e >= ncell) break;
+            const int row = e / H, j = e - row * H;
+            const int b = b0 + row;
+            float gi = gs[row * gp + j], gf = gs[row * gp + H + j], gg = gs[row * gp + 2 * H + j],
+                  go = gs[row * gp + 3 * H + j];
+            if (b < a.B) {
+                const float* gx = a.gx + (long)b * a.bsg + (long)t * a.ldg + dir * G4;
+                gi += gx[j];
+                gf += gx[H + j];
+                gg += gx[2 * H + j];
+                go += gx[3 * H + j];
+            }
+            const float ig = 1.f / (1.f + __expf(-gi));
+            const float fg = 1.f / (1.f + __expf(-gf));
+            const float cg = tanhf(gg);
+            const float og = 1.f / (1.f + __expf(-go));
+            c[i] = fg * c[i] + ig * cg;
+            const float h = og * tanhf(c[i]);
+            const bf16_t hb = f2bf(h);
+            hs[row * hp + j] = hb;
+            if (b < a.B) Y[(long)b * a.bsy + (long)t * a.ldy + dir * H + j] = hb;
         }
         __syncthreads();
     }
@@ -74,16 +103,15 @@ __global__ __launch_bounds__(256) void lstm_rec(const stzs_lstm_args a) {
 
 extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     if (!a || !a->gx || !a->whhT || !a->y) return STZS_EINVAL;
-    if (a->B <= 0 || a->T <= 0 || a->H <= 0 || a->H > 256 || (a->ndir != 1 && a->ndir != 2)) return STZS_ESHAPE;
+    if (a->B <= 0 || a->T <= 0 || a->H <= 0 || a->H > 256 || a->H % 32 || (a->ndir != 1 && a->ndir != 2))
+        return STZS_ESHAPE;
+    if (MB * a->H > 256 * 16) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int thr = ((a->H + 63) / 64) * 64;
-    if (a->B >= 8) {
-        hipLaunchKernelGGL(lstm_rec<8>, dim3((a->B + 7) / 8, a->ndir), dim3(thr), 0, s, *a);
-    } else if (a->B >= 4) {
-        hipLaunchKernelGGL(lstm_rec<4>, dim3((a->B + 3) / 4, a->ndir), dim3(thr), 0, s, *a);
-    } else {
-        hipLaunchKernelGGL(lstm_rec<1>, dim3(a->B, a->ndir), dim3(thr), 0, s, *a);
-    }
+    const int hp = a->H + 8;
+    const size_t lds = ((MB * hp * 2 + 15) & ~15) + (size_t)MB * (4 * a->H + 4) * 4;
+    auto k = lstm_mfma;
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, dim3((a->B + MB - 1) / MB, a->ndir), dim3(256), lds, s, *a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

@@ -146,7 +146,7 @@ class StyleTTSZS:
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
-             T_final=0, refl=0, what="conv"):
+             T_final=0, refl=0, flags=0, what="conv"):
         W = self.W
         a = L.ConvArgs()
         a.x, a.w, a.y = x.ptr, self._t(cw.w).data_ptr(), y.ptr
@@ -178,6 +178,7 @@ class StyleTTSZS:
         if gate is not None:
             a.gate, a.gate_bs = gate, gate_bs
         a.alpha, a.beta, a.epi_act, a.epi_slope = alpha, beta, epi_act, epi_slope
+        a.flags = flags
         tm = self.timer
         if tm is not None and what in tm["tags"]:
             e0 = torch.cuda.Event(enable_timing=True)

@@ -162,8 +162,16 @@ def pack_lstm(A: Arena, name, P) -> LstmW:
     wih = torch.cat([P[name + ".w_ih"], P[name + ".w_ih_rev"]], 0)
     bias = torch.cat([P[name + ".b_ih"] + P[name + ".b_hh"], P[name + ".b_ih_rev"] + P[name + ".b_hh_rev"]], 0)
     ih = pack_conv(A, name + ".ih", wih, bias)
-    whhT = torch.stack([P[name + ".w_hh"].t(), P[name + ".w_hh_rev"].t()], 0).contiguous().float()
-    return LstmW(ih, A.add(name + ".whhT", whhT), H)
+    frags = torch.stack([lstm_frags(P[name + ".w_hh"]), lstm_frags(P[name + ".w_hh_rev"])], 0)
+    return LstmW(ih, A.add(name + ".whhT", frags.to(torch.bfloat16)), H)
+
+
+def lstm_frags(w_hh: torch.Tensor) -> torch.Tensor:
+    """W_hh [4H, H] -> W_hh^T as 16x16x32 B fragments [4H/16][H/32][64 lanes][8]:
+    lane l, element j holds W_hh[n = ct*16 + (l & 15)][k = ks*32 + 8*(l >> 4) + j] (csrc/lstm.hip)."""
+    G4, H = w_hh.shape
+    t = w_hh.reshape(G4 // 16, 16, H // 32, 4, 8).permute(0, 2, 3, 1, 4)
+    return t.reshape(G4 // 16, H // 32, 64, 8).contiguous()
 
 
 def blk_norms(prefix):
