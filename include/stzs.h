@@ -35,6 +35,9 @@ extern "C" {
 enum { STZS_F32 = 0, STZS_BF16 = 1, STZS_I32 = 2 };
 enum { STZS_ACT_NONE = 0, STZS_ACT_LEAKY = 1, STZS_ACT_SNAKE = 2, STZS_ACT_GELU = 3, STZS_ACT_SILU = 4 };
 enum { STZS_PRO_NONE = 0, STZS_PRO_ADAIN = 1 };
+/* stzs_conv_args.flags: the caller guarantees that for a ks=1 bf16 linear every input row can be
+ * read over [0, ci_pad) channels (row padding inside the buffer) -> A streams by LDS-DMA */
+#define STZS_CONV_A_DMA 8
 
 /* ---- library ---- */
 int stzs_init(int device);

@@ -161,6 +161,9 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
     }
 }
 
+template <typename TOut, bool FLAT>
+STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[4][4], unsigned char* smem, int bq, int t0, long row0);
+
 template <typename TIn, typename TOut, bool FLAT, int PACT>
 __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -320,7 +323,14 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         }
     }
 
-    // ---- epilogue through LDS ----
+    finish<TOut, FLAT>(a, acc, smem, bq, t0, row0);
+}
+
+// Accumulators -> LDS (fp32, padded rows) -> vectorised fused epilogue.
+template <typename TOut, bool FLAT>
+STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[4][4], unsigned char* smem, int bq, int t0, long row0) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wt = wave >> 1, wc = wave & 1;
     __syncthreads();
     float* ep = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -330,8 +340,6 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 ep[(wt * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
-    __syncthreads();
-
     if (a.flags & 4) return;
     float* c_bias = ep + BT * EP_PITCH;       // [BCO] bias, [BCO] gate (conv mode: one utterance)
     float* c_gate = c_bias + BCO;
@@ -354,6 +362,85 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     }
 }
 
+STZS_DEV void glds16(const void* src, void* dst) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// Pure GEMM for bf16 linears (ks = 1, no prologue): BOTH operands stream through LDS-DMA rings,
+// one 32-wide K-step per slot (A: 128 rows x 32 k, B: 128 cols x 32 k, 8 KB each), two K-steps in
+// flight.  The A image takes the same XOR swizzle as B through its per-lane SOURCE addresses
+// (LDS-DMA writes lane-linearly), so both fragment reads are conflict-free ds_read_b128.
+template <typename TOut>
+__global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* ringA = smem;
+    unsigned char* ringB = smem + NSLOT * SLOT_BYTES;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wt = wave >> 1, wc = wave & 1;
+    const long row0 = (long)blockIdx.x * BT;
+    const long nR = (long)a.B * a.T_in;
+    const int NK = a.ci_pad >> 5;
+    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
+    const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x);
+    long asrc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int o = wave * 2048 + i * 1024 + lane * 16;
+        const int r = o >> 6, p = (o >> 4) & 3;
+        long R = row0 + r;
+        R = R < nR ? R : nR - 1;
+        const long bb = R / a.T_in;
+        asrc[i] = bb * a.bsx + (R - bb * a.T_in) * a.ldx + ((p ^ gswz(r)) << 3);
+    }
+    auto fill = [&](int k) {
+        const bf16_t* src = Wt + (long)k * (BCO * 32) + wave * 1024 + lane * 8;
+        unsigned char* db = ringB + (k % NSLOT) * SLOT_BYTES + wave * 2048;
+        unsigned char* da = ringA + (k % NSLOT) * SLOT_BYTES + wave * 2048;
+        glds16(src, db);
+        glds16(src + 512, db + 1024);
+        glds16(X + asrc[0] + k * 32, da);
+        glds16(X + asrc[1] + k * 32, da + 1024);
+    };
+    int aoff[4], boff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int ra = wt * 64 + i * 16 + (lane & 15);
+        aoff[i] = ra * 64 + (((lane >> 4) ^ gswz(ra)) << 4);
+        const int rb = wc * 64 + i * 16 + (lane & 15);
+        boff[i] = rb * 64 + (((lane >> 4) ^ gswz(rb)) << 4);
+    }
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    fill(0);
+    if (NK > 1) fill(1);
+    for (int k = 0; k < ((a.flags & 2) ? 0 : NK); ++k) {
+        if (k + 1 < NK)
+            __builtin_amdgcn_s_waitcnt(0x0F70 | 4);
+        else
+            __builtin_amdgcn_s_waitcnt(0x0F70 | 0);
+        __builtin_amdgcn_s_barrier();
+        if (k + 2 < NK) fill(k + 2);
+        const unsigned char* sa = ringA + (k % NSLOT) * SLOT_BYTES;
+        const unsigned char* sb = ringB + (k % NSLOT) * SLOT_BYTES;
+        bf16x8 af[4], bw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sa + aoff[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bw[i] = *reinterpret_cast<const bf16x8*>(sb + boff[i]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bw[nt], acc[mt][nt], 0, 0, 0);
+    }
+    finish<TOut, true>(a, acc, smem, 0, 0, row0);
+}
+
 size_t lds_bytes(int rows_in, int cic) {
     const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + NSLOT * SLOT_BYTES + 4 * 128 * 4;
     const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4;
@@ -371,6 +458,14 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
                              : (unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT);
     dim3 grid(gx, a.co_pad / BCO);
     void (*k)(stzs_conv_args);
+    if (flat && sizeof(TIn) == 2 && (a.flags & STZS_CONV_A_DMA) && a.pro_cscale == 1.f) {
+        const size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4;
+        auto kg = gemm_glds<TOut>;
+        (void)hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);
+        hipLaunchKernelGGL(kg, grid, dim3(NTHR), lg, s, a);
+        STZS_LAUNCH_CHECK();
+        return STZS_OK;
+    }
     if (flat)
         k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE>;
     else if (a.pro_act == STZS_ACT_SNAKE)

@@ -178,6 +178,9 @@ class StyleTTSZS:
         if gate is not None:
             a.gate, a.gate_bs = gate, gate_bs
         a.alpha, a.beta, a.epi_act, a.epi_slope = alpha, beta, epi_act, epi_slope
+        if (cw.ks == 1 and stride == 1 and pad == 0 and not cw.ups and pro is None and pro_act == L.ACT_NONE
+                and cscale == 1.0 and x.t.dtype == torch.bfloat16 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
+            flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
         a.flags = flags
         tm = self.timer
         if tm is not None and what in tm["tags"]:
