@@ -122,14 +122,20 @@ int stzs_attention(const stzs_attn_args* a, void* stream);
  * gx [B, T, ldg] f32 holds x W_ih^T + b_ih + b_hh for both directions (fwd 4H | rev 4H, gate
  * order i,f,g,o); whhT = W_hh^T as bf16 16x16x32 B fragments [2][4H/16][H/32][64][8]
  * (stzs/weights.py lstm_frags); H % 32 == 0, H <= 256; h written bf16 to y[b, t, dir*H + j].
+ * Launches H/32 x ndir x ceil(B/64) co-resident workgroups that exchange h_t every step through
+ * `xchg` (write-through stores + agent-scope arrival counters in `sync`); spins are bounded and a
+ * timeout sets the last word of `sync` instead of hanging.
  * (DurationEncoder BiLSTMs, duration LSTM, shared LSTM) */
 typedef struct stzs_lstm_args {
     const float* gx;
-    const float* whhT;
+    const void* whhT;
     void* y;
+    void* xchg;  /* workspace: stzs_lstm_workspace(B, H, ndir) bytes, zero-initialised once */
+    void* sync;  /* workspace: 4096 bytes of arrival counters (zeroed by the call itself) */
     int64_t ldg, bsg, ldy, bsy;
     int32_t B, T, H, ndir;
 } stzs_lstm_args;
+size_t stzs_lstm_workspace(int B, int H, int ndir);
 int stzs_lstm(const stzs_lstm_args* a, void* stream);
 
 /* ---- predictor glue ---- */

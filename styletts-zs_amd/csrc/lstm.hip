@@ -1,117 +1,187 @@
 // LSTM recurrence of the prosody predictor: the 3 DurationEncoder
 // BiLSTMs, the duration LSTM and the shared F0/N LSTM — 520 dependent steps per 5-s utterance.
 //
-// The input projection x W_ih^T + b is one MFMA GEMM over all steps (stzs_conv1d, ks = 1); this
-// kernel runs only the sequential part.  One workgroup (4 waves) per (direction, 16 utterances):
-// per step gates[16 x 4H] = h_{t-1}[16 x H] W_hh^T on v_mfma_f32_16x16x32_bf16 — h_{t-1} from LDS
-// (A fragments, loaded once per step), W_hh^T streamed from L2 in fragment order (one 1-KB fully
-// coalesced load per 16x32 tile, prefetched one column tile ahead, bf16: 512 KB per step at H=256).
-// Gates go through LDS; each thread updates 16 (utterance, unit) cells with c in registers and
-// publishes h_t (bf16) to LDS and to the output.  Two barriers per step, no inter-workgroup traffic.
+// The input projection x W_ih^T + b is one MFMA GEMM over all steps (stzs_conv1d); this kernel
+// runs only the sequential part, latency-bound by construction.  Design (weights never move):
+//   * per (direction, group of <= 64 utterances) the 4H gate columns are split over P = H/32
+//     workgroups; workgroup p owns hidden units [32p, 32p + 32) = 128 gate columns, and each of its
+//     4 waves keeps ITS gate's 2 x (H/32) W_hh^T B-fragments in REGISTERS for the whole launch;
+//   * per step: h_{t-1} [<=64 x H] (bf16) is read from a double-buffered exchange slab with
+//     write-through (sc1) loads into an LDS A tile, 16x16x32 MFMAs give the gate pre-activations,
+//     gates meet in LDS, each thread updates 8 (utterance, unit) cells (c in registers) and
+//     publishes its h with write-through 8-B stores;
+//   * hand-off (MI355X guide, Guideline 16 'Valid forms' table row 1): every storing wave drains
+//     vmcnt(0), workgroup barrier, ONE lane adds to the direction's agent-scope arrival counter;
+//     consumers poll that counter with sc1 loads, then all loads of the slab are sc1 (no fences).
+//     Spins are bounded: on timeout the kernel records an error word and finishes (never hangs).
+// Residency: grid = P x ndir x groups <= 64 workgroups, one per CU: always co-resident on MI355X.
 #include "common.hpp"
 
 namespace {
 
-constexpr int MB = 16;  // utterances per workgroup (MFMA M)
+constexpr int MROWS = 64;   // utterances per group (4 MFMA row tiles)
+constexpr int UNITS = 32;   // hidden units per workgroup
+constexpr unsigned SPIN_LIMIT = 1u << 22;
 
-__global__ __launch_bounds__(256) void lstm_mfma(const stzs_lstm_args a) {
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+STZS_DEV unsigned poll_ge(gu32* ctr, unsigned target, gu32* err) {
+    unsigned v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (v < target) {
+        __builtin_amdgcn_s_sleep(1);
+        v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (++spins > SPIN_LIMIT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return 0;
+        }
+    }
+    return 1;
+}
+
+template <int NKS>
+__global__ __launch_bounds__(256, 1) void lstm_xchg(const stzs_lstm_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int H = a.H, G4 = 4 * a.H;
-    const int hp = H + 8;                                    // bf16 pitch of the h tile
-    bf16_t* hs = reinterpret_cast<bf16_t*>(smem);            // [MB][hp]
-    float* gs = reinterpret_cast<float*>(smem + ((MB * hp * 2 + 15) & ~15));  // [MB][G4 + 4]
-    const int gp = G4 + 4;
+    const int H = a.H, G4 = 4 * H;
+    const int hp = H + 8;
+    bf16_t* As = reinterpret_cast<bf16_t*>(smem);                                   // [64][hp]
+    float* gs = reinterpret_cast<float*>(smem + ((MROWS * hp * 2 + 15) & ~15));     // [64][4*UNITS + 4]
+    __shared__ int s_ok;
+    const int gp = 4 * UNITS + 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int dir = blockIdx.y;
-    const int b0 = blockIdx.x * MB;
-    const int nks = H / 32, nct = G4 / 16;
-    const bf16_t* Wd = reinterpret_cast<const bf16_t*>(a.whhT) + (long)dir * nct * nks * 512;
-    bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
+    const int p = blockIdx.x, dir = blockIdx.y, grp = blockIdx.z;
+    const int P = H / UNITS;
+    const int b0 = grp * MROWS;
+    const int nrows = min(MROWS, a.B - b0);
+    const int nmt = (nrows + 15) >> 4;
+    // exchange slab [group][dir][2][64][H] bf16, counters [group][dir] (16 words apart)
+    bf16_t* X = reinterpret_cast<bf16_t*>(a.xchg) + ((long)(grp * a.ndir + dir) * 2) * MROWS * H;
+    gu32* ctr = (gu32*)(a.sync) + (grp * a.ndir + dir) * 16;
+    gu32* err = (gu32*)(a.sync) + 1023;
 
-    // cells owned by this thread: (row = e / H, unit = e % H) for e = tid + 256 * i
-    const int ncell = MB * H;
-    const int cpt = (ncell + 255) / 256;
-    float c[16];
+    // W_hh^T fragments of this wave's gate (g = wave) for the workgroup's 32 units, in registers
+    const bf16_t* Wd = reinterpret_cast<const bf16_t*>(a.whhT) + (long)dir * (G4 / 16) * NKS * 512;
+    bf16x8 bw[2][NKS];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) c[i] = 0.f;
-    for (int e = tid; e < MB * hp; e += 256) hs[e] = 0;
-    __syncthreads();
+    for (int c = 0; c < 2; ++c) {
+        const int ct = (wave * H + p * UNITS) / 16 + c;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) bw[c][ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)ct * NKS + ks) * 512 + lane * 8);
+    }
+    // cells of this thread: row = tid / 4, units (tid % 4) * 8 .. +8
+    const int crow = tid >> 2, cu0 = (tid & 3) * 8;
+    const bool cvalid = crow < nrows;
+    const int cb = b0 + (cvalid ? crow : 0);
+    float c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = 0.f;
+    bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
+    if (tid == 0) s_ok = 1;
 
     for (int s = 0; s < a.T; ++s) {
         const int t = dir == 0 ? s : a.T - 1 - s;
-        // A fragments of h_{t-1}: row = lane & 15, k = ks*32 + 8*(lane>>4)
-        bf16x8 af[8];
+        // gate input projections of this thread's cells (issued early, consumed after the MFMAs)
+        float gx[4][8];
+        const float* G = a.gx + (long)cb * a.bsg + (long)t * a.ldg + dir * G4 + p * UNITS + cu0;
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
-            if (ks < nks) af[ks] = *reinterpret_cast<const bf16x8*>(hs + (lane & 15) * hp + ks * 32 + 8 * (lane >> 4));
-        // column tiles of this wave: ct = wave + 4 * i
-        bf16x8 bcur[8], bnxt[8];
-        int ct = wave;
-        if (ct < nct) {
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks)
-                if (ks < nks) bcur[ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)ct * nks + ks) * 512 + lane * 8);
-        }
-        for (; ct < nct; ct += 4) {
-            const int cn = ct + 4;
-            if (cn < nct) {
-#pragma unroll
-                for (int ks = 0; ks < 8; ++ks)
-                    if (ks < nks) bnxt[ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)cn * nks + ks) * 512 + lane * 8);
+        for (int g = 0; g < 4; ++g) load8(G + g * H, gx[g]);
+        // ---- wait for h_{s-1} from all P workgroups, stage it into the A tile ----
+        if (s == 0) {
+            for (int e = tid; e < MROWS * hp / 8; e += 256) reinterpret_cast<uint4*>(As)[e] = make_uint4(0, 0, 0, 0);
+        } else {
+            if (tid == 0 && s_ok) s_ok = poll_ge(ctr, (unsigned)(P * s), err);  // after a timeout: no more spins
+            __syncthreads();
+            gu64* src = (gu64*)(X + (long)((s - 1) & 1) * MROWS * H);
+            const int n8 = MROWS * H / 4;  // 8-byte words
+            for (int e = tid; e < n8; e += 256) {
+                const unsigned long long v = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int r = (e * 4) / H, k = (e * 4) - r * H;
+                *reinterpret_cast<unsigned long long*>(As + r * hp + k) = v;
             }
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks)
-                if (ks < nks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bcur[ks], acc, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) gs[((lane >> 4) * 4 + r) * gp + ct * 16 + (lane & 15)] = acc[r];
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) bcur[ks] = bnxt[ks];
         }
         __syncthreads();
+        // ---- gates of this wave's gate g = wave for all rows: [64 x 32 units] ----
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if (i >= cpt) break;
-            const int e = tid + 256 * i;
-            if (e >= ncell) break;
-            const int row = e / H, j = e - row * H;
-            const int b = b0 + row;
-            float gi = gs[row * gp + j], gf = gs[row * gp + H + j], gg = gs[row * gp + 2 * H + j],
-                  go = gs[row * gp + 3 * H + j];
-            if (b < a.B) {
-                const float* gx = a.gx + (long)b * a.bsg + (long)t * a.ldg + dir * G4;
-                gi += gx[j];
-                gf += gx[H + j];
-                gg += gx[2 * H + j];
-                go += gx[3 * H + j];
+        for (int mt = 0; mt < 4; ++mt) {
+            if (mt >= nmt) break;
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (mt * 16 + (lane & 15)) * hp + ks * 32 + 8 * (lane >> 4));
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[0][ks], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[1][ks], acc1, 0, 0, 0);
             }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = mt * 16 + (lane >> 4) * 4 + r;
+                gs[row * gp + wave * UNITS + (lane & 15)] = acc0[r];
+                gs[row * gp + wave * UNITS + 16 + (lane & 15)] = acc1[r];
+            }
+        }
+        __syncthreads();
+        // ---- cell update, publish h ----
+        float hv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float* gr = gs + crow * gp + cu0 + j;
+            const float gi = gr[0] + gx[0][j], gf = gr[UNITS] + gx[1][j], gg = gr[2 * UNITS] + gx[2][j],
+                        go = gr[3 * UNITS] + gx[3][j];
             const float ig = 1.f / (1.f + __expf(-gi));
             const float fg = 1.f / (1.f + __expf(-gf));
-            const float cg = tanhf(gg);
             const float og = 1.f / (1.f + __expf(-go));
-            c[i] = fg * c[i] + ig * cg;
-            const float h = og * tanhf(c[i]);
-            const bf16_t hb = f2bf(h);
-            hs[row * hp + j] = hb;
-            if (b < a.B) Y[(long)b * a.bsy + (long)t * a.ldy + dir * H + j] = hb;
+            c[j] = fg * c[j] + ig * tanhf(gg);
+            hv[j] = og * tanhf(c[j]);
         }
+        const uint4 hb = pack8(hv);
+        if (cvalid) {
+            *reinterpret_cast<uint4*>(Y + (long)cb * a.bsy + (long)t * a.ldy + dir * H + p * UNITS + cu0) = hb;
+            gu64* dst = (gu64*)(X + (long)(s & 1) * MROWS * H + crow * H + p * UNITS + cu0);
+            __hip_atomic_store(dst, ((unsigned long long)hb.y << 32) | hb.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + 1, ((unsigned long long)hb.w << 32) | hb.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 }  // namespace
 
+extern "C" size_t stzs_lstm_workspace(int B, int H, int ndir) {
+    const int groups = (B + MROWS - 1) / MROWS;
+    return (size_t)groups * ndir * 2 * MROWS * H * sizeof(bf16_t);
+}
+
 extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
-    if (!a || !a->gx || !a->whhT || !a->y) return STZS_EINVAL;
-    if (a->B <= 0 || a->T <= 0 || a->H <= 0 || a->H > 256 || a->H % 32 || (a->ndir != 1 && a->ndir != 2))
+    if (!a || !a->gx || !a->whhT || !a->y || !a->xchg || !a->sync) return STZS_EINVAL;
+    if (a->B <= 0 || a->T <= 0 || a->H <= 0 || a->H > 256 || a->H % UNITS || (a->ndir != 1 && a->ndir != 2))
         return STZS_ESHAPE;
-    if (MB * a->H > 256 * 16) return STZS_ESHAPE;
+    if (a->ldg % 8 || a->bsg % 8 || a->ldy % 8 || a->bsy % 8) return STZS_ESHAPE;
+    const int groups = (a->B + MROWS - 1) / MROWS;
+    const int P = a->H / UNITS;
+    if (groups * a->ndir > 63 || P * a->ndir * groups > 256) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // counters (and the error word) zeroed per call: a memset node under graph capture
+    if (hipMemsetAsync(a->sync, 0, 4096, s) != hipSuccess) return STZS_EHIP;
     const int hp = a->H + 8;
-    const size_t lds = ((MB * hp * 2 + 15) & ~15) + (size_t)MB * (4 * a->H + 4) * 4;
-    auto k = lstm_mfma;
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k, dim3((a->B + MB - 1) / MB, a->ndir), dim3(256), lds, s, *a);
+    const size_t lds = ((MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4;
+    dim3 grid(P, a->ndir, groups);
+    switch (a->H / 32) {
+#define STZS_LSTM_CASE(n)                                                                                   \
+    case n: {                                                                                               \
+        auto k = lstm_xchg<n>;                                                                              \
+        if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+        hipLaunchKernelGGL(k, grid, dim3(256), lds, s, *a);                                                 \
+        break;                                                                                              \
+    }
+        STZS_LSTM_CASE(1)
+        STZS_LSTM_CASE(2)
+        STZS_LSTM_CASE(4)
+        STZS_LSTM_CASE(8)
+#undef STZS_LSTM_CASE
+        default: return STZS_ESHAPE;
+    }
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

@@ -53,7 +53,7 @@ class AttnArgs(C.Structure):
 
 
 class LstmArgs(C.Structure):
-    _fields_ = [("gx", vp), ("whhT", vp), ("y", vp),
+    _fields_ = [("gx", vp), ("whhT", vp), ("y", vp), ("xchg", vp), ("sync", vp),
                 ("ldg", i64), ("bsg", i64), ("ldy", i64), ("bsy", i64),
                 ("B", i32), ("T", i32), ("H", i32), ("ndir", i32)]
 
@@ -110,7 +110,7 @@ class CopyArgs(C.Structure):
 
 # every exported symbol of include/stzs.h (tests check the .so exports exactly these)
 EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_chan_stats_workspace",
-           "stzs_chan_stats", "stzs_row_layernorm", "stzs_attention", "stzs_lstm", "stzs_predictor_prep",
+           "stzs_chan_stats", "stzs_row_layernorm", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_dn_cond", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed"]
@@ -141,6 +141,7 @@ def load():
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
         "stzs_row_layernorm": ([P(RowLNArgs), vp], i32),
         "stzs_attention": ([P(AttnArgs), vp], i32),
+        "stzs_lstm_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_lstm": ([P(LstmArgs), vp], i32),
         "stzs_predictor_prep": ([P(PrPrepArgs), vp], i32),
         "stzs_durations": ([P(DurArgs), vp], i32),

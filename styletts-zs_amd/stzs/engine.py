@@ -250,6 +250,10 @@ class StyleTTSZS:
         self.conv(lw.ih, x, gx, what=key + ".ih")
         a = L.LstmArgs()
         a.gx, a.whhT, a.y = gx.ptr, self._t(lw.whhT).data_ptr(), y.ptr
+        nx = self.lib.stzs_lstm_workspace(x.B, lw.H, 2)
+        xchg = self.buf("lstm.xchg", (max(nx, 16),), torch.uint8, zero=True)
+        sync = self.buf("lstm.sync", (4096,), torch.uint8, zero=True)
+        a.xchg, a.sync = xchg.data_ptr(), sync.data_ptr()
         a.ldg, a.bsg, a.ldy, a.bsy = gx.ld, gx.bs, y.ld, y.bs
         a.B, a.T, a.H, a.ndir = x.B, x.T, lw.H, 2
         self._call(self.lib.stzs_lstm, a, key + ".rec")
