@@ -1,0 +1,100 @@
+"""C-ABI checks that need no GPU: the library loads, exports exactly what include/stzs.h declares,
+the ctypes structures match the C layouts (sizeof/offsetof compiled with gcc from the header), and
+error codes are named.  No compute call is made here."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import ROOT
+
+
+def _header():
+    return open(os.path.join(ROOT, "include", "stzs.h")).read()
+
+
+def test_library_exports_every_declared_symbol():
+    from stzs import _lib
+    decl = set(re.findall(r"\b(stzs_[a-z0-9_]+)\s*\(", _header()))
+    assert decl == set(_lib.EXPORTS), decl ^ set(_lib.EXPORTS)
+    L = _lib.load()
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\b(stzs_[a-z0-9_]+)\b", nm))
+    assert decl <= exported, decl - exported
+    for s in decl:
+        getattr(L, s)
+
+
+def test_strerror_and_version():
+    from stzs import _lib
+    L = _lib.load()
+    assert L.stzs_version() >= 1
+    assert _lib.strerror(0) == "ok"
+    for rc in (-1, -2, -3, -4):
+        assert _lib.strerror(rc).startswith("STZS_E")
+
+
+def test_workspace_queries():
+    from stzs import _lib
+    L = _lib.load()
+    assert L.stzs_chan_stats_workspace(64, 24001, 128) == 64 * 94 * 128 * 8
+    assert L.stzs_lstm_workspace(64, 256, 2) == 2 * 2 * 64 * 256 * 2
+
+
+STRUCTS = {
+    "stzs_conv_args": "ConvArgs", "stzs_stats_args": "StatsArgs", "stzs_rowln_args": "RowLNArgs",
+    "stzs_attn_args": "AttnArgs", "stzs_lstm_args": "LstmArgs", "stzs_prprep_args": "PrPrepArgs",
+    "stzs_dur_args": "DurArgs", "stzs_align_args": "AlignArgs", "stzs_gather_args": "GatherArgs",
+    "stzs_dwup_args": "DwupArgs", "stzs_f0n_args": "F0nArgs", "stzs_source_args": "SourceArgs",
+    "stzs_istft_args": "IstftArgs", "stzs_copy_args": "CopyArgs",
+}
+
+
+def test_ctypes_structs_match_c_layout():
+    """compile a probe with gcc against include/stzs.h and compare sizeof + every field offset."""
+    from stzs import _lib
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "stzs.h"', "int main(void){"]
+    for cname, pyname in STRUCTS.items():
+        py = getattr(_lib, pyname)
+        lines.append(f'printf("{pyname} size %zu\\n", sizeof({cname}));')
+        for f, _t in py._fields_:
+            lines.append(f'printf("{pyname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "probe.c"), os.path.join(d, "probe")
+        open(src, "w").write("\n".join(lines))
+        r = subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), src, "-o", exe], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        out = subprocess.run([exe], capture_output=True, text=True).stdout.split("\n")
+    got = {}
+    for ln in out:
+        if ln.strip():
+            a, b, c = ln.split()
+            got[(a, b)] = int(c)
+    for cname, pyname in STRUCTS.items():
+        py = getattr(_lib, pyname)
+        assert got[(pyname, "size")] == C.sizeof(py), pyname
+        for f, _t in py._fields_:
+            assert got[(pyname, f)] == getattr(py, f).offset, (pyname, f)
+
+
+def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
+    """the product path refuses to run without the HIP library (no silent CPU fallback)."""
+    import importlib
+    from stzs import _lib
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.StzsError):
+        _lib.load()
+    importlib.reload(_lib)
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, "styletts-zs_amd", "stzs")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f
