@@ -1,100 +1,140 @@
-// Denoiser multi-head attention: self-attention over the L_s = 50 style
-// codes and cross-attention to [text ; prompt] context (T_txt + 50 keys).  These are tiny
-// (Lq = 50, Lk <= ~530, dh = 64) and latency-bound, so v1 is an fp32-FMA online-softmax kernel:
-// one workgroup per (row, head, 16 queries); keys streamed through LDS in 128-key chunks
-// (bf16, 16-B padded rows); one lane per key for QK^T, one lane per head-dim for PV.
+// Denoiser multi-head attention: self-attention over the L_s = 50 style codes
+// and cross-attention to [text ; prompt] context (T_txt + 50 keys), head dim 64.
+//
+// Flash-style on v_mfma_f32_16x16x32_bf16: one workgroup (4 waves) per (row, head, 64 queries), one
+// wave per 16 queries.  Keys stream through LDS in 64-key chunks: K as rows (B operand of S = Q K^T),
+// V transposed (B operand of O = P V), both 16-B padded.  Online softmax in fp32 on the accumulator
+// layout (row max / sum by in-register max + 16-lane xor shuffles); P goes C-layout -> A-layout through
+// a per-wave bf16 LDS tile.  Q fragments come straight from global memory (read once).
 #include "common.hpp"
 
 namespace {
 
-constexpr int KC = 128;  // keys per LDS chunk
-constexpr int QB = 16;   // queries per workgroup (4 per wave)
+constexpr int KC = 64;  // keys per chunk
 
 template <int DH>
-__global__ __launch_bounds__(256) void attn_fwd(const stzs_attn_args a) {
-    constexpr int KP = DH + 8;
-    __shared__ __attribute__((aligned(16))) bf16_t Ks[KC][KP];
-    __shared__ __attribute__((aligned(16))) bf16_t Vs[KC][KP];
-    __shared__ float Qs[QB][DH];
-    __shared__ float Ps[4][4][KC];
+__global__ __launch_bounds__(256) void attn_mfma(const stzs_attn_args a) {
+    constexpr int NKS = DH / 32;   // k-steps of S
+    constexpr int NDT = DH / 16;   // d tiles of O
+    constexpr int KP = DH + 8;     // K row pitch (bf16)
+    constexpr int VP = KC + 8;     // V^T row pitch
+    constexpr int PP = KC + 8;     // P row pitch
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[KC * KP];
+    __shared__ __attribute__((aligned(16))) bf16_t Vt[DH * VP];
+    __shared__ __attribute__((aligned(16))) bf16_t Ps[4][16 * PP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long r = blockIdx.x;
-    const int h = blockIdx.y, q0 = blockIdx.z * QB;
+    const int h = blockIdx.y;
+    const int qb = blockIdx.z * 64 + wave * 16;
     const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + r * a.bsq + h * DH;
     const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + r * a.bsk + h * DH;
     const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + r * a.bsv + h * DH;
     const float scale = 1.f / sqrtf((float)DH);
-    for (int i = tid; i < QB * DH; i += 256) {
-        const int qi = i / DH, d = i - qi * DH;
-        Qs[qi][d] = (q0 + qi < a.Lq) ? bf2f(Q[(long)(q0 + qi) * a.ldq + d]) * scale : 0.f;
-    }
-    float m[4], l[4], o[4];
+
+    bf16x8 qf[NKS];
+    {
+        const int qr = min(qb + (lane & 15), a.Lq - 1);
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-        m[qq] = -INFINITY;
-        l[qq] = 0.f;
-        o[qq] = 0.f;
+        for (int ks = 0; ks < NKS; ++ks)
+            qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (long)qr * a.ldq + ks * 32 + 8 * (lane >> 4));
     }
-    constexpr int VPR = DH / 8;
+    f32x4 o[NDT];
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        m[i] = -INFINITY;
+        l[i] = 0.f;
+    }
+    bf16_t* P = Ps[wave];
+
     for (int c0 = 0; c0 < a.Lk; c0 += KC) {
         __syncthreads();
-        for (int i = tid; i < KC * VPR; i += 256) {
-            const int kr = i / VPR, cv = i - kr * VPR;
-            uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-            if (c0 + kr < a.Lk) {
-                kv = *reinterpret_cast<const uint4*>(K + (long)(c0 + kr) * a.ldk + cv * 8);
-                vv = *reinterpret_cast<const uint4*>(V + (long)(c0 + kr) * a.ldv + cv * 8);
-            }
-            *reinterpret_cast<uint4*>(&Ks[kr][cv * 8]) = kv;
-            *reinterpret_cast<uint4*>(&Vs[kr][cv * 8]) = vv;
-        }
-        __syncthreads();
-        float s[4][2];
+        // stage K rows and V^T for keys [c0, c0 + KC)
+        for (int i = tid; i < KC * (DH / 8); i += 256) {
+            const int kr = i / (DH / 8), cv = i - kr * (DH / 8);
+            const bool ok = c0 + kr < a.Lk;
+            const int kk = ok ? c0 + kr : 0;
+            uint4 kv = *reinterpret_cast<const uint4*>(K + (long)kk * a.ldk + cv * 8);
+            uint4 vv = *reinterpret_cast<const uint4*>(V + (long)kk * a.ldv + cv * 8);
+            if (!ok) kv = vv = make_uint4(0, 0, 0, 0);
+            *reinterpret_cast<uint4*>(Ks + kr * KP + cv * 8) = kv;
+            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) s[qq][0] = s[qq][1] = 0.f;
-#pragma unroll
-        for (int slot = 0; slot < 2; ++slot) {
-            const int kr = lane + slot * 64;
-#pragma unroll
-            for (int cv = 0; cv < VPR; ++cv) {
-                float kf[8];
-                load8(&Ks[kr][cv * 8], kf);
-#pragma unroll
-                for (int qq = 0; qq < 4; ++qq) {
-                    const float* qp = &Qs[wave * 4 + qq][cv * 8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) s[qq][slot] += qp[j] * kf[j];
-                }
+            for (int j = 0; j < 4; ++j) {
+                Vt[(cv * 8 + 2 * j) * VP + kr] = (bf16_t)(w[j] & 0xFFFF);
+                Vt[(cv * 8 + 2 * j + 1) * VP + kr] = (bf16_t)(w[j] >> 16);
             }
         }
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-            const float s0 = (c0 + lane < a.Lk) ? s[qq][0] : -INFINITY;
-            const float s1 = (c0 + lane + 64 < a.Lk) ? s[qq][1] : -INFINITY;
-            const float mn = fmaxf(m[qq], wave_max(fmaxf(s0, s1)));
-            const float al = expf(m[qq] - mn);
-            const float p0 = expf(s0 - mn), p1 = expf(s1 - mn);
-            l[qq] = l[qq] * al + wave_sum(p0 + p1);
-            o[qq] *= al;
-            m[qq] = mn;
-            Ps[wave][qq][lane] = p0;
-            Ps[wave][qq][lane + 64] = p1;
-        }
         __syncthreads();
-        const int kmax = min(KC, a.Lk - c0);
-        if (lane < DH) {
-            for (int k = 0; k < kmax; ++k) {
-                const float vk = bf2f(Vs[k][lane]);
+        // S = Q K^T for 16 queries x 64 keys
+        f32x4 s[4];
 #pragma unroll
-                for (int qq = 0; qq < 4; ++qq) o[qq] += Ps[wave][qq][k] * vk;
+        for (int nt = 0; nt < 4; ++nt) {
+            s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (nt * 16 + (lane & 15)) * KP + ks * 32 + 8 * (lane >> 4));
+                s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, s[nt], 0, 0, 0);
+            }
+        }
+        // online softmax; element (row = (lane>>4)*4 + i, key = nt*16 + (lane & 15))
+        float alpha[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const bool ok = c0 + nt * 16 + (lane & 15) < a.Lk;
+                s[nt][i] = ok ? s[nt][i] * scale : -INFINITY;
+                mx = fmaxf(mx, s[nt][i]);
+            }
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+            const float mn = fmaxf(m[i], mx);
+            alpha[i] = __expf(m[i] - mn);
+            float sum = 0.f;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const float pv = __expf(s[nt][i] - mn);
+                s[nt][i] = pv;
+                sum += pv;
+            }
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
+            l[i] = l[i] * alpha[i] + sum;
+            m[i] = mn;
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[dt][i] *= alpha[i];
+        // P -> LDS (C layout) -> A fragments
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) P[((lane >> 4) * 4 + i) * PP + nt * 16 + (lane & 15)] = f2bf(s[nt][i]);
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < KC / 32; ++ks) {
+            const bf16x8 pf = *reinterpret_cast<const bf16x8*>(P + (lane & 15) * PP + ks * 32 + 8 * (lane >> 4));
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vt + (dt * 16 + (lane & 15)) * VP + ks * 32 + 8 * (lane >> 4));
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[dt], 0, 0, 0);
             }
         }
     }
     bf16_t* O = reinterpret_cast<bf16_t*>(a.o) + r * a.bso + h * DH;
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-        const int qi = q0 + wave * 4 + qq;
-        if (qi < a.Lq && lane < DH) O[(long)qi * a.ldo + lane] = f2bf(o[qq] / l[qq]);
+    for (int i = 0; i < 4; ++i) {
+        const int q = qb + (lane >> 4) * 4 + i;
+        if (q < a.Lq) {
+            const float inv = 1.f / l[i];
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) O[(long)q * a.ldo + dt * 16 + (lane & 15)] = f2bf(o[dt][i] * inv);
+        }
     }
 }
 
@@ -103,13 +143,13 @@ __global__ __launch_bounds__(256) void attn_fwd(const stzs_attn_args a) {
 extern "C" int stzs_attention(const stzs_attn_args* a, void* stream) {
     if (!a || !a->q || !a->k || !a->v || !a->o) return STZS_EINVAL;
     if (a->R <= 0 || a->Lq <= 0 || a->Lk <= 0 || a->heads <= 0) return STZS_ESHAPE;
-    if (a->ldk % 8 || a->ldv % 8 || a->bsk % 8 || a->bsv % 8) return STZS_ESHAPE;
+    if (a->ldq % 8 || a->ldk % 8 || a->ldv % 8 || a->bsq % 8 || a->bsk % 8 || a->bsv % 8) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    dim3 g((unsigned)a->R, a->heads, (a->Lq + QB - 1) / QB);
+    dim3 g((unsigned)a->R, a->heads, (a->Lq + 63) / 64);
     if (a->dh == 64)
-        hipLaunchKernelGGL(attn_fwd<64>, g, dim3(256), 0, s, *a);
+        hipLaunchKernelGGL(attn_mfma<64>, g, dim3(256), 0, s, *a);
     else if (a->dh == 32)
-        hipLaunchKernelGGL(attn_fwd<32>, g, dim3(256), 0, s, *a);
+        hipLaunchKernelGGL(attn_mfma<32>, g, dim3(256), 0, s, *a);
     else
         return STZS_ESHAPE;
     STZS_LAUNCH_CHECK();
