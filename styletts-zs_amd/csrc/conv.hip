@@ -53,9 +53,18 @@ STZS_DEV void waitcnt_vm(int n) {
         __builtin_amdgcn_s_waitcnt(0x0F70 | 0);
 }
 
-// Epilogue pass: EB 8-channel output vectors per thread; residual / accumulate loads are issued
+// Epilogue pass: each thread owns ONE 8-channel vector column (cv = tid & 15, so bias/gate sit in
+// registers) and walks rows 16 apart; EB vectors per batch, residual / accumulate loads issued
 // unconditionally from clamped addresses (all in flight) before any is consumed.
-template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA>
+template <int EACT>
+STZS_DEV float epi_act(float x, float slope) {
+    if constexpr (EACT == STZS_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    else if constexpr (EACT == STZS_ACT_SILU) return x / (1.f + __expf(-x));
+    else if constexpr (EACT == STZS_ACT_LEAKY) return x >= 0.f ? x : x * slope;
+    else return x;
+}
+
+template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA, int EACT>
 STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_bias, const float* c_gate, int bq,
                        int t0, long row0, int tid) {
     const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
@@ -64,18 +73,30 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
     const int ncol = a.ups > 0 ? a.ups * a.Co : a.Co;
     const long nrows_flat = (long)a.B * a.T_out;
     const long t_hi = a.ups > 0 ? (long)a.T_final + a.refl - 1 : (long)a.T_out - 1;
+    const int cv = tid & 15;
+    const int n = blockIdx.y * BCO + cv * 8;
+    const bool col_ok = n < ncol;
+    int co = n, p = 0;
+    if (a.ups > 0) {
+        p = n / a.Co;
+        co = n - p * a.Co;
+    }
+    const int cc = col_ok ? co : 0;
+    float kb[8], kg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        kb[j] = c_bias[cv * 8 + j];
+        kg[j] = c_gate[cv * 8 + j];
+    }
     constexpr int EB = 4;
     for (int v0 = 0; v0 < BT * (BCO / 8); v0 += EB * NTHR) {
         long pb[EB], pt[EB];
-        int pco[EB];
         bool pv[EB];
         float rr[EB][8], ai[EB][8];
 #pragma unroll
         for (int i = 0; i < EB; ++i) {
-            const int v = v0 + tid + i * NTHR;
-            const int tl = v >> 4, cv = v & 15;
-            const int n = blockIdx.y * BCO + cv * 8;
-            bool ok = n < ncol;
+            const int tl = ((v0 + tid) >> 4) + i * (NTHR >> 4);
+            bool ok = col_ok;
             long bb, t;
             if (FLAT) {
                 const long Rr = row0 + tl;
@@ -87,21 +108,15 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
                 t = t0 + tl;
                 ok = ok && t < a.T_out;
             }
-            int co = n;
             if (a.ups > 0) {
-                const int p = n / a.Co;
-                co = n - p * a.Co;
                 t = t * a.ups + p - a.ups_pad;
                 ok = ok && t >= 0 && t < a.T_final;
                 t += a.refl;
             }
-            // clamp to a valid element so the loads below need no condition
             const long tc = t < 0 ? 0 : (t > t_hi ? t_hi : t);
             const long bc = bb < a.B ? bb : a.B - 1;
-            const int cc = ok ? co : 0;
             pb[i] = bb;
             pt[i] = t;
-            pco[i] = co;
             pv[i] = ok;
             if constexpr (VEC) {
                 if constexpr (HR) load8(Rp + bc * a.bsr + (tc / a.res_tdiv) * a.ldr + cc, rr[i]);
@@ -111,20 +126,17 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
 #pragma unroll
         for (int i = 0; i < EB; ++i) {
             if (!pv[i]) continue;
-            const int v = v0 + tid + i * NTHR;
-            const int tl = v >> 4, cv = v & 15;
+            const int tl = ((v0 + tid) >> 4) + i * (NTHR >> 4);
             const long bb = pb[i], t = pt[i];
-            const int co = pco[i];
             float u[8];
             const float* er = ep + tl * EP_PITCH + cv * 8;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                float x = er[j] + c_bias[cv * 8 + j];
-                x = act_apply(a.epi_act, x, a.epi_slope, 1.f);
+                float x = epi_act<EACT>(er[j] + kb[j], a.epi_slope);
                 if (FLAT) {
                     if (a.gate) x *= a.gate[bb * a.gate_bs + min(co + j, a.Co - 1)];
                 } else {
-                    x *= c_gate[cv * 8 + j];
+                    x *= kg[j];
                 }
                 u[j] = x;
             }
@@ -158,6 +170,17 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
                 }
             }
         }
+    }
+}
+
+template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA>
+STZS_DEV void epilogue_act(const stzs_conv_args& a, const float* ep, const float* c_bias, const float* c_gate, int bq,
+                           int t0, long row0, int tid) {
+    switch (a.epi_act) {
+        case STZS_ACT_GELU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_GELU>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
+        case STZS_ACT_SILU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_SILU>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
+        case STZS_ACT_LEAKY: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_LEAKY>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
+        default: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_NONE>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
     }
 }
 
@@ -252,18 +275,30 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         // Loads are UNCONDITIONAL from clamped (always valid) addresses and masked afterwards: a
         // runtime-conditioned load makes hipcc drain vmcnt(0) per element (serialised round trips).
         constexpr int SB = sizeof(TIn) == 2 ? 8 : 4;
+        // vpr = cic/8 is a power of two dividing NTHR: a thread's channel vector cv is the SAME for
+        // every row it stages -> its 8 channel coefficients live in registers, rows advance by adds
+        const int lv = cic == 128 ? 4 : (cic == 64 ? 3 : 2);
+        const int cv = tid & (vpr - 1);
+        const int ci = cc * cic + cv * 8;
+        float k_sc[8], k_sh[8], k_al[8], k_ia[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            k_sc[j] = c_sc[cv * 8 + j];
+            k_sh[j] = c_sh[cv * 8 + j];
+            k_al[j] = c_al[cv * 8 + j];
+            k_ia[j] = c_ia[cv * 8 + j];
+        }
+        const bool ci_ok = ci < a.Ci;
+        const int cic0 = ci_ok ? ci : 0;
+        const int rstep = NTHR >> lv;
         for (int v0 = 0; v0 < nv; v0 += SB * NTHR) {
+            const int rb = (v0 >> lv) + (tid >> lv);
             float f[SB][8];
             bool okv[SB];
 #pragma unroll
             for (int i = 0; i < SB; ++i) {
-                int v = v0 + tid + i * NTHR;
-                bool ok = v < nv;
-                v = ok ? v : 0;
-                const int r = v / vpr, cv = v - r * vpr;
-                int ci = cc * cic + cv * 8;
-                ok = ok && ci < a.Ci;
-                ci = ci < a.Ci ? ci : 0;
+                const int r = rb + i * rstep;
+                bool ok = ci_ok && r < rows_in;
                 long off;
                 if (FLAT) {
                     long R = row0 + r;
@@ -271,26 +306,24 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
                     ok = ok && R < nR;
                     R = R < nR ? R : nR - 1;
                     const long bb = R / a.T_in;
-                    off = bb * a.bsx + (R - bb * a.T_in) * a.ldx + ci;
+                    off = bb * a.bsx + (R - bb * a.T_in) * a.ldx + cic0;
                 } else {
                     int tin = t0 * a.stride - a.pad + r;
                     ok = ok && tin >= 0 && tin < a.T_in;
                     tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
-                    off = (long)bq * a.bsx + (long)tin * a.ldx + ci;
+                    off = (long)bq * a.bsx + (long)tin * a.ldx + cic0;
                 }
                 okv[i] = ok;
                 load8(X + off, f[i]);
             }
 #pragma unroll
             for (int i = 0; i < SB; ++i) {
-                const int v = v0 + tid + i * NTHR;
-                if (v >= nv) break;
-                const int r = v / vpr, cv = v - r * vpr;
+                const int r = rb + i * rstep;
+                if (r >= rows_in) break;
                 float o[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float y = pro_act<PACT>(f[i][j] * c_sc[cv * 8 + j] + c_sh[cv * 8 + j], a.pro_slope,
-                                                  c_al[cv * 8 + j], c_ia[cv * 8 + j]);
+                    const float y = pro_act<PACT>(f[i][j] * k_sc[j] + k_sh[j], a.pro_slope, k_al[j], k_ia[j]);
                     o[j] = okv[i] ? y : 0.f;
                 }
                 *reinterpret_cast<uint4*>(in_lds + r * pitch + cv * 16) = pack8(o);
@@ -353,12 +386,12 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[4][4], unsigned char*
     const bool vec = (a.Co % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0) && (!a.acc_in || a.lda % 8 == 0) &&
                      (a.bsy % 8 == 0) && (!a.res || a.bsr % 8 == 0) && (!a.acc_in || a.bsa % 8 == 0);
     if (vec) {
-        if (a.res && a.acc_in) epilogue<TOut, FLAT, true, true, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else if (a.res) epilogue<TOut, FLAT, true, true, false>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else if (a.acc_in) epilogue<TOut, FLAT, true, false, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else epilogue<TOut, FLAT, true, false, false>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        if (a.res && a.acc_in) epilogue_act<TOut, FLAT, true, true, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else if (a.res) epilogue_act<TOut, FLAT, true, true, false>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else if (a.acc_in) epilogue_act<TOut, FLAT, true, false, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else epilogue_act<TOut, FLAT, true, false, false>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
     } else {
-        epilogue<TOut, FLAT, false, true, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        epilogue_act<TOut, FLAT, false, true, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
     }
 }
 

@@ -18,6 +18,9 @@ from stzs.weights import Arena, pack_conv  # noqa: E402
 eng = StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, 0), device="cuda:0")
 B = int(os.environ.get("B", 64))
 cases = [(24001, 128, 3, 1), (24001, 128, 11, 5), (4000, 256, 3, 1), (4000, 256, 11, 5)]
+if os.environ.get("CASE"):
+    cases = [cases[int(os.environ["CASE"])]]
+FLAGS = [int(f) for f in os.environ.get("FLAGS", "0,1,2,4,3,6,5,7").split(",")]
 for (T, C, k, dil) in cases:
     w = torch.randn(C, C, k) / math.sqrt(C * k)
     A = Arena()
@@ -31,7 +34,7 @@ for (T, C, k, dil) in cases:
     gb = torch.zeros(B, 2 * C, device="cuda:0")
     al = torch.ones(C, device="cuda:0")
     flops = 2.0 * B * T * C * C * k
-    for flags in (0, 1, 2, 4, 3, 6, 5, 7):
+    for flags in FLAGS:
         def run():
             eng.conv(cw, x, y, pad=dil * (k - 1) // 2, dil=dil, pro=(mean, rstd, C, gb.data_ptr(), 2 * C, C),
                      pro_act=L.ACT_SNAKE, pro_alpha=al, flags=flags)
