@@ -44,6 +44,31 @@ STZS_DEV float pro_act(float x, float slope, float alpha, float ialpha) {
     }
 }
 
+template <typename T> struct Raw;
+template <> struct Raw<bf16_t> {
+    typedef uint4 T;
+    static STZS_DEV uint4 load(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+    static STZS_DEV void cvt(const uint4& u, float* v) {
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[2 * i] = __uint_as_float(w[i] << 16);
+            v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+        }
+    }
+};
+struct F8 { float4 a, b; };
+template <> struct Raw<float> {
+    typedef F8 T;
+    static STZS_DEV F8 load(const float* p) {
+        return F8{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 4)};
+    }
+    static STZS_DEV void cvt(const F8& u, float* v) {
+        v[0] = u.a.x; v[1] = u.a.y; v[2] = u.a.z; v[3] = u.a.w;
+        v[4] = u.b.x; v[5] = u.b.y; v[6] = u.b.z; v[7] = u.b.w;
+    }
+};
+
 template <typename T> STZS_DEV void store8v(T* p, const float* v) { store8(p, v); }
 
 STZS_DEV void waitcnt_vm(int n) {
@@ -248,53 +273,24 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     int k = 0;
     for (int cc = 0; cc < nchunk; ++cc) {
         __syncthreads();
-        if (tid < cic) {
-            const int ci = cc * cic + tid;
-            float sc = 0.f, sh = 0.f, al = 1.f;
-            if (ci < a.Ci) {
-                if (a.pro_mode == STZS_PRO_ADAIN) {
-                    const float mu = a.pro_mean[(long)bq * a.stat_bs + ci];
-                    const float rs = a.pro_rstd[(long)bq * a.stat_bs + ci];
-                    const float g = a.pro_gb[(long)bq * a.gb_bs + ci];
-                    const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + ci];
-                    sc = (1.f + g) * rs;
-                    sh = be - mu * sc;
-                } else {
-                    sc = a.pro_cscale;
-                }
-                if (a.pro_alpha) al = a.pro_alpha[ci];
-            }
-            c_sc[tid] = sc;
-            c_sh[tid] = sh;
-            c_al[tid] = al;
-            c_ia[tid] = 1.f / al;
-        }
-        __syncthreads();
         const int nv = (a.flags & 1) ? 0 : rows_in * vpr;
-        // batched staging: SB independent 16-B loads in flight per thread before any is consumed.
-        // Loads are UNCONDITIONAL from clamped (always valid) addresses and masked afterwards: a
-        // runtime-conditioned load makes hipcc drain vmcnt(0) per element (serialised round trips).
-        constexpr int SB = sizeof(TIn) == 2 ? 8 : 4;
-        // vpr = cic/8 is a power of two dividing NTHR: a thread's channel vector cv is the SAME for
-        // every row it stages -> its 8 channel coefficients live in registers, rows advance by adds
+        // Staging: ONE batch of SB independent 16-B loads per thread (every MRF tile fits), issued
+        // BEFORE the per-chunk coefficient loads so both latencies overlap in the same wait.  Loads are
+        // UNCONDITIONAL from clamped (always valid) addresses and masked afterwards (a runtime-
+        // conditioned load makes hipcc drain vmcnt(0) per element).  vpr = cic/8 is a power of two
+        // dividing NTHR, so a thread's channel vector cv is the same for every row it stages.
+        constexpr int SB = sizeof(TIn) == 2 ? 12 : 4;
+        using RawT = typename Raw<TIn>::T;
         const int lv = cic == 128 ? 4 : (cic == 64 ? 3 : 2);
         const int cv = tid & (vpr - 1);
         const int ci = cc * cic + cv * 8;
-        float k_sc[8], k_sh[8], k_al[8], k_ia[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            k_sc[j] = c_sc[cv * 8 + j];
-            k_sh[j] = c_sh[cv * 8 + j];
-            k_al[j] = c_al[cv * 8 + j];
-            k_ia[j] = c_ia[cv * 8 + j];
-        }
         const bool ci_ok = ci < a.Ci;
         const int cic0 = ci_ok ? ci : 0;
         const int rstep = NTHR >> lv;
-        for (int v0 = 0; v0 < nv; v0 += SB * NTHR) {
+        RawT raw[SB];
+        bool okv[SB];
+        auto issue = [&](int v0) {
             const int rb = (v0 >> lv) + (tid >> lv);
-            float f[SB][8];
-            bool okv[SB];
 #pragma unroll
             for (int i = 0; i < SB; ++i) {
                 const int r = rb + i * rstep;
@@ -314,16 +310,52 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
                     off = (long)bq * a.bsx + (long)tin * a.ldx + cic0;
                 }
                 okv[i] = ok;
-                load8(X + off, f[i]);
+                raw[i] = Raw<TIn>::load(X + off);
             }
+        };
+        if (nv > 0) issue(0);
+        if (tid < cic) {
+            const int cg = cc * cic + tid;
+            float sc = 0.f, sh = 0.f, al = 1.f;
+            if (cg < a.Ci) {
+                if (a.pro_mode == STZS_PRO_ADAIN) {
+                    const float mu = a.pro_mean[(long)bq * a.stat_bs + cg];
+                    const float rs = a.pro_rstd[(long)bq * a.stat_bs + cg];
+                    const float g = a.pro_gb[(long)bq * a.gb_bs + cg];
+                    const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + cg];
+                    sc = (1.f + g) * rs;
+                    sh = be - mu * sc;
+                } else {
+                    sc = a.pro_cscale;
+                }
+                if (a.pro_alpha) al = a.pro_alpha[cg];
+            }
+            c_sc[tid] = sc;
+            c_sh[tid] = sh;
+            c_al[tid] = al;
+            c_ia[tid] = 1.f / al;
+        }
+        __syncthreads();
+        float k_sc[8], k_sh[8], k_al[8], k_ia[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            k_sc[j] = c_sc[cv * 8 + j];
+            k_sh[j] = c_sh[cv * 8 + j];
+            k_al[j] = c_al[cv * 8 + j];
+            k_ia[j] = c_ia[cv * 8 + j];
+        }
+        for (int v0 = 0; v0 < nv; v0 += SB * NTHR) {
+            if (v0 > 0) issue(v0);
+            const int rb = (v0 >> lv) + (tid >> lv);
 #pragma unroll
             for (int i = 0; i < SB; ++i) {
                 const int r = rb + i * rstep;
                 if (r >= rows_in) break;
-                float o[8];
+                float f[8], o[8];
+                Raw<TIn>::cvt(raw[i], f);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float y = pro_act<PACT>(f[i][j] * k_sc[j] + k_sh[j], a.pro_slope, k_al[j], k_ia[j]);
+                    const float y = pro_act<PACT>(f[j] * k_sc[j] + k_sh[j], a.pro_slope, k_al[j], k_ia[j]);
                     o[j] = okv[i] ? y : 0.f;
                 }
                 *reinterpret_cast<uint4*>(in_lds + r * pitch + cv * 16) = pack8(o);
