@@ -61,22 +61,38 @@ __global__ __launch_bounds__(256) void chan_stats_partial(const stzs_stats_args 
     }
 }
 
+// pass 2: block = (utterance, 32 channels); 8 chunk groups stride over the chunks with coalesced
+// 8-B (sum, sumsq) loads, fp64 sums, combined in fixed group order -> deterministic.
+constexpr int FIN_CH = 32;
 __global__ __launch_bounds__(256) void chan_stats_final(const stzs_stats_args a, int nchunk) {
-    const long i = (long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (long)a.B * a.C) return;
-    const int b = (int)(i / a.C), c = (int)(i - (long)b * a.C);
-    const float* P = reinterpret_cast<const float*>(a.partial);
+    __shared__ double red[8][FIN_CH][2];
+    const int tid = threadIdx.x, cl = tid & (FIN_CH - 1), g = tid >> 5;
+    const int b = blockIdx.x, c = blockIdx.y * FIN_CH + cl;
     double s = 0.0, q = 0.0;
-    for (int k = 0; k < nchunk; ++k) {
-        const long o = (((long)b * nchunk + k) * a.C + c) * 2;
-        s += (double)P[o];
-        q += (double)P[o + 1];
+    if (c < a.C) {
+        const float2* P = reinterpret_cast<const float2*>(a.partial) + (long)b * nchunk * a.C + c;
+        for (int k = g; k < nchunk; k += 8) {
+            const float2 v = P[(long)k * a.C];
+            s += (double)v.x;
+            q += (double)v.y;
+        }
     }
-    const double mean = s / a.T;
-    double var = q / a.T - mean * mean;
-    if (var < 0.0) var = 0.0;
-    a.mean[(long)b * a.stat_bs + c] = (float)mean;
-    a.rstd[(long)b * a.stat_bs + c] = (float)(1.0 / sqrt(var + (double)a.eps));
+    red[g][cl][0] = s;
+    red[g][cl][1] = q;
+    __syncthreads();
+    if (tid < FIN_CH && c < a.C) {
+        s = q = 0.0;
+#pragma unroll
+        for (int y = 0; y < 8; ++y) {
+            s += red[y][tid][0];
+            q += red[y][tid][1];
+        }
+        const double mean = s / a.T;
+        double var = q / a.T - mean * mean;
+        if (var < 0.0) var = 0.0;
+        a.mean[(long)b * a.stat_bs + c] = (float)mean;
+        a.rstd[(long)b * a.stat_bs + c] = (float)(1.0 / sqrt(var + (double)a.eps));
+    }
 }
 
 template <typename TI, typename TO>
@@ -152,8 +168,17 @@ extern "C" int stzs_chan_stats(const stzs_stats_args* a, void* stream) {
     else
         return STZS_EDTYPE;
     STZS_LAUNCH_CHECK();
-    const long n = (long)a->B * a->C;
-    hipLaunchKernelGGL(chan_stats_final, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, *a, nchunk);
+    hipLaunchKernelGGL(chan_stats_final, dim3(a->B, (a->C + FIN_CH - 1) / FIN_CH), dim3(256), 0, s, *a, nchunk);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_chan_stats_final(const stzs_stats_args* a, int chunk_rows, void* stream) {
+    if (!a || !a->mean || !a->rstd || !a->partial) return STZS_EINVAL;
+    if (a->B <= 0 || a->T <= 0 || a->C <= 0 || chunk_rows <= 0) return STZS_ESHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int nchunk = (a->T + chunk_rows - 1) / chunk_rows;
+    hipLaunchKernelGGL(chan_stats_final, dim3(a->B, (a->C + FIN_CH - 1) / FIN_CH), dim3(256), 0, s, *a, nchunk);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

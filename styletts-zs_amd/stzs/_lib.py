@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("STZS_LIB", os.path.join(_HERE, "libstzs_hip.so"))
 F32, BF16, I32 = 0, 1, 2
 ACT_NONE, ACT_LEAKY, ACT_SNAKE, ACT_GELU, ACT_SILU = 0, 1, 2, 3, 4
 PRO_NONE, PRO_ADAIN = 0, 1
+CONV_TILE_ROWS = 128  # include/stzs.h STZS_CONV_TILE_ROWS
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -30,7 +31,8 @@ class ConvArgs(C.Structure):
                [(n, i32) for n in ("B", "T_in", "T_out", "Ci", "Co", "ks", "dil", "stride", "pad",
                                    "ci_pad", "co_pad", "cic", "ups", "ups_pad", "T_final", "refl", "res_tdiv",
                                    "in_dtype", "out_dtype", "pro_mode", "pro_act", "epi_act", "flags")] + \
-               [(n, f32) for n in ("pro_cscale", "pro_slope", "epi_slope", "alpha", "beta", "pad_f")]
+               [(n, f32) for n in ("pro_cscale", "pro_slope", "epi_slope", "alpha", "beta", "pad_f")] + \
+               [("stat_part", vp), ("stat_ld", i64)]
 
 
 class StatsArgs(C.Structure):
@@ -110,7 +112,7 @@ class CopyArgs(C.Structure):
 
 # every exported symbol of include/stzs.h (tests check the .so exports exactly these)
 EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_chan_stats_workspace",
-           "stzs_chan_stats", "stzs_row_layernorm", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
+           "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_dn_cond", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed"]
@@ -139,6 +141,7 @@ def load():
         "stzs_conv1d": ([P(ConvArgs), vp], i32),
         "stzs_chan_stats_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
+        "stzs_chan_stats_final": ([P(StatsArgs), i32, vp], i32),
         "stzs_row_layernorm": ([P(RowLNArgs), vp], i32),
         "stzs_attention": ([P(AttnArgs), vp], i32),
         "stzs_lstm_workspace": ([i32, i32, i32], C.c_size_t),

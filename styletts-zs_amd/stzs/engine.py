@@ -146,7 +146,9 @@ class StyleTTSZS:
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
-             T_final=0, refl=0, flags=0, what="conv"):
+             T_final=0, refl=0, flags=0, stats_key=None, what="conv"):
+        """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
+        output fused into the conv epilogue (per-tile partials) + one small finalize launch."""
         W = self.W
         a = L.ConvArgs()
         a.x, a.w, a.y = x.ptr, self._t(cw.w).data_ptr(), y.ptr
@@ -182,6 +184,14 @@ class StyleTTSZS:
                 and cscale == 1.0 and x.t.dtype == torch.bfloat16 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
         a.flags = flags
+        st = None
+        if stats_key is not None:
+            Cc = _rup(cw.Co, 8)
+            ntile = (a.T_out + L.CONV_TILE_ROWS - 1) // L.CONV_TILE_ROWS
+            slab = self._slab(y.B * ntile * Cc * 2)
+            a.stat_part, a.stat_ld = slab.data_ptr(), Cc
+            st = (slab, Cc, self.buf(stats_key + ".m", (y.B, Cc), torch.float32),
+                  self.buf(stats_key + ".r", (y.B, Cc), torch.float32))
         tm = self.timer
         if tm is not None and what in tm["tags"]:
             e0 = torch.cuda.Event(enable_timing=True)
@@ -196,7 +206,22 @@ class StyleTTSZS:
             tm["rec"].append((what, e0, e1, flops, byt))
         else:
             self._call(self.lib.stzs_conv1d, a, what)
-        return y
+        if st is None:
+            return y
+        slab, Cc, mean, rstd = st
+        s = L.StatsArgs()
+        s.mean, s.rstd, s.partial = mean.data_ptr(), rstd.data_ptr(), slab.data_ptr()
+        s.stat_bs, s.B, s.T, s.C, s.eps = Cc, y.B, a.T_out, Cc, 1e-5
+        self.launches += 1
+        L.check(self.lib.stzs_chan_stats_final(C.byref(s), L.CONV_TILE_ROWS, self.stream()), "chan_stats_final")
+        return y, (mean, rstd, Cc)
+
+    def _slab(self, n):
+        """shared fp32 partial-statistics slab (consumed by the finalize launch right behind its conv)."""
+        t = self._bufs.get("stat_slab")
+        if t is None or t.numel() < n:
+            t = self._bufs["stat_slab"] = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=self.device)
+        return t
 
     timer = None
 
@@ -519,11 +544,11 @@ class StyleTTSZS:
             a.ldx, a.bsx, a.ldy, a.bsy, a.stat_bs, a.gb_bs, a.gb_beta_off = x.ld, x.bs, u.ld, u.bs, sb1, gbs, c1
             a.B, a.T, a.C, a.slope = B, T, bw.din, 0.2
             self._call(self.lib.stzs_adain_dwup, a, key + ".dwup")
-            self.conv(bw.conv1, u, r, pad=1, what=key + ".conv1")
+            _, (m2, r2, sb2) = self.conv(bw.conv1, u, r, pad=1, stats_key=key + ".s2", what=key + ".conv1")
         else:
-            self.conv(bw.conv1, x, r, pad=1, pro=(m1, r1, sb1, gbase + off1 * 4, gbs, c1), pro_act=L.ACT_LEAKY,
-                      pro_slope=0.2, what=key + ".conv1")
-        m2, r2, sb2 = self.stats(r, key + ".s2")
+            _, (m2, r2, sb2) = self.conv(bw.conv1, x, r, pad=1, pro=(m1, r1, sb1, gbase + off1 * 4, gbs, c1),
+                                         pro_act=L.ACT_LEAKY, pro_slope=0.2, stats_key=key + ".s2",
+                                         what=key + ".conv1")
         if bw.sc is not None:
             scb = self.act(key + ".sc", B, T, bw.dout)
             self.conv(bw.sc, x, scb, what=key + ".sc")
@@ -643,16 +668,17 @@ class StyleTTSZS:
                 k, dil = lw["k"], lw["dil"]
                 o1, c1 = ng.offsets[lw["n1"]]
                 o2, c2 = ng.offsets[lw["n2"]]
-                self.conv(lw["c1"], cur, t1, pad=dil * (k - 1) // 2, dil=dil, pro=(cm, cr, sb, gbase + o1 * 4, gbs, c1),
-                          pro_act=L.ACT_SNAKE, pro_alpha=lw["a1"], what="rb.c1")
-                tm, tr, _ = self.stats(t1, f"gen.st{i}")
+                _, (tm, tr, _) = self.conv(lw["c1"], cur, t1, pad=dil * (k - 1) // 2, dil=dil,
+                                           pro=(cm, cr, sb, gbase + o1 * 4, gbs, c1), pro_act=L.ACT_SNAKE,
+                                           pro_alpha=lw["a1"], stats_key=f"gen.st{i}", what="rb.c1")
                 last = m == len(res) - 1
                 out = xs if last else (bufA if cur is not bufA else bufB)
-                self.conv(lw["c2"], t1, out, pad=(k - 1) // 2, pro=(tm, tr, sb, gbase + o2 * 4, gbs, c2),
-                          pro_act=L.ACT_SNAKE, pro_alpha=lw["a2"], res=cur, alpha=(1.0 / nk) if last else 1.0,
-                          acc_in=(xs if (last and j > 0) else None), beta=1.0, what="rb.c2")
+                r2 = self.conv(lw["c2"], t1, out, pad=(k - 1) // 2, pro=(tm, tr, sb, gbase + o2 * 4, gbs, c2),
+                               pro_act=L.ACT_SNAKE, pro_alpha=lw["a2"], res=cur, alpha=(1.0 / nk) if last else 1.0,
+                               acc_in=(xs if (last and j > 0) else None), beta=1.0,
+                               stats_key=None if last else f"gen.sc{i}.{m % 2}", what="rb.c2")
                 if not last:
-                    cm, cr, _ = self.stats(out, f"gen.sc{i}.{m % 2}")
+                    _, (cm, cr, _) = r2
                     cur = out
         return xs
 

@@ -47,6 +47,8 @@ CONV_CASES = [
     (1, 257, 64, 256, 7, 3, 1),
     (2, 2401, 22, 32, 12, 1, 6),
     (3, 50, 514, 64, 3, 1, 1),
+    (2, 700, 256, 256, 7, 3, 1),   # MRF stage-0 form: two 128-channel chunks, two column tiles
+    (1, 3001, 128, 128, 3, 5, 1),
 ]
 
 
@@ -150,6 +152,33 @@ def test_chan_stats(eng):
     mr = x.double().mean(1)
     vr = x.double().var(1, unbiased=False)
     assert max_rel(m.cpu(), mr) < 1e-5
+    assert max_rel(r.cpu(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
+
+
+@pytest.mark.parametrize("B,T,Ci,Co,k,dil,dt_out", [(2, 1000, 128, 128, 11, 5, torch.bfloat16),
+                                                   (3, 300, 96, 80, 3, 1, torch.bfloat16),
+                                                   (2, 257, 64, 256, 7, 3, torch.float32)])
+def test_conv_fused_stats(eng, B, T, Ci, Co, k, dil, dt_out):
+    """InstanceNorm statistics fused into the conv epilogue (stat_part + stzs_chan_stats_final) equal
+    the statistics of the tensor the conv stored, within 1e-5 (fp32 tile partials, fp64 combine)."""
+    g = torch.Generator().manual_seed(B * T + Co)
+    x = bf(torch.randn(B, T, Ci, generator=g))
+    w = torch.randn(Co, Ci, k, generator=g) / math.sqrt(Ci * k)
+    b = torch.randn(Co, generator=g)
+    res = torch.randn(B, T, Co, generator=g)
+    cw, _A = _pack(w, b)
+    from stzs import _lib as L
+    xd = _act(_dev_ntc(x, (Ci + 7) // 8 * 8), Ci)
+    yd = _act(torch.zeros(B, T, Co, dtype=dt_out, device="cuda:0"))
+    rd = _act(res.to(dt_out).cuda())
+    al = (torch.rand(Ci, generator=g) + 0.5).cuda()
+    _, (m, r, sb) = eng.conv(cw, xd, yd, pad=dil * (k - 1) // 2, dil=dil, pro_act=L.ACT_SNAKE, pro_alpha=al,
+                             res=rd, stats_key="t.fstats")
+    assert sb == Co
+    y = yd.t.double().cpu()
+    mr, vr = y.mean(1), y.var(1, unbiased=False)
+    sd = vr.sqrt()
+    assert float(((m.cpu().double() - mr).abs() / (mr.abs() + sd)).max()) < 1e-5
     assert max_rel(r.cpu(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
 
 
@@ -303,3 +332,11 @@ def test_abi_rejects_bad_shapes(eng):
     a.B, a.T_in, a.T_out, a.Ci, a.Co, a.ks, a.dil, a.stride = 1, 4, 4, 8, 8, 1, 1, 1
     a.ci_pad, a.co_pad, a.ldx, a.bsx = 64, 64, 7, 28  # ld not a multiple of 8
     assert eng.lib.stzs_conv1d(C.byref(a), None) == -2
+    # fused statistics are refused on the ConvTranspose (ups) form and on the flat linear form
+    a.ldx, a.bsx, a.ci_pad, a.co_pad = 8, 32, 64, 128
+    a.Ci, a.Co, a.cic, a.ldy, a.bsy = 8, 8, 64, 8, 40
+    a.stat_part, a.stat_ld = t.data_ptr(), 8
+    a.ups, a.ks, a.pad, a.T_out, a.T_final = 2, 2, 1, 5, 8
+    assert eng.lib.stzs_conv1d(C.byref(a), None) == -1
+    a.ups, a.ks, a.pad, a.T_out, a.T_final = 0, 1, 0, 4, 0
+    assert eng.lib.stzs_conv1d(C.byref(a), None) == -1

@@ -20,7 +20,7 @@ B = int(os.environ.get("B", 64))
 cases = [(24001, 128, 3, 1), (24001, 128, 11, 5), (4000, 256, 3, 1), (4000, 256, 11, 5)]
 if os.environ.get("CASE"):
     cases = [cases[int(os.environ["CASE"])]]
-FLAGS = [int(f) for f in os.environ.get("FLAGS", "0,1,2,4,3,6,5,7").split(",")]
+FLAGS = [int(f, 0) for f in os.environ.get("FLAGS", "0,1,2,4,3,6,5,7").split(",")]
 for (T, C, k, dil) in cases:
     w = torch.randn(C, C, k) / math.sqrt(C * k)
     A = Arena()
