@@ -74,14 +74,19 @@ typedef struct stzs_conv_args {
     int32_t pro_mode, pro_act, epi_act, flags;
     float pro_cscale, pro_slope, epi_slope, alpha, beta, pad_f;
     /* optional fused InstanceNorm statistics of the STORED output (after rounding to out_dtype):
-     * per (utterance b, STZS_CONV_TILE_ROWS-row tile, channel c < Co) the fp32 (sum, sumsq) at
-     * stat_part[((b * ntile + tile) * stat_ld + c) * 2 + {0,1}], ntile = ceil(T_out / 128) -- the
-     * partial layout of stzs_chan_stats; finish with stzs_chan_stats_final(chunk_rows = 128).
+     * per (utterance b, STZS_CONV_STAT_ROWS-row chunk, channel c < Co) the fp32 (sum, sumsq) at
+     * stat_part[((b * nch + chunk) * stat_ld + c) * 2 + {0,1}], nch = ceil(T_out / 64) -- the
+     * partial layout of stzs_chan_stats; finish with stzs_chan_stats_final(chunk_rows = 64).
      * Plain (non-ConvTranspose, non-linear) convs only; NULL = off. */
     void* stat_part;
     int64_t stat_ld;
 } stzs_conv_args;
-#define STZS_CONV_TILE_ROWS 128
+#define STZS_CONV_STAT_ROWS 64
+/* flags bit: weights packed with the 16-lane channel permutation of the MRF kernel (stzs/weights.py
+ * pack_conv(lane16=True)): inside each 128-column tile, packed row wc*64 + nt*16 + g*4 + r holds
+ * output channel wc*64 + g*16 + nt*4 + r.  Selects the persistent MRF conv (csrc/mrf.hip): Snake
+ * prologue, bf16 in/out, Ci % 128 == 0, Co % 16 == 0, stride 1, no gate/ups/epilogue activation. */
+#define STZS_CONV_W_LANE16 16
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------
@@ -99,7 +104,7 @@ typedef struct stzs_stats_args {
 size_t stzs_chan_stats_workspace(int B, int T, int C);
 int stzs_chan_stats(const stzs_stats_args* a, void* stream);
 /* second pass only: mean / rstd from a partial slab already holding ceil(T / chunk_rows) chunks
- * (written by stzs_conv1d's stat_part epilogue with chunk_rows = STZS_CONV_TILE_ROWS); x unused. */
+ * (written by stzs_conv1d's stat_part epilogue with chunk_rows = STZS_CONV_STAT_ROWS); x unused. */
 int stzs_chan_stats_final(const stzs_stats_args* a, int chunk_rows, void* stream);
 
 /* ---- row LayerNorm + modulation (+activation), one wave per row -------------------------

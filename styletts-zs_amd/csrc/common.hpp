@@ -45,6 +45,14 @@ STZS_DEV void load8(const float* p, float* v) {
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
+STZS_DEV void unpack8(const uint4& u, float* v) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+}
 STZS_DEV uint4 pack8(const float* v) {
     uint32_t w[4];
 #pragma unroll

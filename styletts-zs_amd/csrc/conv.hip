@@ -118,6 +118,29 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
 #pragma unroll
     for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
     constexpr int EB = 4;
+    float* red = const_cast<float*>(c_gate) + BCO;  // [2 halves][4 waves][BCO][2] statistics partials
+    // (sum, sumsq) per column over 64 valid rows: 4 lanes per wave share a column vector (xor 16, 32),
+    // lanes < 16 park the wave's partial in LDS; the 4 waves are combined after the loop.
+    auto stat_flush = [&](int half) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            st_s[j] += __shfl_xor(st_s[j], 16, 64);
+            st_s[j] += __shfl_xor(st_s[j], 32, 64);
+            st_q[j] += __shfl_xor(st_q[j], 16, 64);
+            st_q[j] += __shfl_xor(st_q[j], 32, 64);
+        }
+        const int wv = tid >> 6;
+        if ((tid & 63) < 16) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                red[((half * 4 + wv) * BCO + cv * 8 + j) * 2] = st_s[j];
+                red[((half * 4 + wv) * BCO + cv * 8 + j) * 2 + 1] = st_q[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
+    };
+    static_assert(BT * (BCO / 8) == 2 * EB * NTHR, "two epilogue passes = two 64-row halves");
     for (int v0 = 0; v0 < BT * (BCO / 8); v0 += EB * NTHR) {
         long pb[EB], pt[EB];
         bool pv[EB];
@@ -222,38 +245,24 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
                 }
             }
         }
+        if (stat) stat_flush(v0 == 0 ? 0 : 1);
     }
     if (stat) {
-        // (sum, sumsq) per column over this tile's valid rows: 4 lanes per wave share a column vector,
-        // then the 4 waves meet in LDS; one deterministic fp32 partial per (utterance, tile, channel).
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            st_s[j] += __shfl_xor(st_s[j], 16, 64);
-            st_s[j] += __shfl_xor(st_s[j], 32, 64);
-            st_q[j] += __shfl_xor(st_q[j], 16, 64);
-            st_q[j] += __shfl_xor(st_q[j], 32, 64);
-        }
-        float* red = const_cast<float*>(c_gate) + BCO;  // [4 waves][BCO][2]
-        const int wave = tid >> 6, lane = tid & 63;
-        if (lane < 16) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                red[(wave * BCO + cv * 8 + j) * 2] = st_s[j];
-                red[(wave * BCO + cv * 8 + j) * 2 + 1] = st_q[j];
-            }
-        }
         __syncthreads();
-        const int c = blockIdx.y * BCO + tid;
-        if (tid < BCO && c < a.Co) {
+        // one deterministic fp32 partial per (utterance, 64-row chunk, channel)
+        const int half = tid >> 7, cl = tid & (BCO - 1);
+        const int c = blockIdx.y * BCO + cl;
+        const int r0 = t0 + half * 64;
+        if (c < a.Co && r0 < a.T_out) {
             float ss = 0.f, qq = 0.f;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
-                ss += red[(w * BCO + tid) * 2];
-                qq += red[(w * BCO + tid) * 2 + 1];
+                ss += red[((half * 4 + w) * BCO + cl) * 2];
+                qq += red[((half * 4 + w) * BCO + cl) * 2 + 1];
             }
-            const int ntile = (a.T_out + BT - 1) / BT;
+            const int nch = (a.T_out + 63) / 64;
             float* P = reinterpret_cast<float*>(a.stat_part);
-            const long o = (((long)bq * ntile + t0 / BT) * a.stat_ld + c) * 2;
+            const long o = (((long)bq * nch + r0 / 64) * a.stat_ld + c) * 2;
             P[o] = ss;
             P[o + 1] = qq;
         }
@@ -459,192 +468,6 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     finish<TOut, FLAT>(a, acc, smem, bq, t0, row0);
 }
 
-// ---------------------------------------------------------------------------------------------
-// The MRF conv (the dominant kernel of the whole path): AdaIN + Snake prologue, 128-channel input
-// chunks, bf16 in / out, stride 1.  Same 128 x 128 tile and epilogue as conv_mfma; differs in
-//  * a 4-slot weight ring: the NEXT K-step's A and B fragments are read (ds_read_b128) under the
-//    current K-step's 16 MFMAs, so the fragment latency is hidden; one counted vmcnt + s_barrier
-//    per K-step, slot = k & 3;
-//  * K-steps unrolled per tap (4 x 32 channels): every fragment address is a per-tap base plus an
-//    immediate offset;
-//  * the Snake prologue in its cosine form, x + 1/(2a) - cos(2 a x)/(2a), with the AdaIN affine
-//    folded into the per-channel constants: three FMAs and one v_cos_f32 per element.
-// LDS: rows_in x 272 B input tile + 32 KB ring (k11 / dil 5: 79.3 KB -> two workgroups per CU).
-constexpr int P128 = 272;
-constexpr int NSL4 = 4;
-
-__global__ __launch_bounds__(NTHR, 2) void conv_snake128(const stzs_conv_args a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int ks = a.ks, dil = a.dil;
-    const int rows_in = BT + (ks - 1) * dil;
-    unsigned char* in_lds = smem;
-    unsigned char* ring = smem + ((rows_in * P128 + 15) & ~15);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wt = wave >> 1, wc = wave & 1;
-    const int tpb = (a.T_out + BT - 1) / BT;
-    const int bq = blockIdx.x / tpb;
-    const int t0 = (blockIdx.x - bq * tpb) * BT;
-    const int nchunk = a.ci_pad >> 7;
-    const int NK = nchunk * ks * 4;
-    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
-    auto fill = [&](int k) {  // k >= NK: a harmless dummy copy (clamped source) into a retired slot
-        const bf16_t* src = Wt + (long)(k < NK ? k : NK - 1) * (BCO * 32) + wave * 1024 + lane * 8;
-        unsigned char* dst = ring + (k & (NSL4 - 1)) * SLOT_BYTES + wave * 2048;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 512),
-                                         (__attribute__((address_space(3))) void*)(dst + 1024), 16, 0, 0);
-    };
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int brow = wc * 64 + (lane & 15);
-    const int boff0 = brow * 64 + (((lane >> 4) ^ gswz(brow)) << 4);
-    const int arow0 = (wt * 64 + (lane & 15)) * P128 + (lane >> 4) * 16;
-    bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
-    auto readB = [&](bf16x8 (&fb)[4], int k) {
-        const unsigned char* wl = ring + (k & (NSL4 - 1)) * SLOT_BYTES + boff0;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) fb[nt] = *reinterpret_cast<const bf16x8*>(wl + nt * 1024);
-    };
-    auto readA = [&](bf16x8 (&fa)[4], int base, int q) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-            fa[mt] = *reinterpret_cast<const bf16x8*>(in_lds + base + mt * 16 * P128 + q * 64);
-    };
-    auto mma = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[4]) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
-    };
-
-    const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x) + (long)bq * a.bsx;
-    const int cv = tid & 15, rsub = tid >> 4;
-    fill(0);
-    fill(1);
-    int k = 0;
-    for (int cc = 0; cc < nchunk; ++cc) {
-        __syncthreads();  // every wave is done reading the previous chunk's input tile
-        if (!(a.flags & 1)) {
-            constexpr int SB = 12;  // 16 row-lanes x 12 = 192 >= rows_in for every MRF conv
-            const int c = cc * 128 + cv * 8;
-            uint4 raw[SB];
-            bool okv[SB];
-#pragma unroll
-            for (int i = 0; i < SB; ++i) {
-                int tin = t0 - a.pad + rsub + 16 * i;
-                okv[i] = tin >= 0 && tin < a.T_in;
-                tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
-                raw[i] = *reinterpret_cast<const uint4*>(X + (long)tin * a.ldx + c);
-            }
-            // Per-channel constants, computed once per channel by 128 threads into the ring slot
-            // that is idle until this chunk's first K-step fills it (slot (k + 3) & 3; fills k+1, k+2
-            // are in flight to the other slots):  t = x*ka + kb  (revolutions of cos(2 a y)),
-            // out = cos(t) * km + (x*ksc + ksh).
-            float* cs = reinterpret_cast<float*>(ring + ((k + 3) & (NSL4 - 1)) * SLOT_BYTES);
-            if (tid < 128) {
-                const int ch = cc * 128 + tid;
-                float sc, sh;
-                if (a.pro_mode == STZS_PRO_ADAIN) {
-                    const float mu = a.pro_mean[(long)bq * a.stat_bs + ch];
-                    const float rs = a.pro_rstd[(long)bq * a.stat_bs + ch];
-                    const float g = a.pro_gb[(long)bq * a.gb_bs + ch];
-                    const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + ch];
-                    sc = (1.f + g) * rs;
-                    sh = be - mu * sc;
-                } else {
-                    sc = a.pro_cscale;
-                    sh = 0.f;
-                }
-                const float al = a.pro_alpha[ch];
-                const float h = 0.5f / al;
-                const float w = al * 0.318309886183790672f;  // a / pi
-                cs[tid] = sc * w;
-                cs[128 + tid] = sh * w;
-                cs[256 + tid] = sc;
-                cs[384 + tid] = sh + h;
-                cs[512 + tid] = -h;
-            }
-            __syncthreads();
-            float ka[8], kb[8], ksc[8], ksh[8], km[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                ka[j] = cs[cv * 8 + j];
-                kb[j] = cs[128 + cv * 8 + j];
-                ksc[j] = cs[256 + cv * 8 + j];
-                ksh[j] = cs[384 + cv * 8 + j];
-                km[j] = cs[512 + cv * 8 + j];
-            }
-#pragma unroll
-            for (int i = 0; i < SB; ++i) {
-                const int r = rsub + 16 * i;
-                if (r < rows_in) {
-                    const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
-                    uint32_t o[4];
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        const float x0 = __uint_as_float(w[p] << 16), x1 = __uint_as_float(w[p] & 0xFFFF0000u);
-                        const int j0 = 2 * p, j1 = 2 * p + 1;
-                        const float c0 = __builtin_amdgcn_cosf(fmaf(x0, ka[j0], kb[j0]));
-                        const float c1 = __builtin_amdgcn_cosf(fmaf(x1, ka[j1], kb[j1]));
-                        const float y0 = fmaf(c0, km[j0], fmaf(x0, ksc[j0], ksh[j0]));
-                        const float y1 = fmaf(c1, km[j1], fmaf(x1, ksc[j1], ksh[j1]));
-                        o[p] = okv[i] ? ((uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16)) : 0u;
-                    }
-                    *reinterpret_cast<uint4*>(in_lds + r * P128 + cv * 16) = make_uint4(o[0], o[1], o[2], o[3]);
-                }
-            }
-        }
-        __syncthreads();
-        if (cc == 0) {  // (the barrier above drained fills 0 and 1)
-            fill(2);
-            readB(fb0, 0);
-        }
-        readA(fa0, arow0, 0);
-        for (int tap = 0; tap < ((a.flags & 2) ? 0 : ks); ++tap) {
-            const int ab = arow0 + tap * dil * P128;
-            const int an = tap + 1 < ks ? ab + dil * P128 : arow0;  // last tap: harmless re-read
-            // One K-step, branch-free so the compiler's lgkmcnt waits stay counted: fill k+1 landed
-            // (fill k+2, real or dummy, may stay in flight) -> barrier -> fill k+3 into the retired
-            // slot k-1 -> read the NEXT fragments -> 16 MFMAs on the CURRENT ones.
-// MFMA / ds_read alternation for the scheduler: 8 x (1 MFMA, 1 read), then the last 8 MFMAs
-#define STZS_INTERLEAVE_8x1                                                     \
-    {                                                                           \
-        _Pragma("unroll") for (int ii = 0; ii < 8; ++ii) {                      \
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  \
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                  \
-        }                                                                       \
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                      \
-    }
-#define STZS_KSTEP(FA, FB, NA, NB, ABASE, AQ)                                   \
-    {                                                                           \
-        __builtin_amdgcn_s_waitcnt(0x0F70 | 2);                                 \
-        __builtin_amdgcn_s_barrier();                                           \
-        fill(k + 3);                                                            \
-        __builtin_amdgcn_sched_barrier(0);                                      \
-        readB(NB, k + 1);                                                       \
-        readA(NA, ABASE, AQ);                                                   \
-        mma(FA, FB);                                                            \
-        STZS_INTERLEAVE_8x1;                                                    \
-        __builtin_amdgcn_sched_barrier(0);                                      \
-        ++k;                                                                    \
-    }
-            STZS_KSTEP(fa0, fb0, fa1, fb1, ab, 1)
-            STZS_KSTEP(fa1, fb1, fa0, fb0, ab, 2)
-            STZS_KSTEP(fa0, fb0, fa1, fb1, ab, 3)
-            STZS_KSTEP(fa1, fb1, fa0, fb0, an, 0)
-#undef STZS_KSTEP
-#undef STZS_INTERLEAVE_8x1
-        }
-    }
-    finish<bf16_t, false>(a, acc, smem, bq, t0, 0);
-}
-
 // Accumulators -> LDS (fp32, padded rows) -> vectorised fused epilogue.
 template <typename TOut, bool FLAT>
 STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[4][4], unsigned char* smem, int bq, int t0, long row0) {
@@ -760,7 +583,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
 
 size_t lds_bytes(int rows_in, int cic) {
     const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + NSLOT * SLOT_BYTES + 4 * 128 * 4;
-    const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 4 * BCO * 2 * 4;
+    const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
     return main > epi ? main : epi;
 }
 
@@ -784,20 +607,6 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
         STZS_LAUNCH_CHECK();
         return STZS_OK;
     }
-    if constexpr (sizeof(TIn) == 2 && sizeof(TOut) == 2) {
-        if (!flat && a.pro_act == STZS_ACT_SNAKE && a.cic == 128 && a.stride == 1 && a.Ci % 128 == 0 &&
-            a.ups == 0 && BT + (a.ks - 1) * a.dil <= 192) {
-            const int ri = BT + (a.ks - 1) * a.dil;
-            size_t l2 = (((size_t)ri * P128 + 15) & ~(size_t)15) + NSL4 * SLOT_BYTES;
-            const size_t le = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 4 * BCO * 2 * 4;
-            l2 = l2 > le ? l2 : le;
-            if (l2 > 160 * 1024) return STZS_ESHAPE;
-            (void)hipFuncSetAttribute((const void*)conv_snake128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
-            hipLaunchKernelGGL(conv_snake128, grid, dim3(NTHR), l2, s, a);
-            STZS_LAUNCH_CHECK();
-            return STZS_OK;
-        }
-    }
     if (flat)
         k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE>;
     else if (a.pro_act == STZS_ACT_SNAKE)
@@ -813,6 +622,8 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
 }
 
 }  // namespace
+
+int stzs_mrf_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrf.hip
 
 extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
     if (!a || !a->x || !a->w || !a->y) return STZS_EINVAL;
@@ -838,6 +649,7 @@ extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
     if (a->stat_part && (a->ups > 0 || !epi_vec(*a) || a->stat_ld < a->Co || !stzs_aligned(a->stat_part, 8)))
         return STZS_EINVAL;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (a->flags & STZS_CONV_W_LANE16) return stzs_mrf_conv_launch(*a, s);
     if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) return launch_dt<bf16_t, bf16_t>(*a, s);
     if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) return launch_dt<bf16_t, float>(*a, s);
     if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_BF16) return launch_dt<float, bf16_t>(*a, s);

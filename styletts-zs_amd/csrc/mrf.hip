@@ -1,0 +1,339 @@
+// The MRF conv (the generator's AdaINResBlock1 convs, about half of all
+// synthesis time) on gfx950.
+//
+// y[b, t, co] = epi( sum_{tap, ci} W[tap, co, ci] * snake(adain(x))[b, t + tap*dil - pad, ci] ),
+// 128-channel input chunks, bf16 in / out, stride 1; epi = ((v + bias + res) * alpha + beta * acc_in),
+// optional fused InstanceNorm statistics of the stored output.
+//
+// One 256-thread workgroup (4 waves, 2 x 2) per 128-row x 128-channel output tile, two workgroups
+// per CU (<= 80 KB LDS each):
+//  * STAGING, per 128-channel input chunk: the tile's rows plus the dilation halo, one batch of 16-B
+//    loads per thread, the AdaIN affine folded into per-channel constants that sit in the idle weight
+//    ring slot, and the Snake in its cosine form  x + 1/(2a) - cos(2 a x)/(2a)  (three FMAs and one
+//    v_cos_f32 per element) -> bf16 rows with a 272-B pitch (conflict-free ds_read_b128).
+//  * K LOOP: one K-step = 32 input channels of one tap = 16 MFMAs (v_mfma_f32_16x16x32_bf16) per
+//    wave.  Weights stream by LDS-DMA through a 4-slot ring, filled three K-steps ahead; each K-step
+//    does one counted vmcnt + s_barrier, and the NEXT K-step's fragments are read (ds_read_b128)
+//    between the current K-step's MFMAs.  The K-step body is branch-free (past the end a fill is a
+//    harmless re-copy into a retired slot), so the compiler's lgkmcnt waits stay counted.
+//  * EPILOGUE straight from the accumulators: the MFMA operands are swapped (weights = A, input = B,
+//    so C is [channel][time]) and the packer permutes channels (STZS_CONV_W_LANE16) so that each lane
+//    holds 16 consecutive channels of one time step -> 32-B vector residual / accumulate loads and
+//    stores, no LDS round trip.  Statistics: per-lane sums, xor-reduced over the 16 time lanes, one
+//    deterministic fp32 partial per (utterance, 64-row chunk, channel).
+// (A persistent warp-specialised variant -- producer waves staging the next tile beside the MFMA
+// waves -- measured 2x slower: see DESIGN.md, "MRF conv".)
+#include "common.hpp"
+
+namespace {
+
+constexpr int NTH = 256;
+constexpr int BT = 128, BCO = 128;
+constexpr int P = 272;  // staged input row pitch, bytes
+constexpr int NSL = 4, SLOT = 8192;
+constexpr int SB = 12;  // staged 16-B vectors per thread: 16 row lanes x 12 = 192 >= rows_in
+
+STZS_DEV int gswz(int r) { return (0x1320 >> (((r >> 2) & 3) * 4)) & 3; }
+
+// sum over the 16 lanes of a DPP row, result in every lane: VALU-only (no ds_bpermute)
+STZS_DEV float row_sum16(float x) {
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, true));  // row_half_mirror
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, true));  // row_mirror
+    return x;
+}
+
+template <bool HR, bool HA>
+__global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int ks = a.ks, dil = a.dil;
+    const int rows_in = BT + (ks - 1) * dil;
+    unsigned char* ring = smem + ((rows_in * P + 15) & ~15);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wt = wave >> 1, wc = wave & 1;
+    const int tpb = (a.T_out + BT - 1) / BT;
+    const int bq = blockIdx.x / tpb;
+    const int t0 = (blockIdx.x - bq * tpb) * BT;
+    const int nchunk = a.ci_pad >> 7;
+    const int NK = nchunk * ks * 4;
+    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
+    auto fill = [&](int k) {  // k >= NK: a harmless re-copy (clamped source) into a retired slot
+        const bf16_t* src = Wt + (long)(k < NK ? k : NK - 1) * (BCO * 32) + wave * 1024 + lane * 8;
+        unsigned char* dst = ring + (k & (NSL - 1)) * SLOT + wave * 2048;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 512),
+                                         (__attribute__((address_space(3))) void*)(dst + 1024), 16, 0, 0);
+    };
+    f32x4 acc[4][4];  // [nt: channel tile][mt: time tile]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int brow = wc * 64 + (lane & 15);
+    const int boff0 = brow * 64 + (((lane >> 4) ^ gswz(brow)) << 4);
+    const int arow0 = (wt * 64 + (lane & 15)) * P + (lane >> 4) * 16;
+    bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
+    auto readB = [&](bf16x8 (&fb)[4], int k) {
+        const unsigned char* wl = ring + (k & (NSL - 1)) * SLOT + boff0;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) fb[nt] = *reinterpret_cast<const bf16x8*>(wl + nt * 1024);
+    };
+    auto readA = [&](bf16x8 (&fx)[4], int off) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) fx[mt] = *reinterpret_cast<const bf16x8*>(smem + off + mt * 16 * P);
+    };
+    auto mma = [&](const bf16x8 (&fx)[4], const bf16x8 (&fw)[4]) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+                acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[nt], fx[mt], acc[nt][mt], 0, 0, 0);
+    };
+
+    const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x) + (long)bq * a.bsx;
+    const int cv = tid & 15, rsub = tid >> 4;
+    fill(0);
+    fill(1);
+    int k = 0;
+    for (int cc = 0; cc < nchunk; ++cc) {
+        __syncthreads();  // every wave is done reading the previous chunk's input tile
+        if (!(a.flags & 1)) {
+            const int c = cc * 128 + cv * 8;
+            uint4 raw[SB];
+            bool okv[SB];
+#pragma unroll
+            for (int i = 0; i < SB; ++i) {
+                int tin = t0 - a.pad + rsub + 16 * i;
+                okv[i] = tin >= 0 && tin < a.T_in;
+                tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+                raw[i] = *reinterpret_cast<const uint4*>(X + (long)tin * a.ldx + c);
+            }
+            // per-channel constants, computed once per channel by 128 threads into the ring slot that
+            // stays idle until this chunk's first K-step fills it (slot (k + 3) & 3):
+            //   t = x*ka + kb (revolutions of cos(2 a y)),  out = cos(t) * km + (x*ksc + ksh)
+            float* cs = reinterpret_cast<float*>(ring + ((k + 3) & (NSL - 1)) * SLOT);
+            if (tid < 128) {
+                const int ch = cc * 128 + tid;
+                float sc, sh;
+                if (a.pro_mode == STZS_PRO_ADAIN) {
+                    const float mu = a.pro_mean[(long)bq * a.stat_bs + ch];
+                    const float rs = a.pro_rstd[(long)bq * a.stat_bs + ch];
+                    const float gm = a.pro_gb[(long)bq * a.gb_bs + ch];
+                    const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + ch];
+                    sc = (1.f + gm) * rs;
+                    sh = be - mu * sc;
+                } else {
+                    sc = a.pro_cscale;
+                    sh = 0.f;
+                }
+                const float al = a.pro_alpha[ch];
+                const float h = 0.5f / al;
+                const float w = al * 0.318309886183790672f;  // a / pi
+                cs[tid] = sc * w;
+                cs[128 + tid] = sh * w;
+                cs[256 + tid] = sc;
+                cs[384 + tid] = sh + h;
+                cs[512 + tid] = -h;
+            }
+            __syncthreads();
+            float ka[8], kb[8], ksc[8], ksh[8], km[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                ka[j] = cs[cv * 8 + j];
+                kb[j] = cs[128 + cv * 8 + j];
+                ksc[j] = cs[256 + cv * 8 + j];
+                ksh[j] = cs[384 + cv * 8 + j];
+                km[j] = cs[512 + cv * 8 + j];
+            }
+#pragma unroll
+            for (int i = 0; i < SB; ++i) {
+                const int r = rsub + 16 * i;
+                if (r < rows_in) {
+                    const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+                    uint32_t o[4];
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        const float x0 = __uint_as_float(w[p] << 16), x1 = __uint_as_float(w[p] & 0xFFFF0000u);
+                        const int j0 = 2 * p, j1 = 2 * p + 1;
+                        const float c0 = __builtin_amdgcn_cosf(fmaf(x0, ka[j0], kb[j0]));
+                        const float c1 = __builtin_amdgcn_cosf(fmaf(x1, ka[j1], kb[j1]));
+                        const float y0 = fmaf(c0, km[j0], fmaf(x0, ksc[j0], ksh[j0]));
+                        const float y1 = fmaf(c1, km[j1], fmaf(x1, ksc[j1], ksh[j1]));
+                        o[p] = okv[i] ? ((uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16)) : 0u;
+                    }
+                    *reinterpret_cast<uint4*>(smem + r * P + cv * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+                }
+            }
+        }
+        __syncthreads();
+        if (cc == 0) {  // (the barrier above drained fills 0 and 1)
+            fill(2);
+            readB(fb0, 0);
+        }
+        readA(fa0, arow0);
+        const int ntap = (a.flags & 2) ? 1 : ks;
+        // fill k+1 landed (fill k+2 may stay in flight) -> barrier -> fill k+3 into the retired
+        // slot k-1 -> NEXT fragments read between the CURRENT K-step's 16 MFMAs
+#define STZS_MRF_STEP(FX, FW, NX, NW, AOFF)                                     \
+    {                                                                           \
+        __builtin_amdgcn_s_waitcnt(0x0F72);                                     \
+        __builtin_amdgcn_s_barrier();                                           \
+        fill(k + 3);                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                      \
+        readB(NW, k + 1);                                                       \
+        readA(NX, AOFF);                                                        \
+        mma(FX, FW);                                                            \
+        _Pragma("unroll") for (int ii = 0; ii < 8; ++ii) {                      \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  \
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                  \
+        }                                                                       \
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                      \
+        __builtin_amdgcn_sched_barrier(0);                                      \
+        ++k;                                                                    \
+    }
+        for (int tap = 0; tap + 1 < ntap; ++tap) {
+            const int ab = arow0 + tap * dil * P;
+            STZS_MRF_STEP(fa0, fb0, fa1, fb1, ab + 64)
+            STZS_MRF_STEP(fa1, fb1, fa0, fb0, ab + 128)
+            STZS_MRF_STEP(fa0, fb0, fa1, fb1, ab + 192)
+            STZS_MRF_STEP(fa1, fb1, fa0, fb0, ab + dil * P)
+        }
+        {  // last tap of the chunk (peeled: the final K-step of the last chunk is special)
+            const int ab = arow0 + (ntap - 1) * dil * P;
+            STZS_MRF_STEP(fa0, fb0, fa1, fb1, ab + 64)
+            STZS_MRF_STEP(fa1, fb1, fa0, fb0, ab + 128)
+            STZS_MRF_STEP(fa0, fb0, fa1, fb1, ab + 192)
+            if (cc + 1 < nchunk) STZS_MRF_STEP(fa1, fb1, fa0, fb0, arow0)  // next chunk re-reads A after staging
+        }
+#undef STZS_MRF_STEP
+    }
+    // The final K-step needs no wait, barrier, fill or prefetch: its fragments are in registers.  The
+    // epilogue's residual / accumulate loads go out first so their latency hides under its MFMAs.
+    const int gq = lane >> 4, n = lane & 15;
+    const int co0 = blockIdx.y * BCO + wc * 64 + gq * 16;
+    const bool col_ok = co0 < a.Co;
+    const int coc = col_ok ? co0 : 0;
+    uint4 rr[4][2], aa[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+        const int t = t0 + wt * 64 + mt * 16 + n;
+        const int tc = t < a.T_out ? t : a.T_out - 1;
+        if constexpr (HR) {
+            const bf16_t* p = reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr + (long)tc * a.ldr + coc;
+            rr[mt][0] = *reinterpret_cast<const uint4*>(p);
+            rr[mt][1] = *reinterpret_cast<const uint4*>(p + 8);
+        }
+        if constexpr (HA) {
+            const bf16_t* p = reinterpret_cast<const bf16_t*>(a.acc_in) + (long)bq * a.bsa + (long)tc * a.lda + coc;
+            aa[mt][0] = *reinterpret_cast<const uint4*>(p);
+            aa[mt][1] = *reinterpret_cast<const uint4*>(p + 8);
+        }
+    }
+    mma(fa1, fb1);
+    if (a.flags & 4) return;
+
+    // ---------------- epilogue straight from the accumulators
+    // lane (gq = lane >> 4, n = lane & 15): time t = t0 + wt*64 + mt*16 + n, channels co0 .. co0+15
+    // (packed row nt*16 + gq*4 + r of the wave's 64 columns  <->  channel co0 + nt*4 + r)
+    float bias[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
+    const bool stat = a.stat_part != nullptr;
+    float ss[16], sq[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ss[i] = sq[i] = 0.f;
+    bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
+    {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const int t = t0 + wt * 64 + mt * 16 + n;
+            float v[16];
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[nt][mt][r] + bias[nt * 4 + r];
+            if constexpr (HR) {
+                float f[16];
+                unpack8(rr[mt][0], f);
+                unpack8(rr[mt][1], f + 8);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] += f[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] *= a.alpha;
+            if constexpr (HA) {
+                float f[16];
+                unpack8(aa[mt][0], f);
+                unpack8(aa[mt][1], f + 8);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = fmaf(a.beta, f[i], v[i]);
+            }
+            const uint4 o0 = pack8(v), o1 = pack8(v + 8);
+            const bool ok = col_ok && t < a.T_out;
+            if (ok) {
+                bf16_t* p = Y + (long)bq * a.bsy + (long)t * a.ldy + co0;
+                *reinterpret_cast<uint4*>(p) = o0;
+                *reinterpret_cast<uint4*>(p + 8) = o1;
+            }
+            if (stat && ok) {  // statistics of the stored (bf16-rounded) values
+                float f[16];
+                unpack8(o0, f);
+                unpack8(o1, f + 8);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    ss[i] += f[i];
+                    sq[i] = fmaf(f[i], f[i], sq[i]);
+                }
+            }
+        }
+    }
+    if (stat) {
+        // the 16 time lanes (n) of a channel group: xor-reduce, one 64-row partial per wave
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            ss[i] = row_sum16(ss[i]);
+            sq[i] = row_sum16(sq[i]);
+        }
+        const int r0 = t0 + wt * 64;
+        if (n == 0 && col_ok && r0 < a.T_out) {
+            const int nch = (a.T_out + 63) / 64;
+            float* Pp = reinterpret_cast<float*>(a.stat_part) + (((long)bq * nch + r0 / 64) * a.stat_ld + co0) * 2;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                Pp[2 * i] = ss[i];
+                Pp[2 * i + 1] = sq[i];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// internal entry used by stzs_conv1d for STZS_CONV_W_LANE16 weights
+__attribute__((visibility("hidden"))) int stzs_mrf_conv_launch(const stzs_conv_args& a, hipStream_t s) {
+    const int rows_in = BT + (a.ks - 1) * a.dil;
+    if (a.stride != 1 || a.cic != 128 || a.Ci % 128 || a.ci_pad % 128 || a.Co % 16 || rows_in > 16 * SB ||
+        a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.ups || a.pro_act != STZS_ACT_SNAKE || !a.pro_alpha ||
+        a.gate || a.epi_act != STZS_ACT_NONE || a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8)) ||
+        (a.acc_in && (a.lda % 8 || a.bsa % 8)) || a.res_tdiv != 1)
+        return STZS_ESHAPE;
+    const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + NSL * SLOT;
+    if (lds > 160 * 1024) return STZS_ESHAPE;
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / BCO);
+    void (*k)(stzs_conv_args);
+    if (a.res && a.acc_in)
+        k = mrf_conv<true, true>;
+    else if (a.res)
+        k = mrf_conv<true, false>;
+    else if (a.acc_in)
+        k = mrf_conv<false, true>;
+    else
+        k = mrf_conv<false, false>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}

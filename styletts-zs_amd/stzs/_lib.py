@@ -15,7 +15,8 @@ LIB_PATH = os.environ.get("STZS_LIB", os.path.join(_HERE, "libstzs_hip.so"))
 F32, BF16, I32 = 0, 1, 2
 ACT_NONE, ACT_LEAKY, ACT_SNAKE, ACT_GELU, ACT_SILU = 0, 1, 2, 3, 4
 PRO_NONE, PRO_ADAIN = 0, 1
-CONV_TILE_ROWS = 128  # include/stzs.h STZS_CONV_TILE_ROWS
+CONV_STAT_ROWS = 64  # include/stzs.h STZS_CONV_STAT_ROWS
+CONV_W_LANE16 = 16  # include/stzs.h STZS_CONV_W_LANE16
 
 vp = C.c_void_p
 i64 = C.c_int64

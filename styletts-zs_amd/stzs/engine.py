@@ -183,11 +183,13 @@ class StyleTTSZS:
         if (cw.ks == 1 and stride == 1 and pad == 0 and not cw.ups and pro is None and pro_act == L.ACT_NONE
                 and cscale == 1.0 and x.t.dtype == torch.bfloat16 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
+        if getattr(cw, "lane16", False):
+            flags |= L.CONV_W_LANE16  # persistent MRF kernel (csrc/mrf.hip)
         a.flags = flags
         st = None
         if stats_key is not None:
             Cc = _rup(cw.Co, 8)
-            ntile = (a.T_out + L.CONV_TILE_ROWS - 1) // L.CONV_TILE_ROWS
+            ntile = (a.T_out + L.CONV_STAT_ROWS - 1) // L.CONV_STAT_ROWS
             slab = self._slab(y.B * ntile * Cc * 2)
             a.stat_part, a.stat_ld = slab.data_ptr(), Cc
             st = (slab, Cc, self.buf(stats_key + ".m", (y.B, Cc), torch.float32),
@@ -213,7 +215,7 @@ class StyleTTSZS:
         s.mean, s.rstd, s.partial = mean.data_ptr(), rstd.data_ptr(), slab.data_ptr()
         s.stat_bs, s.B, s.T, s.C, s.eps = Cc, y.B, a.T_out, Cc, 1e-5
         self.launches += 1
-        L.check(self.lib.stzs_chan_stats_final(C.byref(s), L.CONV_TILE_ROWS, self.stream()), "chan_stats_final")
+        L.check(self.lib.stzs_chan_stats_final(C.byref(s), L.CONV_STAT_ROWS, self.stream()), "chan_stats_final")
         return y, (mean, rstd, Cc)
 
     def _slab(self, n):

@@ -41,6 +41,7 @@ class ConvW:
     co_pad: int
     cic: int
     ups: int = 0
+    lane16: bool = False  # packed with the MRF kernel's channel permutation (STZS_CONV_W_LANE16)
 
 
 class Arena:
@@ -102,8 +103,17 @@ def kstep_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
     return t.reshape(ncot, nchunk * ks * kpc, 128, 32).contiguous()
 
 
-def pack_conv(A: Arena, name, w, b=None, ups=0) -> ConvW:
-    """w: Conv1d [Co, Ci, k] / Linear [Co, Ci] / ConvTranspose1d [Ci, Co, 2*ups] (ups > 0)."""
+def lane16_perm() -> torch.Tensor:
+    """packed row rr = wc*64 + nt*16 + g*4 + r of a 128-column tile holds output channel
+    wc*64 + g*16 + nt*4 + r: the MRF kernel's swapped-operand accumulators then give each lane 16
+    consecutive channels of one time step (include/stzs.h STZS_CONV_W_LANE16, csrc/mrf.hip)."""
+    rr = torch.arange(128)
+    return (rr & 64) + ((rr >> 2) & 3) * 16 + ((rr >> 4) & 3) * 4 + (rr & 3)
+
+
+def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False) -> ConvW:
+    """w: Conv1d [Co, Ci, k] / Linear [Co, Ci] / ConvTranspose1d [Ci, Co, 2*ups] (ups > 0).
+    lane16: the MRF kernel's layout (Ci % 128 == 0, Co % 16 == 0, plain conv)."""
     if ups:
         Ci, Co, k = w.shape
         assert k == 2 * ups
@@ -124,9 +134,13 @@ def pack_conv(A: Arena, name, w, b=None, ups=0) -> ConvW:
     co_pad = _rup(ncol, 128)
     wp = torch.zeros(ks, co_pad, ci_pad)
     wp[:, :ncol, :Ci] = wk
+    if lane16:
+        assert not ups and Ci % 128 == 0 and Co % 16 == 0, (name, Ci, Co)
+        perm = lane16_perm()
+        wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, perm].reshape(ks, co_pad, ci_pad)
     wn = A.add(name + ".wpk", kstep_stream(wp, cic).to(torch.bfloat16))
     bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups)
+    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16)
 
 
 @dataclass
@@ -275,9 +289,10 @@ class PackedModel:
                 res = []
                 for m, dil in enumerate(S.rb_dils):
                     p = f"gen.rb{i}.{j}.{m}"
+                    l16 = S.gen_ch[i] % 128 == 0 and (kr - 1) * dil <= 64  # persistent MRF kernel
                     res.append(dict(
-                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"]),
-                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"]),
+                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16),
+                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"], lane16=l16),
                         a1=A.add(p + ".a1", P[p + ".alpha1"].float()), a2=A.add(p + ".a2", P[p + ".alpha2"].float()),
                         n1=p + ".n1", n2=p + ".n2", k=kr, dil=dil))
                     dec_norms += [p + ".n1", p + ".n2"]

@@ -18,10 +18,10 @@ def eng(gpu_device, tiny, tiny_params):
     return StyleTTSZS(tiny, tiny_params, device=gpu_device)
 
 
-def _pack(w, b, ups=0):
+def _pack(w, b, ups=0, lane16=False):
     from stzs.weights import Arena, pack_conv
     A = Arena()
-    cw = pack_conv(A, "t", w, b, ups=ups)
+    cw = pack_conv(A, "t", w, b, ups=ups, lane16=lane16)
     A.finalize("cuda:0")
     cw.w = A[cw.w]
     cw.b = A[cw.b] if cw.b is not None else None
@@ -180,6 +180,60 @@ def test_conv_fused_stats(eng, B, T, Ci, Co, k, dil, dt_out):
     sd = vr.sqrt()
     assert float(((m.cpu().double() - mr).abs() / (mr.abs() + sd)).max()) < 1e-5
     assert max_rel(r.cpu(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
+
+
+MRF_CASES = [
+    # B, T, C, k, dil, res, acc_in, stats
+    (3, 1000, 128, 11, 5, False, False, True),    # c1 form (3 x 8 tiles: fewer tiles than CUs)
+    (40, 1000, 128, 3, 1, True, True, False),     # last c2 form (320 tiles: persistent, 2 units on some)
+    (9, 4000, 128, 7, 3, True, False, True),      # c2 form + stats (288 tiles)
+    (2, 777, 256, 7, 1, True, True, True),        # stage-0 width: 2 input chunks x 2 column tiles
+    (1, 129, 256, 3, 5, False, False, True),      # ragged: 2 row tiles, the second with 1 valid row
+]
+
+
+@pytest.mark.parametrize("case", MRF_CASES)
+def test_mrf_persistent_conv(eng, case):
+    """persistent warp-specialised MRF conv (csrc/mrf.hip, STZS_CONV_W_LANE16 weights): AdaIN + Snake
+    prologue, residual / alpha / acc_in epilogue and fused statistics vs the fp32 reference.
+    tolerance: max-abs error <= 1.5e-2 of max|ref| (bf16 output); statistics 1e-5 of the stored tensor."""
+    B, T, C, k, dil, hr, ha, st = case
+    g = torch.Generator().manual_seed(B * T + C + k)
+    pad = dil * (k - 1) // 2
+    x = bf(torch.randn(B, T, C, generator=g))
+    w = torch.randn(C, C, k, generator=g) / math.sqrt(C * k)
+    b = torch.randn(C, generator=g) * 0.1
+    mean = torch.randn(B, C, generator=g) * 0.1
+    rstd = torch.rand(B, C, generator=g) + 0.5
+    gb = torch.randn(B, 2 * C, generator=g) * 0.2
+    alpha = torch.rand(C, generator=g) + 0.5
+    res = bf(torch.randn(B, T, C, generator=g)) if hr else None
+    acc = bf(torch.randn(B, T, C, generator=g)) if ha else None
+    sc = (1 + gb[:, :C]) * rstd
+    sh = gb[:, C:] - mean * sc
+    osc = 1 / 3 if ha else 1.0
+    ref = conv_ref(x, w, b, pad=pad, dil=dil, stride=1, sc=sc, sh=sh, pro_act="snake", alpha=alpha,
+                   res=res, out_scale=osc, acc_in=acc, beta=1.0)
+    cw, _A = _pack(w, b, lane16=True)
+    from stzs import _lib as L
+    xd = _act(x.to(torch.bfloat16).cuda())
+    yd = _act(torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda:0"))
+    keep = [mean.cuda(), rstd.cuda(), gb.cuda(), alpha.cuda()]
+    rd = _act(res.to(torch.bfloat16).cuda()) if hr else None
+    ad = _act(acc.to(torch.bfloat16).cuda()) if ha else None
+    out = eng.conv(cw, xd, yd, pad=pad, dil=dil, pro=(keep[0], keep[1], C, keep[2].data_ptr(), 2 * C, C),
+                   pro_act=L.ACT_SNAKE, pro_alpha=keep[3], res=rd, alpha=osc, acc_in=ad, beta=1.0,
+                   stats_key="t.mrfst" if st else None)
+    got = yd.t.float().cpu()
+    e = max_rel(got, ref)
+    print(case, "max_rel", e, "rel_l2", rel_err(got, ref))
+    assert e < 1.5e-2
+    if st:
+        _, (m, r, _) = out
+        y = yd.t.double().cpu()
+        mr, vr = y.mean(1), y.var(1, unbiased=False)
+        assert float(((m.cpu().double() - mr).abs() / (mr.abs() + vr.sqrt())).max()) < 1e-5
+        assert max_rel(r.cpu(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
 
 
 def test_row_layernorm(eng):

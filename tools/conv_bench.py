@@ -24,7 +24,7 @@ FLAGS = [int(f, 0) for f in os.environ.get("FLAGS", "0,1,2,4,3,6,5,7").split(","
 for (T, C, k, dil) in cases:
     w = torch.randn(C, C, k) / math.sqrt(C * k)
     A = Arena()
-    cw = pack_conv(A, "t", w, torch.zeros(C))
+    cw = pack_conv(A, "t", w, torch.zeros(C), lane16=os.environ.get("L16", "1") == "1")
     A.finalize("cuda:0")
     cw.w, cw.b = A[cw.w], A[cw.b]
     x = Act(torch.randn(B, T, C, device="cuda:0").to(torch.bfloat16))
@@ -37,7 +37,9 @@ for (T, C, k, dil) in cases:
     for flags in FLAGS:
         def run():
             eng.conv(cw, x, y, pad=dil * (k - 1) // 2, dil=dil, pro=(mean, rstd, C, gb.data_ptr(), 2 * C, C),
-                     pro_act=L.ACT_SNAKE, pro_alpha=al, flags=flags)
+                     pro_act=L.ACT_SNAKE, pro_alpha=al, flags=flags,
+                     res=(x if os.environ.get("RES") == "1" else None),
+                     stats_key=("bench.st" if os.environ.get("STATS") == "1" else None))
         run()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
