@@ -7,9 +7,10 @@
 //     workgroups; workgroup p owns hidden units [32p, 32p + 32) = 128 gate columns, and each of its
 //     4 waves keeps ITS gate's 2 x (H/32) W_hh^T B-fragments in REGISTERS for the whole launch;
 //   * per step: h_{t-1} [<=64 x H] (bf16) is read from a double-buffered exchange slab with
-//     write-through (sc1) loads into an LDS A tile, 16x16x32 MFMAs give the gate pre-activations,
-//     gates meet in LDS, each thread updates 8 (utterance, unit) cells (c in registers) and
-//     publishes its h with write-through 8-B stores;
+//     16-B write-through (sc1) buffer loads, all in flight at once, into an LDS A tile; 16x16x32
+//     MFMAs give the gate pre-activations, gates meet in LDS, each thread updates 8 (utterance,
+//     unit) cells (c in registers; sigmoid / tanh from v_exp + v_rcp) and publishes its h with
+//     one 16-B write-through buffer store;
 //   * hand-off (MI355X guide, Guideline 16 'Valid forms' table row 1): every storing wave drains
 //     vmcnt(0), workgroup barrier, ONE lane adds to the direction's agent-scope arrival counter;
 //     consumers poll that counter with sc1 loads, then all loads of the slab are sc1 (no fences).
@@ -40,6 +41,11 @@ STZS_DEV unsigned poll_ge(gu32* ctr, unsigned target, gu32* err) {
     return 1;
 }
 
+STZS_DEV float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+STZS_DEV float fast_tanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
 template <int NKS>
 __global__ __launch_bounds__(256, 1) void lstm_xchg(const stzs_lstm_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -58,6 +64,8 @@ __global__ __launch_bounds__(256, 1) void lstm_xchg(const stzs_lstm_args a) {
     // exchange slab [group][dir][2][64][H] bf16, counters [group][dir] (16 words apart)
     bf16_t* X = reinterpret_cast<bf16_t*>(a.xchg) + ((long)(grp * a.ndir + dir) * 2) * MROWS * H;
     gu32* ctr = (gu32*)(a.sync) + (grp * a.ndir + dir) * 16;
+    // the slab through a buffer descriptor: 16-B write-through (sc1, aux 16) stores and loads
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(X, 0, 2 * MROWS * H * 2, 0x00020000);
     gu32* err = (gu32*)(a.sync) + 1023;
 
     // W_hh^T fragments of this wave's gate (g = wave) for the workgroup's 32 units, in registers
@@ -79,7 +87,14 @@ __global__ __launch_bounds__(256, 1) void lstm_xchg(const stzs_lstm_args a) {
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
     if (tid == 0) s_ok = 1;
 
+#ifdef STZS_LSTM_PROF
+    unsigned long long pt[6] = {0, 0, 0, 0, 0, 0}, tp = 0;
+#define PROF(i) if (tid == 0 && p == 0 && dir == 0) { unsigned long long n_ = __builtin_amdgcn_s_memtime(); if (i) pt[i] += n_ - tp; tp = n_; }
+#else
+#define PROF(i)
+#endif
     for (int s = 0; s < a.T; ++s) {
+        PROF(0)
         const int t = dir == 0 ? s : a.T - 1 - s;
         // gate input projections of this thread's cells (issued early, consumed after the MFMAs)
         float gx[4][8];
@@ -91,16 +106,22 @@ __global__ __launch_bounds__(256, 1) void lstm_xchg(const stzs_lstm_args a) {
             for (int e = tid; e < MROWS * hp / 8; e += 256) reinterpret_cast<uint4*>(As)[e] = make_uint4(0, 0, 0, 0);
         } else {
             if (tid == 0 && s_ok) s_ok = poll_ge(ctr, (unsigned)(P * s), err);  // after a timeout: no more spins
+            PROF(1)
             __syncthreads();
-            gu64* src = (gu64*)(X + (long)((s - 1) & 1) * MROWS * H);
-            const int n8 = MROWS * H / 4;  // 8-byte words
-            for (int e = tid; e < n8; e += 256) {
-                const unsigned long long v = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const int r = (e * 4) / H, k = (e * 4) - r * H;
-                *reinterpret_cast<unsigned long long*>(As + r * hp + k) = v;
+            // h_{s-1}: MROWS x H bf16 = H/8 16-B words per row, all of this thread's sc1 loads in flight
+            const int base = ((s - 1) & 1) * MROWS * H * 2;
+            constexpr int NW = MROWS * NKS * 32 / 8 / 256;  // 16-B words per thread (H = 32 NKS)
+            u32x4 v[NW];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + (tid + i * 256) * 16, 0, 16);
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int e = tid + i * 256, r = (e * 8) / H, k = (e * 8) - r * H;
+                *reinterpret_cast<u32x4*>(As + r * hp + k) = v[i];
             }
         }
         __syncthreads();
+        PROF(2)
         // ---- gates of this wave's gate g = wave for all rows: [64 x 32 units] ----
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
@@ -120,6 +141,7 @@ __global__ __launch_bounds__(256, 1) void lstm_xchg(const stzs_lstm_args a) {
             }
         }
         __syncthreads();
+        PROF(3)
         // ---- cell update, publish h ----
         float hv[8];
 #pragma unroll
@@ -127,23 +149,27 @@ __global__ __launch_bounds__(256, 1) void lstm_xchg(const stzs_lstm_args a) {
             const float* gr = gs + crow * gp + cu0 + j;
             const float gi = gr[0] + gx[0][j], gf = gr[UNITS] + gx[1][j], gg = gr[2 * UNITS] + gx[2][j],
                         go = gr[3 * UNITS] + gx[3][j];
-            const float ig = 1.f / (1.f + __expf(-gi));
-            const float fg = 1.f / (1.f + __expf(-gf));
-            const float og = 1.f / (1.f + __expf(-go));
-            c[j] = fg * c[j] + ig * tanhf(gg);
-            hv[j] = og * tanhf(c[j]);
+            const float ig = fast_sigmoid(gi), fg = fast_sigmoid(gf), og = fast_sigmoid(go);
+            c[j] = fg * c[j] + ig * fast_tanh(gg);
+            hv[j] = og * fast_tanh(c[j]);
         }
         const uint4 hb = pack8(hv);
         if (cvalid) {
             *reinterpret_cast<uint4*>(Y + (long)cb * a.bsy + (long)t * a.ldy + dir * H + p * UNITS + cu0) = hb;
-            gu64* dst = (gu64*)(X + (long)(s & 1) * MROWS * H + crow * H + p * UNITS + cu0);
-            __hip_atomic_store(dst, ((unsigned long long)hb.y << 32) | hb.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(dst + 1, ((unsigned long long)hb.w << 32) | hb.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u32x4 hw = {hb.x, hb.y, hb.z, hb.w};
+            __builtin_amdgcn_raw_buffer_store_b128(hw, xr, ((s & 1) * MROWS * H + crow * H + p * UNITS + cu0) * 2, 0, 16);
         }
+        PROF(4)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        PROF(5)
     }
+#ifdef STZS_LSTM_PROF
+    if (tid == 0 && p == 0 && dir == 0)
+        for (int i = 1; i < 6; ++i) ((unsigned long long*)a.sync)[256 + i] = pt[i];
+#endif
+#undef PROF
 }
 
 }  // namespace
