@@ -1,0 +1,12 @@
+#!/bin/bash
+# HBM traffic of the dominant kernel on the bench workload: two separate PMC passes (kernel-trace only)
+# over the eager bench command, summarised into profiles/<tag>_pmc_mrf.json.   usage: tools/pmc_bench.sh <tag>
+tag=${1:-r01}
+export TMPDIR=/tmp
+out=gpurun_out/pmcb_$tag
+for c in FETCH_SIZE WRITE_SIZE; do
+  mkdir -p $out/$c
+  timeout -k 10 400 rocprofv3 --pmc $c --kernel-trace -d $GRAFT_REPO_ROOT/$out/$c -o run --output-format csv -- \
+    python3 bench.py --steps 1 --warmup 1 --no-cpu --no-latency --no-graph > $out/$c.log 2>&1 || { echo "PMC $c failed"; tail -5 $out/$c.log; exit 1; }
+done
+python3 tools/pmc_traffic.py $out mrf_conv > profiles/${tag}_pmc_mrf.json && cat profiles/${tag}_pmc_mrf.json
