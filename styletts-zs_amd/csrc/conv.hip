@@ -114,6 +114,7 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
         kg[j] = c_gate[cv * 8 + j];
     }
     const bool stat = !FLAT && a.stat_part != nullptr;
+    const bool gate_vec = (reinterpret_cast<uintptr_t>(a.gate) & 15) == 0 && a.gate_bs % 4 == 0;
     float st_s[8], st_q[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
@@ -180,13 +181,22 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
             if (!pv[i]) continue;
             const int tl = ((v0 + tid) >> 4) + i * (NTHR >> 4);
             const long bb = pb[i], t = pt[i];
-            float u[8];
+            float u[8], gv[8];
+            if (FLAT && a.gate) {  // DiT gate of this row's utterance: two 16-B loads when aligned
+                const float* gp = a.gate + bb * a.gate_bs;
+                if (gate_vec && co + 8 <= a.Co) {
+                    load8(gp + co, gv);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) gv[j] = gp[min(co + j, a.Co - 1)];
+                }
+            }
             const float* er = ep + tl * EP_PITCH + cv * 8;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 float x = epi_act<EACT>(er[j] + kb[j], a.epi_slope);
                 if (FLAT) {
-                    if (a.gate) x *= a.gate[bb * a.gate_bs + min(co + j, a.Co - 1)];
+                    if (a.gate) x *= gv[j];
                 } else {
                     x *= kg[j];
                 }
@@ -507,15 +517,17 @@ STZS_DEV void glds16(const void* src, void* dst) {
                                      (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
-// Pure GEMM for bf16 linears (ks = 1, no prologue): BOTH operands stream through LDS-DMA rings,
-// one 32-wide K-step per slot (A: 128 rows x 32 k, B: 128 cols x 32 k, 8 KB each), two K-steps in
-// flight.  The A image takes the same XOR swizzle as B through its per-lane SOURCE addresses
-// (LDS-DMA writes lane-linearly), so both fragment reads are conflict-free ds_read_b128.
+// Pure GEMM for bf16 linears (ks = 1, no prologue): BOTH operands stream through an LDS-DMA ring,
+// one 32-wide K-step per slot (A: 128 rows x 32 k, B: 128 cols x 32 k, 8 KB each), 4 slots filled
+// three K-steps ahead.  The A image takes the same XOR swizzle as B through its per-lane SOURCE
+// addresses (LDS-DMA writes lane-linearly), so both fragment reads are conflict-free ds_read_b128.
+// Per K-step: counted vmcnt + one s_barrier, then the NEXT K-step's fragments are read between the
+// current K-step's 16 MFMAs (as csrc/mrf.hip); the body is branch-free (a fill past the end re-copies
+// the last K-step into a retired slot) and the last K-step is peeled.
+constexpr int GSLOT = 2 * SLOT_BYTES;  // A + B of one K-step
 template <typename TOut>
 __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* ringA = smem;
-    unsigned char* ringB = smem + NSLOT * SLOT_BYTES;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
     const long row0 = (long)blockIdx.x * BT;
@@ -534,50 +546,77 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         asrc[i] = bb * a.bsx + (R - bb * a.T_in) * a.ldx + ((p ^ gswz(r)) << 3);
     }
     auto fill = [&](int k) {
-        const bf16_t* src = Wt + (long)k * (BCO * 32) + wave * 1024 + lane * 8;
-        unsigned char* db = ringB + (k % NSLOT) * SLOT_BYTES + wave * 2048;
-        unsigned char* da = ringA + (k % NSLOT) * SLOT_BYTES + wave * 2048;
+        const int kc = k < NK ? k : NK - 1;
+        const bf16_t* src = Wt + (long)kc * (BCO * 32) + wave * 1024 + lane * 8;
+        unsigned char* da = smem + (k & 3) * GSLOT + wave * 2048;
+        unsigned char* db = da + SLOT_BYTES;
         glds16(src, db);
         glds16(src + 512, db + 1024);
-        glds16(X + asrc[0] + k * 32, da);
-        glds16(X + asrc[1] + k * 32, da + 1024);
+        glds16(X + asrc[0] + kc * 32, da);
+        glds16(X + asrc[1] + kc * 32, da + 1024);
     };
-    int aoff[4], boff[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int ra = wt * 64 + i * 16 + (lane & 15);
-        aoff[i] = ra * 64 + (((lane >> 4) ^ gswz(ra)) << 4);
-        const int rb = wc * 64 + i * 16 + (lane & 15);
-        boff[i] = rb * 64 + (((lane >> 4) ^ gswz(rb)) << 4);
+    int aoff0, boff0;
+    {
+        const int ra = wt * 64 + (lane & 15);
+        aoff0 = ra * 64 + (((lane >> 4) ^ gswz(ra)) << 4);
+        const int rb = wc * 64 + (lane & 15);
+        boff0 = SLOT_BYTES + rb * 64 + (((lane >> 4) ^ gswz(rb)) << 4);
     }
     f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    fill(0);
-    if (NK > 1) fill(1);
-    for (int k = 0; k < ((a.flags & 2) ? 0 : NK); ++k) {
-        if (k + 1 < NK)
-            __builtin_amdgcn_s_waitcnt(0x0F70 | 4);
-        else
-            __builtin_amdgcn_s_waitcnt(0x0F70 | 0);
-        __builtin_amdgcn_s_barrier();
-        if (k + 2 < NK) fill(k + 2);
-        const unsigned char* sa = ringA + (k % NSLOT) * SLOT_BYTES;
-        const unsigned char* sb = ringB + (k % NSLOT) * SLOT_BYTES;
-        bf16x8 af[4], bw[4];
+    bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
+    auto rd = [&](bf16x8 (&fa)[4], bf16x8 (&fb)[4], int k) {
+        const unsigned char* sl = smem + (k & 3) * GSLOT;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sa + aoff[i]);
+        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(sl + aoff0 + i * 1024);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) bw[i] = *reinterpret_cast<const bf16x8*>(sb + boff[i]);
-        __builtin_amdgcn_sched_barrier(0);
+        for (int i = 0; i < 4; ++i) fb[i] = *reinterpret_cast<const bf16x8*>(sl + boff0 + i * 1024);
+    };
+    auto mma = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[4]) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bw[nt], acc[mt][nt], 0, 0, 0);
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+    };
+    fill(0);
+    fill(1);
+    __builtin_amdgcn_s_waitcnt(0x0F70 | 4);  // K-step 0 landed (K-step 1 may be in flight)
+    __builtin_amdgcn_s_barrier();
+    fill(2);
+    rd(fa0, fb0, 0);
+#define STZS_GEMM_STEP(FA, FB, NA, NB)                                          \
+    {                                                                           \
+        __builtin_amdgcn_s_waitcnt(0x0F70 | 4);                                 \
+        __builtin_amdgcn_s_barrier();                                           \
+        fill(k + 3);                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                      \
+        rd(NA, NB, k + 1);                                                      \
+        mma(FA, FB);                                                            \
+        _Pragma("unroll") for (int ii = 0; ii < 8; ++ii) {                      \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  \
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                  \
+        }                                                                       \
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                      \
+        __builtin_amdgcn_sched_barrier(0);                                      \
+        ++k;                                                                    \
     }
+    int k = 0;
+    const int nsteps = (a.flags & 2) ? 1 : NK;
+    for (; k + 2 < nsteps;) {
+        STZS_GEMM_STEP(fa0, fb0, fa1, fb1)
+        STZS_GEMM_STEP(fa1, fb1, fa0, fb0)
+    }
+    if (k + 1 < nsteps) {
+        STZS_GEMM_STEP(fa0, fb0, fa1, fb1)
+        mma(fa1, fb1);
+    } else {
+        mma(fa0, fb0);
+    }
+#undef STZS_GEMM_STEP
     finish<TOut, true>(a, acc, smem, 0, 0, row0);
 }
 
@@ -600,7 +639,8 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     if (flat && a.stat_part) return STZS_EINVAL;  // fused statistics: per-utterance tiles only
     void (*k)(stzs_conv_args);
     if (flat && sizeof(TIn) == 2 && (a.flags & STZS_CONV_A_DMA) && a.pro_cscale == 1.f) {
-        const size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4;
+        size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
+        lg = lg > 4 * (size_t)GSLOT ? lg : 4 * (size_t)GSLOT;
         auto kg = gemm_glds<TOut>;
         (void)hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);
         hipLaunchKernelGGL(kg, grid, dim3(NTHR), lg, s, a);
