@@ -1,5 +1,6 @@
 // The MRF conv (the generator's AdaINResBlock1 convs, about half of all
-// synthesis time) on gfx950.
+// synthesis time) on gfx950 -- also the k3 convs of the decoder / prosody-predictor AdaIN residual
+// blocks (a9, a11) with a LeakyReLU or identity prologue and the nearest-x2 residual (t / res_tdiv).
 //
 // y[b, t, co] = epi( sum_{tap, ci} W[tap, co, ci] * snake(adain(x))[b, t + tap*dil - pad, ci] ),
 // 128-channel input chunks, bf16 in / out, stride 1; epi = ((v + bias + res) * alpha + beta * acc_in),
@@ -44,7 +45,7 @@ STZS_DEV float row_sum16(float x) {
     return x;
 }
 
-template <bool HR, bool HA>
+template <int PACT, bool HR, bool HA>
 __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ks = a.ks, dil = a.dil;
@@ -102,14 +103,16 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
         __syncthreads();  // every wave is done reading the previous chunk's input tile
         if (!(a.flags & 1)) {
             const int c = cc * 128 + cv * 8;
+            const bool c_ok = c < a.Ci;  // vectors past Ci (ci_pad > Ci) are zero; weights there are 0
+            const int cl = c_ok ? c : 0;
             uint4 raw[SB];
             bool okv[SB];
 #pragma unroll
             for (int i = 0; i < SB; ++i) {
                 int tin = t0 - a.pad + rsub + 16 * i;
-                okv[i] = tin >= 0 && tin < a.T_in;
+                okv[i] = c_ok && tin >= 0 && tin < a.T_in;
                 tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
-                raw[i] = *reinterpret_cast<const uint4*>(X + (long)tin * a.ldx + c);
+                raw[i] = *reinterpret_cast<const uint4*>(X + (long)tin * a.ldx + cl);
             }
             // per-channel constants, computed once per channel by 128 threads into the ring slot that
             // stays idle until this chunk's first K-step fills it (slot (k + 3) & 3):
@@ -117,37 +120,45 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
             float* cs = reinterpret_cast<float*>(ring + ((k + 3) & (NSL - 1)) * SLOT);
             if (tid < 128) {
                 const int ch = cc * 128 + tid;
-                float sc, sh;
-                if (a.pro_mode == STZS_PRO_ADAIN) {
+                const bool ok = ch < a.Ci;
+                float sc = 0.f, sh = 0.f;
+                if (ok && a.pro_mode == STZS_PRO_ADAIN) {
                     const float mu = a.pro_mean[(long)bq * a.stat_bs + ch];
                     const float rs = a.pro_rstd[(long)bq * a.stat_bs + ch];
                     const float gm = a.pro_gb[(long)bq * a.gb_bs + ch];
                     const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + ch];
                     sc = (1.f + gm) * rs;
                     sh = be - mu * sc;
-                } else {
+                } else if (ok) {
                     sc = a.pro_cscale;
-                    sh = 0.f;
                 }
-                const float al = a.pro_alpha[ch];
-                const float h = 0.5f / al;
-                const float w = al * 0.318309886183790672f;  // a / pi
-                cs[tid] = sc * w;
-                cs[128 + tid] = sh * w;
-                cs[256 + tid] = sc;
-                cs[384 + tid] = sh + h;
-                cs[512 + tid] = -h;
+                if constexpr (PACT == STZS_ACT_SNAKE) {
+                    const float al = ok ? a.pro_alpha[ch] : 1.f;
+                    const float h = 0.5f / al;
+                    const float w = al * 0.318309886183790672f;  // a / pi
+                    cs[tid] = sc * w;
+                    cs[128 + tid] = sh * w;
+                    cs[256 + tid] = sc;
+                    cs[384 + tid] = sh + h;
+                    cs[512 + tid] = -h;
+                } else {  // LeakyReLU / identity: y = x*sc + sh
+                    cs[256 + tid] = sc;
+                    cs[384 + tid] = sh;
+                }
             }
             __syncthreads();
             float ka[8], kb[8], ksc[8], ksh[8], km[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                ka[j] = cs[cv * 8 + j];
-                kb[j] = cs[128 + cv * 8 + j];
                 ksc[j] = cs[256 + cv * 8 + j];
                 ksh[j] = cs[384 + cv * 8 + j];
-                km[j] = cs[512 + cv * 8 + j];
+                if constexpr (PACT == STZS_ACT_SNAKE) {
+                    ka[j] = cs[cv * 8 + j];
+                    kb[j] = cs[128 + cv * 8 + j];
+                    km[j] = cs[512 + cv * 8 + j];
+                }
             }
+            const float slope = a.pro_slope;
 #pragma unroll
             for (int i = 0; i < SB; ++i) {
                 const int r = rsub + 16 * i;
@@ -158,10 +169,14 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
                     for (int p = 0; p < 4; ++p) {
                         const float x0 = __uint_as_float(w[p] << 16), x1 = __uint_as_float(w[p] & 0xFFFF0000u);
                         const int j0 = 2 * p, j1 = 2 * p + 1;
-                        const float c0 = __builtin_amdgcn_cosf(fmaf(x0, ka[j0], kb[j0]));
-                        const float c1 = __builtin_amdgcn_cosf(fmaf(x1, ka[j1], kb[j1]));
-                        const float y0 = fmaf(c0, km[j0], fmaf(x0, ksc[j0], ksh[j0]));
-                        const float y1 = fmaf(c1, km[j1], fmaf(x1, ksc[j1], ksh[j1]));
+                        float y0 = fmaf(x0, ksc[j0], ksh[j0]), y1 = fmaf(x1, ksc[j1], ksh[j1]);
+                        if constexpr (PACT == STZS_ACT_SNAKE) {
+                            y0 = fmaf(__builtin_amdgcn_cosf(fmaf(x0, ka[j0], kb[j0])), km[j0], y0);
+                            y1 = fmaf(__builtin_amdgcn_cosf(fmaf(x1, ka[j1], kb[j1])), km[j1], y1);
+                        } else if constexpr (PACT == STZS_ACT_LEAKY) {
+                            y0 = y0 >= 0.f ? y0 : y0 * slope;
+                            y1 = y1 >= 0.f ? y1 : y1 * slope;
+                        }
                         o[p] = okv[i] ? ((uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16)) : 0u;
                     }
                     *reinterpret_cast<uint4*>(smem + r * P + cv * 16) = make_uint4(o[0], o[1], o[2], o[3]);
@@ -221,8 +236,8 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
     for (int mt = 0; mt < 4; ++mt) {
         const int t = t0 + wt * 64 + mt * 16 + n;
         const int tc = t < a.T_out ? t : a.T_out - 1;
-        if constexpr (HR) {
-            const bf16_t* p = reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr + (long)tc * a.ldr + coc;
+        if constexpr (HR) {  // (row t / res_tdiv: the nearest-x2 shortcut of an upsampling block)
+            const bf16_t* p = reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr + (long)(tc / a.res_tdiv) * a.ldr + coc;
             rr[mt][0] = *reinterpret_cast<const uint4*>(p);
             rr[mt][1] = *reinterpret_cast<const uint4*>(p + 8);
         }
@@ -315,23 +330,31 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
 // internal entry used by stzs_conv1d for STZS_CONV_W_LANE16 weights
 __attribute__((visibility("hidden"))) int stzs_mrf_conv_launch(const stzs_conv_args& a, hipStream_t s) {
     const int rows_in = BT + (a.ks - 1) * a.dil;
-    if (a.stride != 1 || a.cic != 128 || a.Ci % 128 || a.ci_pad % 128 || a.Co % 16 || rows_in > 16 * SB ||
-        a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.ups || a.pro_act != STZS_ACT_SNAKE || !a.pro_alpha ||
-        a.gate || a.epi_act != STZS_ACT_NONE || a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8)) ||
-        (a.acc_in && (a.lda % 8 || a.bsa % 8)) || a.res_tdiv != 1)
+    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 16 || rows_in > 16 * SB ||
+        a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.ups || a.gate || a.epi_act != STZS_ACT_NONE ||
+        a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8)) || (a.acc_in && (a.lda % 8 || a.bsa % 8)))
         return STZS_ESHAPE;
+    if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
     const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + NSL * SLOT;
     if (lds > 160 * 1024) return STZS_ESHAPE;
     dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / BCO);
-    void (*k)(stzs_conv_args);
-    if (a.res && a.acc_in)
-        k = mrf_conv<true, true>;
-    else if (a.res)
-        k = mrf_conv<true, false>;
-    else if (a.acc_in)
-        k = mrf_conv<false, true>;
-    else
-        k = mrf_conv<false, false>;
+    void (*k)(stzs_conv_args) = nullptr;
+    if (a.pro_act == STZS_ACT_SNAKE) {
+        if (a.res && a.acc_in)
+            k = mrf_conv<STZS_ACT_SNAKE, true, true>;
+        else if (a.res)
+            k = mrf_conv<STZS_ACT_SNAKE, true, false>;
+        else if (a.acc_in)
+            k = mrf_conv<STZS_ACT_SNAKE, false, true>;
+        else
+            k = mrf_conv<STZS_ACT_SNAKE, false, false>;
+    } else if (!a.acc_in) {  // the AdaIN residual blocks of the decoder / prosody predictor
+        if (a.pro_act == STZS_ACT_LEAKY)
+            k = a.res ? mrf_conv<STZS_ACT_LEAKY, true, false> : mrf_conv<STZS_ACT_LEAKY, false, false>;
+        else if (a.pro_act == STZS_ACT_NONE)
+            k = a.res ? mrf_conv<STZS_ACT_NONE, true, false> : mrf_conv<STZS_ACT_NONE, false, false>;
+    }
+    if (!k) return STZS_ESHAPE;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
     STZS_LAUNCH_CHECK();

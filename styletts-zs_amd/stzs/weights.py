@@ -135,7 +135,7 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False) -> ConvW:
     wp = torch.zeros(ks, co_pad, ci_pad)
     wp[:, :ncol, :Ci] = wk
     if lane16:
-        assert not ups and Ci % 128 == 0 and Co % 16 == 0, (name, Ci, Co)
+        assert not ups and cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, perm].reshape(ks, co_pad, ci_pad)
     wn = A.add(name + ".wpk", kstep_stream(wp, cic).to(torch.bfloat16))
@@ -206,9 +206,16 @@ class BlkW:
     pool_b: Optional[str]
 
 
+def _lane16_ok(w) -> bool:
+    """conv eligible for the MRF-family kernel (csrc/mrf.hip): 128-channel input chunks, Co % 16 == 0."""
+    Co, Ci = w.shape[0], w.shape[1]
+    return Ci > 64 and Co % 16 == 0
+
+
 def pack_blk(A: Arena, P, name, up=False) -> BlkW:
-    c1 = pack_conv(A, name + ".conv1", P[name + ".conv1.w"], P[name + ".conv1.b"])
-    c2 = pack_conv(A, name + ".conv2", P[name + ".conv2.w"], P[name + ".conv2.b"])
+    w1, w2 = P[name + ".conv1.w"], P[name + ".conv2.w"]
+    c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1))
+    c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2))
     sc = pack_conv(A, name + ".sc", P[name + ".sc.w"]) if name + ".sc.w" in P else None
     pw = pb = None
     if up:

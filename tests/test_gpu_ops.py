@@ -183,47 +183,55 @@ def test_conv_fused_stats(eng, B, T, Ci, Co, k, dil, dt_out):
 
 
 MRF_CASES = [
-    # B, T, C, k, dil, res, acc_in, stats
-    (3, 1000, 128, 11, 5, False, False, True),    # c1 form (3 x 8 tiles: fewer tiles than CUs)
-    (40, 1000, 128, 3, 1, True, True, False),     # last c2 form (320 tiles: persistent, 2 units on some)
-    (9, 4000, 128, 7, 3, True, False, True),      # c2 form + stats (288 tiles)
-    (2, 777, 256, 7, 1, True, True, True),        # stage-0 width: 2 input chunks x 2 column tiles
-    (1, 129, 256, 3, 5, False, False, True),      # ragged: 2 row tiles, the second with 1 valid row
+    # B, T, Ci, Co, k, dil, prologue, res, acc_in, stats, res_tdiv
+    (3, 1000, 128, 128, 11, 5, "snake", False, False, True, 1),  # c1 form (fewer tiles than CUs)
+    (40, 1000, 128, 128, 3, 1, "snake", True, True, False, 1),   # last c2 form (320 tiles)
+    (9, 4000, 128, 128, 7, 3, "snake", True, False, True, 1),    # c2 form + stats (288 tiles)
+    (2, 777, 256, 256, 7, 1, "snake", True, True, True, 1),      # stage-0 width: 2 input chunks x 2 column tiles
+    (1, 129, 256, 256, 3, 5, "snake", False, False, True, 1),    # ragged: the second row tile has 1 valid row
+    (3, 400, 1090, 256, 3, 1, "leaky", True, False, True, 2),    # decoder block conv2: Ci 1090 (9 chunks), x2 shortcut
+    (4, 200, 200, 96, 3, 1, "leaky", False, False, True, 1),     # predictor block conv1 (2 chunks, 1 column tile)
+    (2, 300, 130, 64, 3, 1, "none", False, False, True, 1),      # up-block conv1 after the dw-ConvT: no prologue
 ]
 
 
 @pytest.mark.parametrize("case", MRF_CASES)
 def test_mrf_persistent_conv(eng, case):
-    """persistent warp-specialised MRF conv (csrc/mrf.hip, STZS_CONV_W_LANE16 weights): AdaIN + Snake
-    prologue, residual / alpha / acc_in epilogue and fused statistics vs the fp32 reference.
-    tolerance: max-abs error <= 1.5e-2 of max|ref| (bf16 output); statistics 1e-5 of the stored tensor."""
-    B, T, C, k, dil, hr, ha, st = case
-    g = torch.Generator().manual_seed(B * T + C + k)
+    """MRF-family conv (csrc/mrf.hip, STZS_CONV_W_LANE16 weights): AdaIN + Snake / LeakyReLU / identity
+    prologue, residual (at t / res_tdiv) / alpha / acc_in epilogue and fused statistics vs the fp32
+    reference.  tolerance: max-abs error <= 1.5e-2 of max|ref| (bf16 output); statistics 1e-5 of the
+    stored tensor."""
+    B, T, Ci, Co, k, dil, act, hr, ha, st, tdiv = case
+    g = torch.Generator().manual_seed(B * T + Ci + k)
     pad = dil * (k - 1) // 2
-    x = bf(torch.randn(B, T, C, generator=g))
-    w = torch.randn(C, C, k, generator=g) / math.sqrt(C * k)
-    b = torch.randn(C, generator=g) * 0.1
-    mean = torch.randn(B, C, generator=g) * 0.1
-    rstd = torch.rand(B, C, generator=g) + 0.5
-    gb = torch.randn(B, 2 * C, generator=g) * 0.2
-    alpha = torch.rand(C, generator=g) + 0.5
-    res = bf(torch.randn(B, T, C, generator=g)) if hr else None
-    acc = bf(torch.randn(B, T, C, generator=g)) if ha else None
-    sc = (1 + gb[:, :C]) * rstd
-    sh = gb[:, C:] - mean * sc
-    osc = 1 / 3 if ha else 1.0
-    ref = conv_ref(x, w, b, pad=pad, dil=dil, stride=1, sc=sc, sh=sh, pro_act="snake", alpha=alpha,
-                   res=res, out_scale=osc, acc_in=acc, beta=1.0)
+    x = bf(torch.randn(B, T, Ci, generator=g))
+    w = torch.randn(Co, Ci, k, generator=g) / math.sqrt(Ci * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    mean = torch.randn(B, Ci, generator=g) * 0.1
+    rstd = torch.rand(B, Ci, generator=g) + 0.5
+    gb = torch.randn(B, 2 * Ci, generator=g) * 0.2
+    alpha = torch.rand(Ci, generator=g) + 0.5
+    res = bf(torch.randn(B, (T + tdiv - 1) // tdiv, Co, generator=g)) if hr else None
+    acc = bf(torch.randn(B, T, Co, generator=g)) if ha else None
+    sc = (1 + gb[:, :Ci]) * rstd
+    sh = gb[:, Ci:] - mean * sc
+    if act == "none":
+        sc, sh = torch.ones(B, Ci), torch.zeros(B, Ci)
+    osc = 1 / 3 if ha else (0.7071 if hr else 1.0)
+    ref = conv_ref(x, w, b, pad=pad, dil=dil, stride=1, sc=sc, sh=sh, pro_act=None if act == "none" else act,
+                   slope=0.2, alpha=alpha, res=res, res_tdiv=tdiv, out_scale=osc, acc_in=acc, beta=1.0)
     cw, _A = _pack(w, b, lane16=True)
     from stzs import _lib as L
-    xd = _act(x.to(torch.bfloat16).cuda())
-    yd = _act(torch.zeros(B, T, C, dtype=torch.bfloat16, device="cuda:0"))
+    xd = _act(_dev_ntc(x, (Ci + 7) // 8 * 8), Ci)
+    yd = _act(torch.zeros(B, T, Co, dtype=torch.bfloat16, device="cuda:0"))
     keep = [mean.cuda(), rstd.cuda(), gb.cuda(), alpha.cuda()]
     rd = _act(res.to(torch.bfloat16).cuda()) if hr else None
     ad = _act(acc.to(torch.bfloat16).cuda()) if ha else None
-    out = eng.conv(cw, xd, yd, pad=pad, dil=dil, pro=(keep[0], keep[1], C, keep[2].data_ptr(), 2 * C, C),
-                   pro_act=L.ACT_SNAKE, pro_alpha=keep[3], res=rd, alpha=osc, acc_in=ad, beta=1.0,
-                   stats_key="t.mrfst" if st else None)
+    pro = None if act == "none" else (keep[0], keep[1], Ci, keep[2].data_ptr(), 2 * Ci, Ci)
+    pa = {"snake": L.ACT_SNAKE, "leaky": L.ACT_LEAKY, "none": L.ACT_NONE}[act]
+    out = eng.conv(cw, xd, yd, pad=pad, dil=dil, pro=pro, pro_act=pa, pro_slope=0.2,
+                   pro_alpha=keep[3] if act == "snake" else None, res=rd, res_tdiv=tdiv, alpha=osc, acc_in=ad,
+                   beta=1.0, stats_key="t.mrfst" if st else None)
     got = yd.t.float().cpu()
     e = max_rel(got, ref)
     print(case, "max_rel", e, "rel_l2", rel_err(got, ref))
