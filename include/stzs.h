@@ -87,6 +87,11 @@ typedef struct stzs_conv_args {
  * output channel wc*64 + g*16 + nt*4 + r.  Selects the persistent MRF conv (csrc/mrf.hip): Snake
  * prologue, bf16 in/out, Ci % 128 == 0, Co % 16 == 0, stride 1, no gate/ups/epilogue activation. */
 #define STZS_CONV_W_LANE16 16
+/* flags bit: narrow weights (Co <= 32) packed as [NK][32][32] K-steps with packed row nt*16 + g*4 + r
+ * holding output channel g*8 + nt*4 + r (stzs/weights.py pack_conv(narrow32=True)).  Selects the
+ * narrow conv of csrc/mrf.hip: 128-channel chunks, bf16 in, fp32 out, LeakyReLU / identity prologue
+ * (no AdaIN), bias, alpha; no residual / gate / statistics.  (conv_post: 128 -> 22 channels) */
+#define STZS_CONV_W_NARROW32 32
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------

@@ -663,7 +663,8 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
 
 }  // namespace
 
-int stzs_mrf_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrf.hip
+int stzs_mrf_conv_launch(const stzs_conv_args& a, hipStream_t s);     // csrc/mrf.hip
+int stzs_narrow_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrf.hip
 
 extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
     if (!a || !a->x || !a->w || !a->y) return STZS_EINVAL;
@@ -690,6 +691,7 @@ extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
         return STZS_EINVAL;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (a->flags & STZS_CONV_W_LANE16) return stzs_mrf_conv_launch(*a, s);
+    if (a->flags & STZS_CONV_W_NARROW32) return stzs_narrow_conv_launch(*a, s);
     if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) return launch_dt<bf16_t, bf16_t>(*a, s);
     if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) return launch_dt<bf16_t, float>(*a, s);
     if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_BF16) return launch_dt<float, bf16_t>(*a, s);

@@ -325,6 +325,167 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Narrow conv (Co <= 32): conv_post (128 -> 22 channels, k 7, LeakyReLU(0.01) prologue, fp32 out) at
+// the full frame rate.  A 128-column tile would waste 5/6 of the MFMAs; here a workgroup owns 256
+// time rows x 32 channels, each wave 64 rows x 32 channels = 4 x 2 accumulators, 8 MFMAs per K-step.
+// Weights: [NK][32][32] bf16 K-steps (2 KB, packed with STZS_CONV_W_NARROW32: packed row
+// nt*16 + g*4 + r holds channel g*8 + nt*4 + r, so each lane ends up with 8 consecutive channels)
+// through a 4-slot LDS-DMA ring filled by waves 0-1; the staging / K-step / epilogue scheme is the
+// MRF kernel's.
+constexpr int NBT = 256;
+constexpr int NSLOT_B = 2048;
+constexpr int NSB = 9;  // staged vectors per thread per batch (two batches: 16 x 18 = 288 rows)
+
+__global__ __launch_bounds__(NTH, 2) void narrow_conv(const stzs_conv_args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int ks = a.ks, dil = a.dil;
+    const int rows_in = NBT + (ks - 1) * dil;
+    unsigned char* ring = smem + ((rows_in * P + 15) & ~15);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tpb = (a.T_out + NBT - 1) / NBT;
+    const int bq = blockIdx.x / tpb;
+    const int t0 = (blockIdx.x - bq * tpb) * NBT;
+    const int nchunk = a.ci_pad >> 7;
+    const int NK = nchunk * ks * 4;
+    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w);
+    auto fill = [&](int k) {  // 2 KB per K-step: one 1-KB piece from each of waves 0 and 1
+        if (wave < 2) {
+            const bf16_t* src = Wt + (long)(k < NK ? k : NK - 1) * 1024 + wave * 512 + lane * 8;
+            unsigned char* dst = ring + (k & (NSL - 1)) * NSLOT_B + wave * 1024;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+    };
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int brow = lane & 15;
+    const int boff0 = brow * 64 + (((lane >> 4) ^ gswz(brow)) << 4);
+    const int arow0 = (wave * 64 + (lane & 15)) * P + (lane >> 4) * 16;
+    bf16x8 fa0[4], fb0[2], fa1[4], fb1[2];
+    auto readB = [&](bf16x8 (&fb)[2], int k) {
+        const unsigned char* wl = ring + (k & (NSL - 1)) * NSLOT_B + boff0;
+        fb[0] = *reinterpret_cast<const bf16x8*>(wl);
+        fb[1] = *reinterpret_cast<const bf16x8*>(wl + 1024);
+    };
+    auto readA = [&](bf16x8 (&fx)[4], int off) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) fx[mt] = *reinterpret_cast<const bf16x8*>(smem + off + mt * 16 * P);
+    };
+    auto mma = [&](const bf16x8 (&fx)[4], const bf16x8 (&fw)[2]) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+                acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[nt], fx[mt], acc[nt][mt], 0, 0, 0);
+    };
+    const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x) + (long)bq * a.bsx;
+    const int cv = tid & 15, rsub = tid >> 4;
+    const float csc = a.pro_cscale, slope = a.pro_slope;
+    const bool leaky = a.pro_act == STZS_ACT_LEAKY;
+    fill(0);
+    fill(1);
+    int k = 0;
+    for (int cc = 0; cc < nchunk; ++cc) {
+        __syncthreads();
+        const int c = cc * 128 + cv * 8;
+        const bool c_ok = c < a.Ci;
+        const int cl = c_ok ? c : 0;
+#pragma unroll
+        for (int bt = 0; bt < 2; ++bt) {  // two staging batches of NSB vectors per thread
+            uint4 raw[NSB];
+#pragma unroll
+            for (int i = 0; i < NSB; ++i) {
+                int tin = t0 - a.pad + rsub + 16 * (bt * NSB + i);
+                tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+                raw[i] = *reinterpret_cast<const uint4*>(X + (long)tin * a.ldx + cl);
+            }
+#pragma unroll
+            for (int i = 0; i < NSB; ++i) {
+                const int r = rsub + 16 * (bt * NSB + i);
+                if (r < rows_in) {
+                    const int tin = t0 - a.pad + r;
+                    const bool ok = c_ok && tin >= 0 && tin < a.T_in;
+                    float f[8];
+                    unpack8(raw[i], f);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        float y = f[j] * csc;
+                        if (leaky) y = y >= 0.f ? y : y * slope;
+                        f[j] = ok ? y : 0.f;
+                    }
+                    *reinterpret_cast<uint4*>(smem + r * P + cv * 16) = pack8(f);
+                }
+            }
+        }
+        __syncthreads();
+        if (cc == 0) {
+            fill(2);
+            readB(fb0, 0);
+        }
+        readA(fa0, arow0);
+        // one K-step: fill k+1 landed (waves 0-1 hold one piece of fill k+2 in flight) -> barrier ->
+        // fill k+3 -> next fragments read between the current 8 MFMAs
+#define STZS_NARROW_STEP(FX, FW, NX, NW, AOFF)                                  \
+    {                                                                           \
+        __builtin_amdgcn_s_waitcnt(0x0F71);                                     \
+        __builtin_amdgcn_s_barrier();                                           \
+        fill(k + 3);                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                      \
+        readB(NW, k + 1);                                                       \
+        readA(NX, AOFF);                                                        \
+        mma(FX, FW);                                                            \
+        _Pragma("unroll") for (int ii = 0; ii < 6; ++ii) {                      \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  \
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                  \
+        }                                                                       \
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                      \
+        __builtin_amdgcn_sched_barrier(0);                                      \
+        ++k;                                                                    \
+    }
+        for (int tap = 0; tap + 1 < ks; ++tap) {
+            const int ab = arow0 + tap * dil * P;
+            STZS_NARROW_STEP(fa0, fb0, fa1, fb1, ab + 64)
+            STZS_NARROW_STEP(fa1, fb1, fa0, fb0, ab + 128)
+            STZS_NARROW_STEP(fa0, fb0, fa1, fb1, ab + 192)
+            STZS_NARROW_STEP(fa1, fb1, fa0, fb0, ab + dil * P)
+        }
+        const int ab = arow0 + (ks - 1) * dil * P;
+        STZS_NARROW_STEP(fa0, fb0, fa1, fb1, ab + 64)
+        STZS_NARROW_STEP(fa1, fb1, fa0, fb0, ab + 128)
+        STZS_NARROW_STEP(fa0, fb0, fa1, fb1, ab + 192)
+        if (cc + 1 < nchunk) {
+            STZS_NARROW_STEP(fa1, fb1, fa0, fb0, arow0)
+        } else {
+            mma(fa1, fb1);
+        }
+#undef STZS_NARROW_STEP
+    }
+    // epilogue: lane (g, n) holds time t = t0 + wave*64 + mt*16 + n, channels g*8 .. g*8+7 (fp32)
+    const int g = lane >> 4, n = lane & 15;
+    const int ch0 = g * 8;
+    if (ch0 >= a.Co) return;
+    float bias[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bias[i] = (a.bias && ch0 + i < a.Co) ? a.bias[ch0 + i] : 0.f;
+    float* Y = reinterpret_cast<float*>(a.y);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+        const int t = t0 + wave * 64 + mt * 16 + n;
+        if (t < a.T_out) {
+            float v[8];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[nt * 4 + r] = (acc[nt][mt][r] + bias[nt * 4 + r]) * a.alpha;
+            store8(Y + (long)bq * a.bsy + (long)t * a.ldy + ch0, v);
+        }
+    }
+}
+
 }  // namespace
 
 // internal entry used by stzs_conv1d for STZS_CONV_W_LANE16 weights
@@ -357,6 +518,22 @@ __attribute__((visibility("hidden"))) int stzs_mrf_conv_launch(const stzs_conv_a
     if (!k) return STZS_ESHAPE;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+// internal entry used by stzs_conv1d for STZS_CONV_W_NARROW32 weights
+__attribute__((visibility("hidden"))) int stzs_narrow_conv_launch(const stzs_conv_args& a, hipStream_t s) {
+    const int rows_in = NBT + (a.ks - 1) * a.dil;
+    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co > 32 || a.co_pad != 128 || rows_in > 16 * 2 * NSB ||
+        a.in_dtype != STZS_BF16 || a.out_dtype != STZS_F32 || a.ups || a.gate || a.res || a.acc_in ||
+        a.pro_mode != STZS_PRO_NONE || (a.pro_act != STZS_ACT_LEAKY && a.pro_act != STZS_ACT_NONE) ||
+        a.epi_act != STZS_ACT_NONE || a.stat_part || a.ldy % 8 || a.bsy % 8 || a.ldy < ((a.Co + 7) / 8) * 8)
+        return STZS_ESHAPE;
+    const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + NSL * NSLOT_B;
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + NBT - 1) / NBT));
+    (void)hipFuncSetAttribute((const void*)narrow_conv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(narrow_conv, grid, dim3(NTH), lds, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

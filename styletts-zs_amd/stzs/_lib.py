@@ -17,6 +17,7 @@ ACT_NONE, ACT_LEAKY, ACT_SNAKE, ACT_GELU, ACT_SILU = 0, 1, 2, 3, 4
 PRO_NONE, PRO_ADAIN = 0, 1
 CONV_STAT_ROWS = 64  # include/stzs.h STZS_CONV_STAT_ROWS
 CONV_W_LANE16 = 16  # include/stzs.h STZS_CONV_W_LANE16
+CONV_W_NARROW32 = 32  # include/stzs.h STZS_CONV_W_NARROW32
 
 vp = C.c_void_p
 i64 = C.c_int64

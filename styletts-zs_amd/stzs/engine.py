@@ -184,7 +184,9 @@ class StyleTTSZS:
                 and cscale == 1.0 and x.t.dtype == torch.bfloat16 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
         if getattr(cw, "lane16", False):
-            flags |= L.CONV_W_LANE16  # persistent MRF kernel (csrc/mrf.hip)
+            flags |= L.CONV_W_LANE16  # MRF-family kernel (csrc/mrf.hip)
+        if getattr(cw, "narrow32", False):
+            flags |= L.CONV_W_NARROW32  # narrow conv (csrc/mrf.hip)
         a.flags = flags
         st = None
         if stats_key is not None:
@@ -609,7 +611,8 @@ class StyleTTSZS:
                 host = torch.as_tensor(np.asarray(seeds, dtype=np.uint32).view(np.int32).copy())
                 sd = self._consts[skey] = host.to(self.device)
         pref = self.buf("gen.pref", (B, nh, T80), torch.float32)
-        har = self.act("gen.har", B, Tf, S.har_ch)
+        # row pitch = the noise convs' padded K (32): the 1x1 noise conv then takes the LDS-DMA GEMM path
+        har = Act(self.buf("gen.har", (B, Tf, _rup(S.har_ch, 32)), zero=True), 0, S.har_ch)
         a = L.SourceArgs()
         a.f0, a.seeds, a.merge_w, a.prefix, a.har = F0.data_ptr(), sd.data_ptr(), W.t(W.src_merge).data_ptr(), \
             pref.data_ptr(), har.ptr

@@ -42,6 +42,7 @@ class ConvW:
     cic: int
     ups: int = 0
     lane16: bool = False  # packed with the MRF kernel's channel permutation (STZS_CONV_W_LANE16)
+    narrow32: bool = False  # [NK][32][32] narrow packing (STZS_CONV_W_NARROW32)
 
 
 class Arena:
@@ -111,7 +112,22 @@ def lane16_perm() -> torch.Tensor:
     return (rr & 64) + ((rr >> 2) & 3) * 16 + ((rr >> 4) & 3) * 4 + (rr & 3)
 
 
-def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False) -> ConvW:
+def narrow32_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
+    """[ks, 32, ci_pad] -> [NK, 32, 32] K-steps for the narrow conv (csrc/mrf.hip narrow_conv): packed row
+    rr = nt*16 + g*4 + r holds output channel g*8 + nt*4 + r; 16-B chunks XOR-swizzled as kstep_stream."""
+    ks, _, ci_pad = wp.shape
+    rr = torch.arange(32)
+    perm = ((rr >> 2) & 3) * 8 + ((rr >> 4) & 1) * 4 + (rr & 3)
+    wp = wp[:, perm]
+    nchunk, kpc = ci_pad // cic, cic // 32
+    t = wp.view(ks, 32, nchunk, kpc, 4, 8).permute(2, 0, 3, 1, 4, 5)  # cc, tap, kq, row, c, 8
+    g = torch.tensor(_GSWZ)[(rr >> 2) & 3]
+    src_c = torch.arange(4)[None, :] ^ g[:, None]
+    t = t[:, :, :, rr[:, None], src_c, :]
+    return t.reshape(nchunk * ks * kpc, 32, 32).contiguous()
+
+
+def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False) -> ConvW:
     """w: Conv1d [Co, Ci, k] / Linear [Co, Ci] / ConvTranspose1d [Ci, Co, 2*ups] (ups > 0).
     lane16: the MRF kernel's layout (Ci % 128 == 0, Co % 16 == 0, plain conv)."""
     if ups:
@@ -134,6 +150,11 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False) -> ConvW:
     co_pad = _rup(ncol, 128)
     wp = torch.zeros(ks, co_pad, ci_pad)
     wp[:, :ncol, :Ci] = wk
+    if narrow32:
+        assert not ups and cic == 128 and Co <= 32, (name, Ci, Co)
+        wn = A.add(name + ".wpk", narrow32_stream(wp[:, :32], cic).to(torch.bfloat16))
+        bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
+        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True)
     if lane16:
         assert not ups and cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
@@ -305,7 +326,9 @@ class PackedModel:
                     dec_norms += [p + ".n1", p + ".n2"]
                 stage.append(res)
             self.rb.append(stage)
-        self.conv_post = pack_conv(A, "gen.conv_post", P["gen.conv_post.w"], P["gen.conv_post.b"])
+        wpost = P["gen.conv_post.w"]
+        self.conv_post = pack_conv(A, "gen.conv_post", wpost, P["gen.conv_post.b"],
+                                   narrow32=wpost.shape[1] > 64 and wpost.shape[0] <= 32)
         self.dec_norm = pack_norm_group(A, "dec.norms", P, dec_norms, S.style_ac)
         A.finalize(device, fill=fill)
         self.device = device

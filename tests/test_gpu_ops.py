@@ -18,10 +18,10 @@ def eng(gpu_device, tiny, tiny_params):
     return StyleTTSZS(tiny, tiny_params, device=gpu_device)
 
 
-def _pack(w, b, ups=0, lane16=False):
+def _pack(w, b, ups=0, lane16=False, narrow32=False):
     from stzs.weights import Arena, pack_conv
     A = Arena()
-    cw = pack_conv(A, "t", w, b, ups=ups, lane16=lane16)
+    cw = pack_conv(A, "t", w, b, ups=ups, lane16=lane16, narrow32=narrow32)
     A.finalize("cuda:0")
     cw.w = A[cw.w]
     cw.b = A[cw.b] if cw.b is not None else None
@@ -242,6 +242,26 @@ def test_mrf_persistent_conv(eng, case):
         mr, vr = y.mean(1), y.var(1, unbiased=False)
         assert float(((m.cpu().double() - mr).abs() / (mr.abs() + vr.sqrt())).max()) < 1e-5
         assert max_rel(r.cpu(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
+
+
+@pytest.mark.parametrize("B,T,Ci,Co,k", [(2, 3001, 128, 22, 7), (1, 300, 256, 32, 3), (3, 257, 128, 8, 7)])
+def test_narrow_conv(eng, B, T, Ci, Co, k):
+    """narrow conv (conv_post form: LeakyReLU(0.01) prologue, Co <= 32, fp32 out, csrc/mrf.hip
+    narrow_conv) vs the fp32 reference; tolerance 2e-3 of max|ref| (fp32 output, bf16 operands)."""
+    g = torch.Generator().manual_seed(T + Co)
+    pad = (k - 1) // 2
+    x = bf(torch.randn(B, T, Ci, generator=g))
+    w = torch.randn(Co, Ci, k, generator=g) / math.sqrt(Ci * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    ref = conv_ref(x, w, b, pad=pad, pro_act="leaky", slope=0.01)
+    cw, _A = _pack(w, b, narrow32=True)
+    from stzs import _lib as L
+    yd = _act(torch.zeros(B, T, (Co + 7) // 8 * 8, device="cuda:0"), Co)
+    eng.conv(cw, _act(x.to(torch.bfloat16).cuda()), yd, pad=pad, pro_act=L.ACT_LEAKY, pro_slope=0.01)
+    got = yd.t[:, :, :Co].cpu()
+    e = max_rel(got, ref)
+    print(B, T, Ci, Co, k, e)
+    assert e < 2e-3
 
 
 def test_row_layernorm(eng):
