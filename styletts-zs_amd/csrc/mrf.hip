@@ -227,15 +227,32 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
     }
     // The final K-step needs no wait, barrier, fill or prefetch: its fragments are in registers.  The
     // epilogue's residual / accumulate loads go out first so their latency hides under its MFMAs.
+    // Output row of GEMM row q: t = q, or for the polyphase ConvTranspose (ups > 0) column n = phase p *
+    // Co + channel (a 16-channel group never straddles phases, Co % 16 == 0): t = q*ups + p - ups_pad,
+    // valid in [0, T_final), shifted by refl (ReflectionPad(1,0)).
     const int gq = lane >> 4, n = lane & 15;
     const int co0 = blockIdx.y * BCO + wc * 64 + gq * 16;
-    const bool col_ok = co0 < a.Co;
-    const int coc = col_ok ? co0 : 0;
+    const int ph = a.ups > 0 ? co0 / a.Co : 0;
+    const bool col_ok = a.ups > 0 ? co0 < a.ups * a.Co : co0 < a.Co;
+    const int cof = col_ok ? co0 - ph * a.Co : 0;  // channel of this lane group's first value
+    const int t_hi = a.ups > 0 ? a.T_final + a.refl - 1 : a.T_out - 1;
+    auto orow = [&](int mt, bool& ok) {
+        const int q = t0 + wt * 64 + mt * 16 + n;
+        if (a.ups > 0) {
+            const int t = q * a.ups + ph - a.ups_pad;
+            ok = col_ok && q < a.T_out && t >= 0 && t < a.T_final;
+            return t + a.refl;
+        }
+        ok = col_ok && q < a.T_out;
+        return q;
+    };
+    const int coc = cof;
     uint4 rr[4][2], aa[4][2];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-        const int t = t0 + wt * 64 + mt * 16 + n;
-        const int tc = t < a.T_out ? t : a.T_out - 1;
+        bool okm;
+        const int t = orow(mt, okm);
+        const int tc = t < 0 ? 0 : (t > t_hi ? t_hi : t);
         if constexpr (HR) {  // (row t / res_tdiv: the nearest-x2 shortcut of an upsampling block)
             const bf16_t* p = reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr + (long)(tc / a.res_tdiv) * a.ldr + coc;
             rr[mt][0] = *reinterpret_cast<const uint4*>(p);
@@ -264,7 +281,8 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
     {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
-            const int t = t0 + wt * 64 + mt * 16 + n;
+            bool ok;
+            const int t = orow(mt, ok);
             float v[16];
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
@@ -287,11 +305,29 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
                 for (int i = 0; i < 16; ++i) v[i] = fmaf(a.beta, f[i], v[i]);
             }
             const uint4 o0 = pack8(v), o1 = pack8(v + 8);
-            const bool ok = col_ok && t < a.T_out;
             if (ok) {
-                bf16_t* p = Y + (long)bq * a.bsy + (long)t * a.ldy + co0;
+                bf16_t* p = Y + (long)bq * a.bsy + (long)t * a.ldy + cof;
                 *reinterpret_cast<uint4*>(p) = o0;
                 *reinterpret_cast<uint4*>(p + 8) = o1;
+            }
+            if (a.refl && ok && t == 2) {  // ReflectionPad(1,0): row 0 mirrors source row 1 (+ row 0's residual)
+                float w[16];
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) w[nt * 4 + r] = acc[nt][mt][r] + bias[nt * 4 + r];
+                if constexpr (HR) {
+                    float f[16];
+                    load8(reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr + coc, f);
+                    load8(reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr + coc + 8, f + 8);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] += f[i];
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) w[i] *= a.alpha;
+                bf16_t* p = Y + (long)bq * a.bsy + cof;
+                *reinterpret_cast<uint4*>(p) = pack8(w);
+                *reinterpret_cast<uint4*>(p + 8) = pack8(w + 8);
             }
             if (stat && ok) {  // statistics of the stored (bf16-rounded) values
                 float f[16];
@@ -492,7 +528,8 @@ __global__ __launch_bounds__(NTH, 2) void narrow_conv(const stzs_conv_args a) {
 __attribute__((visibility("hidden"))) int stzs_mrf_conv_launch(const stzs_conv_args& a, hipStream_t s) {
     const int rows_in = BT + (a.ks - 1) * a.dil;
     if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 16 || rows_in > 16 * SB ||
-        a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.ups || a.gate || a.epi_act != STZS_ACT_NONE ||
+        a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.gate || a.epi_act != STZS_ACT_NONE ||
+        (a.ups && (a.acc_in || a.stat_part || a.res_tdiv != 1)) ||
         a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8)) || (a.acc_in && (a.lda % 8 || a.bsa % 8)))
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;

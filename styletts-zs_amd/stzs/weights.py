@@ -156,7 +156,7 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False) ->
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
         return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True)
     if lane16:
-        assert not ups and cic == 128 and Co % 16 == 0, (name, Ci, Co)
+        assert cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, perm].reshape(ks, co_pad, ci_pad)
     wn = A.add(name + ".wpk", kstep_stream(wp, cic).to(torch.bfloat16))
@@ -311,7 +311,9 @@ class PackedModel:
         self.noise_conv, self.ups, self.rb = [], [], []
         for i, (r, k) in enumerate(zip(S.up_rates, S.up_kernels)):
             self.noise_conv.append(pack_conv(A, f"gen.noise_conv{i}", P[f"gen.noise_conv{i}.w"], P[f"gen.noise_conv{i}.b"]))
-            self.ups.append(pack_conv(A, f"gen.ups{i}", P[f"gen.ups{i}.w"], P[f"gen.ups{i}.b"], ups=r))
+            wu = P[f"gen.ups{i}.w"]  # ConvTranspose1d [Ci, Co, 2r]
+            self.ups.append(pack_conv(A, f"gen.ups{i}", wu, P[f"gen.ups{i}.b"], ups=r,
+                                      lane16=wu.shape[0] > 64 and wu.shape[1] % 16 == 0))
             stage = []
             for j, kr in enumerate(S.rb_kernels):
                 res = []

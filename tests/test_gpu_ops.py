@@ -119,8 +119,10 @@ def test_linear_flat(eng, dt_in, dt_out):
     assert e < (1e-2 if dt_out == torch.bfloat16 else 2e-3)
 
 
-@pytest.mark.parametrize("Ci,Co,s,refl", [(64, 32, 10, 0), (32, 16, 6, 1), (512, 256, 10, 0), (256, 128, 6, 1)])
-def test_convtranspose_polyphase(eng, Ci, Co, s, refl):
+@pytest.mark.parametrize("Ci,Co,s,refl,l16", [(64, 32, 10, 0, False), (32, 16, 6, 1, False), (512, 256, 10, 0, False),
+                                               (256, 128, 6, 1, False), (512, 256, 10, 0, True), (256, 128, 6, 1, True),
+                                               (200, 48, 4, 1, True)])
+def test_convtranspose_polyphase(eng, Ci, Co, s, refl, l16):
     """polyphase ConvTranspose1d(k=2s) + LeakyReLU(0.1) prologue + ReflectionPad(1,0) + residual."""
     g = torch.Generator().manual_seed(Ci + s)
     B, T = 2, 40
@@ -131,7 +133,7 @@ def test_convtranspose_polyphase(eng, Ci, Co, s, refl):
     Tn = T * s + refl
     res = bf(torch.randn(B, Tn, Co, generator=g))
     ref = convT_ref(x, w, b, stride=s, pad=pad, refl=refl, pro_act="leaky", slope=0.1, res=res)
-    cw, _A = _pack(w, b, ups=s)
+    cw, _A = _pack(w, b, ups=s, lane16=l16)  # l16: the MRF-family kernel's polyphase epilogue
     from stzs import _lib as L
     yd = _act(torch.zeros(B, Tn, Co, dtype=torch.bfloat16, device="cuda:0"))
     eng.conv(cw, _act(x.to(torch.bfloat16).cuda()), yd, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=pad,
