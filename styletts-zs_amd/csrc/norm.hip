@@ -71,7 +71,18 @@ __global__ __launch_bounds__(256) void chan_stats_final(const stzs_stats_args a,
     double s = 0.0, q = 0.0;
     if (c < a.C) {
         const float2* P = reinterpret_cast<const float2*>(a.partial) + (long)b * nchunk * a.C + c;
-        for (int k = g; k < nchunk; k += 8) {
+        int k = g;
+        for (; k + 24 < nchunk; k += 32) {  // four independent loads in flight per iteration
+            float2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = P[(long)(k + 8 * u) * a.C];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s += (double)v[u].x;
+                q += (double)v[u].y;
+            }
+        }
+        for (; k < nchunk; k += 8) {
             const float2 v = P[(long)k * a.C];
             s += (double)v.x;
             q += (double)v.y;
@@ -130,17 +141,20 @@ __global__ __launch_bounds__(256) void row_ln(const stzs_rowln_args a) {
     const float rstd = 1.f / sqrtf(wave_sum(q) / a.C + a.eps);
     const long grp = r / a.gdiv;
     TO* Y = reinterpret_cast<TO*>(a.y) + r * a.ldy;
+    // modulation rows as 32-B vectors (gs, bs and the bases are multiples of 8 floats: checked on the host)
+    const float* Gr = a.G ? a.G + grp * a.gs : nullptr;
+    const float* Br = a.Bt ? a.Bt + grp * a.bs : nullptr;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
         const int vi = lane + i * 64;
         if (vi < nv) {
-            float o[8];
+            float g[8], bt[8], o[8];
+            if (Gr) load8(Gr + vi * 8, g);
+            if (Br) load8(Br + vi * 8, bt);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int c = vi * 8 + j;
-                float g = a.gadd + (a.G ? a.G[grp * a.gs + c] : 0.f);
-                float bt = a.Bt ? a.Bt[grp * a.bs + c] : 0.f;
-                o[j] = act_apply(a.act, (v[i][j] - mu) * rstd * g + bt, a.slope, 1.f);
+                const float gg = a.gadd + (Gr ? g[j] : 0.f);
+                o[j] = act_apply(a.act, (v[i][j] - mu) * rstd * gg + (Br ? bt[j] : 0.f), a.slope, 1.f);
             }
             store8(Y + vi * 8, o);
         }
@@ -187,6 +201,8 @@ extern "C" int stzs_row_layernorm(const stzs_rowln_args* a, void* stream) {
     if (!a || !a->x || !a->y) return STZS_EINVAL;
     if (a->R <= 0 || a->C <= 0 || a->C % 8 || a->C > 2048 || a->ldx % 8 || a->ldy % 8 || a->gdiv <= 0)
         return STZS_ESHAPE;
+    if ((a->G && (a->gs % 8 || !stzs_aligned(a->G, 32))) || (a->Bt && (a->bs % 8 || !stzs_aligned(a->Bt, 32))))
+        return STZS_ESHAPE;  // modulation rows are read as 32-B vectors
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     dim3 g((a->R + 3) / 4);
     if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16)
