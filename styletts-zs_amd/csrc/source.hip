@@ -6,7 +6,10 @@
 // in-frame phase is then prefix + (j+1) * f/sr in fp32 (|arg| < 60 cycles, so < 4e-6 cycles of
 // error).  Every fp32/fp64 op that must agree bit-for-bit with the oracle uses explicit _rn
 // intrinsics (no FMA contraction).  Samples are generated once per workgroup into LDS
-// (reflect-padded at the ends, centre=True) and consumed by all frames that overlap them.
+// (reflect-padded at the ends, centre=True) and consumed by all frames that overlap them; the
+// per-frame phase increments and prefixes of the few frames a workgroup spans sit in LDS.  Sine and
+// the noise's Box-Muller use the hardware transcendentals (v_sin / v_cos in revolutions, v_log):
+// the counter stream is the oracle's, the transform within ~1e-6 of its fp64 one.
 #include "common.hpp"
 
 namespace {
@@ -29,6 +32,15 @@ STZS_DEV float counter_normal(uint32_t key, uint32_t idx) {
     const double u2 = (double)(b >> 8) * (1.0 / 16777216.0);
     return (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
 }
+// the same counter pair as counter_normal, Box-Muller in fp32 hardware intrinsics (v_log_f32,
+// v_sqrt_f32, v_cos_f32 in revolutions): within ~2e-6 of the fp64 transform (tests/test_gpu_ops.py)
+STZS_DEV float counter_normal_fast(uint32_t key, uint32_t idx) {
+    const uint32_t a = hash32(key ^ hash32(idx * 2u));
+    const uint32_t b = hash32(key ^ hash32(idx * 2u + 1u));
+    const float u1 = ((float)(a >> 8) + 1.f) * (1.f / 16777216.f);
+    const float u2 = (float)(b >> 8) * (1.f / 16777216.f);
+    return __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1)) * __builtin_amdgcn_cosf(u2);
+}
 STZS_DEV float initial_phase(uint32_t key) {
     return (float)((double)(hash32(key ^ 0xA5A5A5A5u) >> 8) * (1.0 / 16777216.0));
 }
@@ -49,6 +61,7 @@ __global__ void phase_prefix_kernel(const stzs_source_args a) {
 }
 
 constexpr int FB = 256;  // STFT frames per workgroup
+constexpr int KW = 8;    // 80-fps frames spanned by one workgroup's samples (checked on the host)
 
 __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args a) {
     extern __shared__ float sm[];
@@ -60,6 +73,9 @@ __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args
     float* win = tws + nfft;          // nfft hann
     uint32_t* keys = reinterpret_cast<uint32_t*>(win + nfft);  // nh
     float* ph0 = reinterpret_cast<float*>(keys + a.nh);        // nh
+    float* finc = ph0 + a.nh;                                   // [KW][nh] per-frame phase increment
+    float* fpre = finc + KW * a.nh;                             // [KW][nh] per-frame phase prefix + ph0
+    float* mw = fpre + KW * a.nh;                               // nh merge weights
     const int b = blockIdx.y, f0i = blockIdx.x * FB, tid = threadIdx.x;
     const int N = a.T80 * a.hop;
     const int Tf = N / hs + 1;
@@ -73,11 +89,21 @@ __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args
         const uint32_t key = stream_key(a.seeds[b], (uint32_t)tid);
         keys[tid] = key;
         ph0[tid] = tid == 0 ? 0.f : initial_phase(key);
+        mw[tid] = a.merge_w[tid];
     }
     __syncthreads();
     const float* F = a.f0 + (long)b * a.ldf;
     const float* P = a.prefix + (long)b * a.nh * a.T80;
-    const float amp = a.sine_amp, amp3 = __fdiv_rn(a.sine_amp, 3.0f), two_pi = 6.2831853071795864f;
+    // the <= KW 80-fps frames this workgroup's samples fall in (reflection maps into them as well)
+    const int nlo = max(f0i * hs - nfft / 2, 0), nhi = min(f0i * hs - nfft / 2 + NS - 1, N - 1);
+    const int k_lo = nlo / a.hop, nk = nhi / a.hop - k_lo + 1;
+    for (int e = tid; e < nk * a.nh; e += 256) {
+        const int kk = e / a.nh, h = e - kk * a.nh, k = k_lo + kk;
+        finc[kk * a.nh + h] = __fdiv_rn(__fmul_rn(F[k], (float)(h + 1)), a.sr);
+        fpre[kk * a.nh + h] = __fadd_rn(P[(long)h * a.T80 + k], ph0[h]);
+    }
+    __syncthreads();
+    const float amp = a.sine_amp, amp3 = __fdiv_rn(a.sine_amp, 3.0f);
     const float wb = a.merge_w[a.nh];
     for (int p = tid; p < NS; p += 256) {
         int n = (f0i * hs + p) - nfft / 2;  // centre=True: padded index -> signal index
@@ -85,24 +111,23 @@ __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args
         if (n >= N) n = 2 * (N - 1) - n;
         float v = 0.f;
         if (n >= 0 && n < N) {
-            const int k = n / a.hop;
+            const int k = n / a.hop, kk = k - k_lo;
             const float jj = (float)(n - k * a.hop + 1);
-            const float f0v = F[k];
-            const bool voiced = f0v > a.voiced_thr;
+            const bool voiced = F[k] > a.voiced_thr;
             const float uv = voiced ? 1.f : 0.f;
             const float namp = voiced ? a.noise_std : amp3;
+            const float* fi = finc + kk * a.nh;
+            const float* fp = fpre + kk * a.nh;
             float acc = 0.f;
             for (int h = 0; h < a.nh; ++h) {
-                const float inc = __fdiv_rn(__fmul_rn(f0v, (float)(h + 1)), a.sr);
-                float t = __fadd_rn(P[(long)h * a.T80 + k], ph0[h]);
-                t = __fadd_rn(t, __fmul_rn(jj, inc));
-                const float th = __fsub_rn(t, floorf(t));
-                const float sine = __fmul_rn(amp, sinf(__fmul_rn(two_pi, th)));
-                const float z = counter_normal(keys[h], (uint32_t)n);
-                const float sw = __fadd_rn(__fmul_rn(sine, uv), __fmul_rn(namp, z));
-                acc = __fadd_rn(acc, __fmul_rn(a.merge_w[h], sw));
+                const float t = __fadd_rn(fp[h], __fmul_rn(jj, fi[h]));
+                const float th = __fsub_rn(t, floorf(t));  // wrapped phase, cycles
+                const float sine = amp * __builtin_amdgcn_sinf(th);
+                const float z = counter_normal_fast(keys[h], (uint32_t)n);
+                acc = fmaf(mw[h], fmaf(sine, uv, namp * z), acc);
             }
-            v = tanhf(__fadd_rn(acc, wb));
+            const float xx = acc + wb;
+            v = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * xx));  // tanh
         }
         sbuf[p] = v;
     }
@@ -140,7 +165,8 @@ extern "C" int stzs_harmonic_source(const stzs_source_args* a, void* stream) {
     const int N = a->T80 * a->hop;
     const int Tf = N / a->hop_s + 1;
     const int NS = a->hop_s * (FB - 1) + a->n_fft;
-    const size_t lds = (size_t)(NS + 3 * a->n_fft) * 4 + (size_t)a->nh * 8;
+    if (NS / a->hop + 2 > KW) return STZS_ESHAPE;
+    const size_t lds = (size_t)(NS + 3 * a->n_fft) * 4 + (size_t)a->nh * (8 + 4 + 2 * KW * 4);
     hipLaunchKernelGGL(source_stft_kernel, dim3((Tf + FB - 1) / FB, a->B), dim3(256), lds, s, *a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
