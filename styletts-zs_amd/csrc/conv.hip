@@ -89,7 +89,7 @@ STZS_DEV float epi_act(float x, float slope) {
     else return x;
 }
 
-template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA, int EACT>
+template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA, int EACT, int BTM>
 STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_bias, const float* c_gate, int bq,
                        int t0, long row0, int tid) {
     const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
@@ -142,7 +142,7 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
         for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
     };
     static_assert(BT * (BCO / 8) == 2 * EB * NTHR, "two epilogue passes = two 64-row halves");
-    for (int v0 = 0; v0 < BT * (BCO / 8); v0 += EB * NTHR) {
+    for (int v0 = 0; v0 < BTM * (BCO / 8); v0 += EB * NTHR) {
         long pb[EB], pt[EB];
         bool pv[EB];
         float rr[EB][8], ai[EB][8];
@@ -279,19 +279,19 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
     }
 }
 
-template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA>
+template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA, int BTM>
 STZS_DEV void epilogue_act(const stzs_conv_args& a, const float* ep, const float* c_bias, const float* c_gate, int bq,
                            int t0, long row0, int tid) {
     switch (a.epi_act) {
-        case STZS_ACT_GELU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_GELU>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
-        case STZS_ACT_SILU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_SILU>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
-        case STZS_ACT_LEAKY: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_LEAKY>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
-        default: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_NONE>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
+        case STZS_ACT_GELU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_GELU, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
+        case STZS_ACT_SILU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_SILU, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
+        case STZS_ACT_LEAKY: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_LEAKY, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
+        default: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_NONE, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
     }
 }
 
-template <typename TOut, bool FLAT>
-STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[4][4], unsigned char* smem, int bq, int t0, long row0);
+template <typename TOut, bool FLAT, int BTM = BT>
+STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0);
 
 // 8-wide vector epilogue legal (every output / residual / accumulate row 16-B aligned)
 __host__ __device__ inline bool epi_vec(const stzs_conv_args& a) {
@@ -479,19 +479,19 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
 }
 
 // Accumulators -> LDS (fp32, padded rows) -> vectorised fused epilogue.
-template <typename TOut, bool FLAT>
-STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[4][4], unsigned char* smem, int bq, int t0, long row0) {
+template <typename TOut, bool FLAT, int BTM>
+STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
     __syncthreads();
     float* ep = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < BTM / 32; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                ep[(wt * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
+                ep[(wt * (BTM / 2) + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
     if (a.flags & 4) return;
     float* c_bias = ep + BT * EP_PITCH;       // [BCO] bias, [BCO] gate (conv mode: one utterance)
     float* c_gate = c_bias + BCO;
@@ -503,12 +503,12 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[4][4], unsigned char*
     }
     __syncthreads();
     if (epi_vec(a)) {
-        if (a.res && a.acc_in) epilogue_act<TOut, FLAT, true, true, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else if (a.res) epilogue_act<TOut, FLAT, true, true, false>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else if (a.acc_in) epilogue_act<TOut, FLAT, true, false, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else epilogue_act<TOut, FLAT, true, false, false>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        if (a.res && a.acc_in) epilogue_act<TOut, FLAT, true, true, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else if (a.res) epilogue_act<TOut, FLAT, true, true, false, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else if (a.acc_in) epilogue_act<TOut, FLAT, true, false, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        else epilogue_act<TOut, FLAT, true, false, false, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
     } else {
-        epilogue_act<TOut, FLAT, false, true, true>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        epilogue_act<TOut, FLAT, false, true, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
     }
 }
 
@@ -524,21 +524,25 @@ STZS_DEV void glds16(const void* src, void* dst) {
 // Per K-step: counted vmcnt + one s_barrier, then the NEXT K-step's fragments are read between the
 // current K-step's 16 MFMAs (as csrc/mrf.hip); the body is branch-free (a fill past the end re-copies
 // the last K-step into a retired slot) and the last K-step is peeled.
-constexpr int GSLOT = 2 * SLOT_BYTES;  // A + B of one K-step
-template <typename TOut>
+template <int BTM>
+constexpr int gslot() { return BTM * 64 + SLOT_BYTES; }  // A (BTM rows x 32 k) + B of one K-step
+template <typename TOut, int BTM>
 __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
+    constexpr int MT = BTM / 32;           // 16-row tiles per wave (2 x 2 waves)
+    constexpr int GS = gslot<BTM>();
+    constexpr int AP = BTM / 64;           // A pieces (1 KB) per wave per K-step
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
-    const long row0 = (long)blockIdx.x * BT;
+    const long row0 = (long)blockIdx.x * BTM;
     const long nR = (long)a.B * a.T_in;
     const int NK = a.ci_pad >> 5;
     const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
     const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x);
-    long asrc[2];
+    long asrc[AP];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int o = wave * 2048 + i * 1024 + lane * 16;
+    for (int i = 0; i < AP; ++i) {
+        const int o = wave * AP * 1024 + i * 1024 + lane * 16;
         const int r = o >> 6, p = (o >> 4) & 3;
         long R = row0 + r;
         R = R < nR ? R : nR - 1;
@@ -548,59 +552,60 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     auto fill = [&](int k) {
         const int kc = k < NK ? k : NK - 1;
         const bf16_t* src = Wt + (long)kc * (BCO * 32) + wave * 1024 + lane * 8;
-        unsigned char* da = smem + (k & 3) * GSLOT + wave * 2048;
-        unsigned char* db = da + SLOT_BYTES;
+        unsigned char* da = smem + (k & 3) * GS + wave * AP * 1024;
+        unsigned char* db = smem + (k & 3) * GS + BTM * 64 + wave * 2048;
         glds16(src, db);
         glds16(src + 512, db + 1024);
-        glds16(X + asrc[0] + kc * 32, da);
-        glds16(X + asrc[1] + kc * 32, da + 1024);
+#pragma unroll
+        for (int i = 0; i < AP; ++i) glds16(X + asrc[i] + kc * 32, da + i * 1024);
     };
     int aoff0, boff0;
     {
-        const int ra = wt * 64 + (lane & 15);
+        const int ra = wt * (BTM / 2) + (lane & 15);
         aoff0 = ra * 64 + (((lane >> 4) ^ gswz(ra)) << 4);
         const int rb = wc * 64 + (lane & 15);
-        boff0 = SLOT_BYTES + rb * 64 + (((lane >> 4) ^ gswz(rb)) << 4);
+        boff0 = BTM * 64 + rb * 64 + (((lane >> 4) ^ gswz(rb)) << 4);
     }
-    f32x4 acc[4][4];
+    f32x4 acc[MT][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
-    auto rd = [&](bf16x8 (&fa)[4], bf16x8 (&fb)[4], int k) {
-        const unsigned char* sl = smem + (k & 3) * GSLOT;
+    bf16x8 fa0[MT], fb0[4], fa1[MT], fb1[4];
+    auto rd = [&](bf16x8 (&fa)[MT], bf16x8 (&fb)[4], int k) {
+        const unsigned char* sl = smem + (k & 3) * GS;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(sl + aoff0 + i * 1024);
+        for (int i = 0; i < MT; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(sl + aoff0 + i * 1024);
 #pragma unroll
         for (int i = 0; i < 4; ++i) fb[i] = *reinterpret_cast<const bf16x8*>(sl + boff0 + i * 1024);
     };
-    auto mma = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[4]) {
+    auto mma = [&](const bf16x8 (&fa)[MT], const bf16x8 (&fb)[4]) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
     };
+    constexpr int PER_FILL = 2 + AP;  // LDS-DMA instructions per wave per K-step
     fill(0);
     fill(1);
-    __builtin_amdgcn_s_waitcnt(0x0F70 | 4);  // K-step 0 landed (K-step 1 may be in flight)
+    __builtin_amdgcn_s_waitcnt(0x0F70 | PER_FILL);  // K-step 0 landed (K-step 1 may be in flight)
     __builtin_amdgcn_s_barrier();
     fill(2);
     rd(fa0, fb0, 0);
 #define STZS_GEMM_STEP(FA, FB, NA, NB)                                          \
     {                                                                           \
-        __builtin_amdgcn_s_waitcnt(0x0F70 | 4);                                 \
+        __builtin_amdgcn_s_waitcnt(0x0F70 | PER_FILL);                          \
         __builtin_amdgcn_s_barrier();                                           \
         fill(k + 3);                                                            \
         __builtin_amdgcn_sched_barrier(0);                                      \
         rd(NA, NB, k + 1);                                                      \
         mma(FA, FB);                                                            \
-        _Pragma("unroll") for (int ii = 0; ii < 8; ++ii) {                      \
+        _Pragma("unroll") for (int ii = 0; ii < MT + 4; ++ii) {                 \
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  \
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                  \
         }                                                                       \
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                      \
+        __builtin_amdgcn_sched_group_barrier(0x008, MT * 4 - MT - 4, 0);        \
         __builtin_amdgcn_sched_barrier(0);                                      \
         ++k;                                                                    \
     }
@@ -617,7 +622,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         mma(fa0, fb0);
     }
 #undef STZS_GEMM_STEP
-    finish<TOut, true>(a, acc, smem, 0, 0, row0);
+    finish<TOut, true, BTM>(a, acc, smem, 0, 0, row0);
 }
 
 size_t lds_bytes(int rows_in, int cic) {
@@ -639,9 +644,20 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     if (flat && a.stat_part) return STZS_EINVAL;  // fused statistics: per-utterance tiles only
     void (*k)(stzs_conv_args);
     if (flat && sizeof(TIn) == 2 && (a.flags & STZS_CONV_A_DMA) && a.pro_cscale == 1.f) {
+        // 64-row tiles when 128-row tiles would leave the GPU under-filled (< 2 workgroups per CU)
+        static int n_cu = 0;
+        if (n_cu == 0) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+                n_cu = 256;
+        }
+        const bool small = (long)grid.x * grid.y < 2L * n_cu;
         size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
-        lg = lg > 4 * (size_t)GSLOT ? lg : 4 * (size_t)GSLOT;
-        auto kg = gemm_glds<TOut>;
+        const size_t lr = 4 * (size_t)(small ? gslot<64>() : gslot<128>());
+        lg = lg > lr ? lg : lr;
+        auto kg = small ? gemm_glds<TOut, 64> : gemm_glds<TOut, 128>;
+        if (small) grid.x = (unsigned)(((long)a.B * a.T_out + 63) / 64);
         (void)hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);
         hipLaunchKernelGGL(kg, grid, dim3(NTHR), lg, s, a);
         STZS_LAUNCH_CHECK();
