@@ -81,9 +81,19 @@ STZS_DEV void waitcnt_vm(int n) {
 // Epilogue pass: each thread owns ONE 8-channel vector column (cv = tid & 15, so bias/gate sit in
 // registers) and walks rows 16 apart; EB vectors per batch, residual / accumulate loads issued
 // unconditionally from clamped addresses (all in flight) before any is consumed.
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7; one v_exp + one v_rcp instead of libm erff)
+STZS_DEV float fast_erf(float x) {
+    const float ax = fabsf(x);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
+    const float p = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
+                             0.254829592f);
+    const float y = 1.f - p * __expf(-ax * ax);
+    return copysignf(y, x);
+}
+
 template <int EACT>
 STZS_DEV float epi_act(float x, float slope) {
-    if constexpr (EACT == STZS_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    if constexpr (EACT == STZS_ACT_GELU) return 0.5f * x * (1.f + fast_erf(x * 0.70710678118654752f));
     else if constexpr (EACT == STZS_ACT_SILU) return x / (1.f + __expf(-x));
     else if constexpr (EACT == STZS_ACT_LEAKY) return x >= 0.f ? x : x * slope;
     else return x;
