@@ -18,6 +18,12 @@ STZS_DEV bf16_t f2bf(float f) {
     __bf16 h = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving on gfx950
     return __builtin_bit_cast(bf16_t, h);
 }
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+// two floats -> one packed bf16 pair (lo = a) in a single v_cvt_pk_bf16_f32
+STZS_DEV uint32_t pack2bf(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
 
 template <typename T> struct DT;
 template <> struct DT<float> {
@@ -56,7 +62,7 @@ STZS_DEV void unpack8(const uint4& u, float* v) {
 STZS_DEV uint4 pack8(const float* v) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = pack2bf(v[2 * i], v[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 STZS_DEV void store8(bf16_t* p, const float* v) { *reinterpret_cast<uint4*>(p) = pack8(v); }

@@ -159,8 +159,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
             c[j] = fg * c[j] + ig * fast_tanh(gg);
             hv[j] = og * fast_tanh(c[j]);
         }
-        const uint2 hb = make_uint2((uint32_t)f2bf(hv[0]) | ((uint32_t)f2bf(hv[1]) << 16),
-                                    (uint32_t)f2bf(hv[2]) | ((uint32_t)f2bf(hv[3]) << 16));
+        const uint2 hb = make_uint2(pack2bf(hv[0], hv[1]), pack2bf(hv[2], hv[3]));
         if (cvalid) {
             const __attribute__((ext_vector_type(2))) unsigned int hw = {hb.x, hb.y};
             __builtin_amdgcn_raw_buffer_store_b64(hw, xr, ((s & 1) * MROWS * H + crow * H + p * UNITS + cu0) * 2, 0, 16);

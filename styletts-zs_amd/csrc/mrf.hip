@@ -177,7 +177,7 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
                             y0 = y0 >= 0.f ? y0 : y0 * slope;
                             y1 = y1 >= 0.f ? y1 : y1 * slope;
                         }
-                        o[p] = okv[i] ? ((uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16)) : 0u;
+                        o[p] = okv[i] ? pack2bf(y0, y1) : 0u;
                     }
                     *reinterpret_cast<uint4*>(smem + r * P + cv * 16) = make_uint4(o[0], o[1], o[2], o[3]);
                 }
