@@ -56,7 +56,7 @@ def make_inputs(S, B, seed):
     return tok, ref, eps, dur
 
 
-def cpu_baseline(S, P, budget_s=12.0):
+def cpu_baseline(S, P, budget_s=15.0):
     from oracle import stzs_ref as R
     nthr = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(nthr)
@@ -66,7 +66,7 @@ def cpu_baseline(S, P, budget_s=12.0):
         R.synth(P, S, tok, ref, STEPS_THROUGHPUT, CFG, eps, dur, seeds=[0])
         n += 1
         el = time.perf_counter() - t0
-        if el > budget_s or n >= 8:
+        if el > budget_s or n >= 64:
             break
     return dict(value=n * TARGET_S / el, unit="audio-s/s", cores=nthr, kind="port",
                 sample=f"{n} x 1 utterance of the bench workload (5-s target, {STEPS_THROUGHPUT}-step CFG-{CFG:g}), "

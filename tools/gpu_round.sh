@@ -1,0 +1,12 @@
+#!/bin/bash
+# full GPU round trip (tag = $1): gpu parity tests, default bench (with CPU baseline), kernel-trace profile
+tag=${1:-x}
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/ -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t_$tag.log 2>&1
+rc=$?; echo TEST $rc; grep -E "passed|failed|FAILED|Error" gpurun_out/t_$tag.log | tail -8
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$tag.log 2>&1 || exit $?
+tail -1 gpurun_out/smoke_$tag.log
+timeout -k 10 500 python bench.py > gpurun_out/bench_$tag.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_$tag.log
+bash tools/prof.sh prof_$tag
