@@ -256,6 +256,26 @@ typedef struct stzs_istft_args {
 } stzs_istft_args;
 int stzs_istft(const stzs_istft_args* a, void* stream);
 
+/* streaming iSTFT (SURVEY §8(a) a14, configs[4] long-form): the frames of one chunk [f0, f0 + Fc)
+ * emit every output sample whose overlapping frames are all known; the `halo` (= ceil(n_fft/hop_s)
+ * - 1, 3 at 20/5) raw frame rows before the chunk are carried in a caller-owned tail
+ * [B][halo][ldt] f32 (ldt >= n_fft + 2): tail_in holds frames f0-halo .. f0-1 (unused at f0 = 0),
+ * tail_out receives frames f0+Fc-halo .. f0+Fc-1 (must not alias tail_in: ping-pong two buffers).
+ * The chunk writes samples n in [n0, n1) (stzs_istft_stream_span) to wav[b*bsw + n - n0]; the
+ * final chunk also emits the trailing samples up to (f0 + Fc - 1) * hop_s.  Concatenated chunks
+ * are bit-identical to stzs_istft over the whole utterance (same kernel, same summation order). */
+typedef struct stzs_istft_stream_args {
+    const float* post;     /* chunk frames: row j = frame f0 + j, [B, Fc, ldp] */
+    const float* tail_in;
+    float* tail_out;
+    float* wav;
+    int64_t ldp, bsp, bsw, ldt;
+    int32_t B, f0, Fc, final_chunk, n_fft, hop_s;
+} stzs_istft_stream_args;
+int stzs_istft_stream(const stzs_istft_stream_args* a, void* stream);
+/* -> halo (>= 0) or a negative error; [*n0, *n1) = output samples of the chunk */
+int stzs_istft_stream_span(int f0, int Fc, int final_chunk, int n_fft, int hop_s, int64_t* n0, int64_t* n1);
+
 /* ---- sampler glue ---- */
 /* c[r, j] = silu(pool[r, j] + temb[j]) -> bf16 */
 int stzs_dn_cond(const float* pool, const float* temb, void* c, int R, int D, void* stream);

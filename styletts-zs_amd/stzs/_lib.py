@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STZS_LIB", os.path.join(_HERE, "libstzs_hip.so"))
 
 F32, BF16, I32 = 0, 1, 2
+OK, EINVAL, ESHAPE, EDTYPE, EHIP = 0, -1, -2, -3, -4
 ACT_NONE, ACT_LEAKY, ACT_SNAKE, ACT_GELU, ACT_SILU = 0, 1, 2, 3, 4
 PRO_NONE, PRO_ADAIN = 0, 1
 CONV_STAT_ROWS = 64  # include/stzs.h STZS_CONV_STAT_ROWS
@@ -107,6 +108,12 @@ class IstftArgs(C.Structure):
                 ("B", i32), ("Tf", i32), ("n_fft", i32), ("hop_s", i32)]
 
 
+class IstftStreamArgs(C.Structure):
+    _fields_ = [("post", vp), ("tail_in", vp), ("tail_out", vp), ("wav", vp),
+                ("ldp", i64), ("bsp", i64), ("bsw", i64), ("ldt", i64),
+                ("B", i32), ("f0", i32), ("Fc", i32), ("final_chunk", i32), ("n_fft", i32), ("hop_s", i32)]
+
+
 class CopyArgs(C.Structure):
     _fields_ = [("x", vp), ("y", vp)] + [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy")] + \
                [(n, i32) for n in ("B", "R", "C", "in_dtype", "out_dtype", "pad_i")]
@@ -116,7 +123,8 @@ class CopyArgs(C.Structure):
 EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_chan_stats_workspace",
            "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
-           "stzs_harmonic_source", "stzs_istft", "stzs_dn_cond", "stzs_adaln_expand", "stzs_cfg_euler",
+           "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
+           "stzs_dn_cond", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed"]
 
 _lib = None
@@ -156,6 +164,8 @@ def load():
         "stzs_f0n_down": ([P(F0nArgs), vp], i32),
         "stzs_harmonic_source": ([P(SourceArgs), vp], i32),
         "stzs_istft": ([P(IstftArgs), vp], i32),
+        "stzs_istft_stream": ([P(IstftStreamArgs), vp], i32),
+        "stzs_istft_stream_span": ([i32, i32, i32, i32, i32, P(i64), P(i64)], i32),
         "stzs_dn_cond": ([vp, vp, vp, i32, i32, vp], i32),
         "stzs_adaln_expand": ([vp, vp, vp, i32, i32, i32, i32, C.c_uint32, vp], i32),
         "stzs_cfg_euler": ([vp, vp, i32, i32, i32, f32, f32, f32, vp], i32),

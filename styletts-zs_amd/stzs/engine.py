@@ -564,7 +564,7 @@ class StyleTTSZS:
         return out
 
     # ------------------------------------------------------------------ (c) decoder
-    def decode(self, pro: dict, codes: torch.Tensor, seeds) -> torch.Tensor:
+    def decode(self, pro: dict, codes: torch.Tensor, seeds, istft=True) -> torch.Tensor:
         S, W = self.spec, self.W
         enc_in, F0, Nn, T40 = pro["asr_buf"], pro["F0"], pro["N"], pro["T40"]
         B = enc_in.B
@@ -593,9 +593,9 @@ class StyleTTSZS:
             src = 1 - src
         gen_in = self.act("dec.gen_in", B, T80, S.dec_out)
         self.blk(W.dec_blk["dec.decode3"], Act(cats[src].t, 0, dcat), gen_in, ng, gbd, "dec.decode3")
-        return self.generator(gen_in, F0, seeds, gbd)
+        return self.generator(gen_in, F0, seeds, gbd, istft=istft)
 
-    def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None):
+    def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None, istft=True):
         S, W = self.spec, self.W
         B, T80 = x.B, x.T
         ng = W.dec_norm
@@ -649,6 +649,8 @@ class StyleTTSZS:
                   what="conv_post")
         if trace is not None:
             trace["post"] = post
+        if not istft:
+            return post
         Nout = (Tcur - 1) * S.istft_hop
         wav = self.buf("gen.wav", (B, Nout), torch.float32)
         a = L.IstftArgs()
@@ -656,6 +658,39 @@ class StyleTTSZS:
         a.B, a.Tf, a.n_fft, a.hop_s = B, Tcur, S.n_fft, S.istft_hop
         self._call(self.lib.stzs_istft, a, "istft")
         return wav
+
+    def istft_stream(self, post: Act, chunk_frames: int):
+        """iSTFT of conv_post frames [B, Tf, 22] in chunks of `chunk_frames` frames,
+        the 3-frame tail carried between chunks (ping-pong buffers).  Yields (n0, wav[:, n0:n1]) as each
+        chunk is enqueued; the views are slices of one [B, Nout] buffer, so no chunk overwrites another,
+        and their concatenation is bit-identical to the whole-utterance iSTFT."""
+        S = self.spec
+        B, Tf = post.B, post.T
+        Nout = (Tf - 1) * S.istft_hop
+        wav = self.buf("gen.wav_stream", (B, Nout), torch.float32)
+        ncol = _rup(S.n_fft + 2, 4)
+        tails = [self.buf("gen.tail0", (B, 8, ncol), torch.float32), self.buf("gen.tail1", (B, 8, ncol), torch.float32)]
+        n0, n1 = C.c_int64(), C.c_int64()
+        f0, i = 0, 0
+        while f0 < Tf:
+            Fc = min(chunk_frames, Tf - f0)
+            if 0 < Tf - f0 - Fc < 2:  # fold a 1-frame remainder (Tf = 600*T40/5 + 1) into this chunk
+                Fc = Tf - f0
+            fin = int(f0 + Fc == Tf)
+            halo = self.lib.stzs_istft_stream_span(f0, Fc, fin, S.n_fft, S.istft_hop, C.byref(n0), C.byref(n1))
+            L.check(min(halo, 0), "istft_stream_span")
+            assert halo <= 8
+            a = L.IstftStreamArgs()
+            a.post = post.ptr + f0 * post.ld * 4
+            a.tail_in = tails[i % 2].data_ptr() if f0 > 0 else None
+            a.tail_out = tails[(i + 1) % 2].data_ptr() if not fin else None
+            a.wav = wav.data_ptr() + n0.value * 4
+            a.ldp, a.bsp, a.bsw, a.ldt = post.ld, post.bs, Nout, ncol
+            a.B, a.f0, a.Fc, a.final_chunk, a.n_fft, a.hop_s = B, f0, Fc, fin, S.n_fft, S.istft_hop
+            self._call(self.lib.stzs_istft_stream, a, "istft_stream")
+            yield n0.value, wav[:, n0.value:n1.value]
+            f0 += Fc
+            i += 1
 
     def mrf(self, x: Act, i, gbd, ng):
         S, W = self.spec, self.W
@@ -725,6 +760,31 @@ class StyleTTSZS:
         seeds = list(range(B)) if seeds is None else seeds
         wav = self.decode(pro, codes, seeds)
         return dict(wav=wav, codes=codes, h_txt=h, prompt=prompt, **pro)
+
+
+    def synth_stream(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None,
+                     codes=None, n_frames=None, chunk_s=1.0):
+        """configs[4] long-form synthesis with the streaming iSTFT decoder: the text,
+        style, prosody and conv stack run over the whole target (AdaIN instance statistics are
+        utterance-global), then the waveform is emitted in `chunk_s`-second chunks.  Yields
+        (first_sample, wav_chunk [B, n]) device views; their concatenation equals synth()["wav"]."""
+        S = self.spec
+        dev = self.device
+        tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
+        B = tokens.shape[0]
+        h = self.text_encode(tokens)
+        prompt = self.prompt_encode(ref_wav.to(dev))
+        if prompt.shape[0] == 1 and B > 1:
+            pe = self.buf("prompt.bc", (B, S.L_s, S.code_dim), torch.float32)
+            pe.copy_(prompt.expand(B, -1, -1))
+            prompt = pe
+        if codes is None:
+            codes = self.sample_style(h, prompt, noise.to(dev, torch.float32), steps, cfg_scale)
+        pro = self.predict_prosody(h, codes, durations, n_frames)
+        seeds = list(range(B)) if seeds is None else seeds
+        post = self.decode(pro, codes, seeds, istft=False)
+        frames = max(1, int(round(chunk_s * S.sr / S.istft_hop)))
+        yield from self.istft_stream(post, frames)
 
 
 class _OffsetAct(Act):

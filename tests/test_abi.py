@@ -49,7 +49,7 @@ STRUCTS = {
     "stzs_attn_args": "AttnArgs", "stzs_lstm_args": "LstmArgs", "stzs_prprep_args": "PrPrepArgs",
     "stzs_dur_args": "DurArgs", "stzs_align_args": "AlignArgs", "stzs_gather_args": "GatherArgs",
     "stzs_dwup_args": "DwupArgs", "stzs_f0n_args": "F0nArgs", "stzs_source_args": "SourceArgs",
-    "stzs_istft_args": "IstftArgs", "stzs_copy_args": "CopyArgs",
+    "stzs_istft_args": "IstftArgs", "stzs_istft_stream_args": "IstftStreamArgs", "stzs_copy_args": "CopyArgs",
 }
 
 
@@ -98,3 +98,22 @@ def test_product_never_imports_oracle():
         if f.endswith(".py"):
             src = open(os.path.join(pkg, f)).read()
             assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f
+
+
+@pytest.mark.parametrize("Tf,chunks", [(24001, [4000] * 6 + [1]), (144001, [24000] * 6 + [1]), (9, [1, 1, 2, 5]),
+                                       (257, [256, 1]), (300, [2, 298])])
+def test_istft_stream_spans_tile_the_output(Tf, chunks):
+    """host-side span query (no GPU): the chunks' [n0, n1) tile [0, (Tf-1)*hop) exactly (row a14)."""
+    from stzs import _lib
+    L = _lib.load()
+    assert sum(chunks) == Tf
+    n0, n1 = C.c_int64(), C.c_int64()
+    f0, nxt = 0, 0
+    for i, Fc in enumerate(chunks):
+        halo = L.stzs_istft_stream_span(f0, Fc, int(i == len(chunks) - 1), 20, 5, C.byref(n0), C.byref(n1))
+        assert halo == 3
+        assert n0.value == nxt and n1.value >= n0.value
+        nxt = n1.value
+        f0 += Fc
+    assert nxt == (Tf - 1) * 5
+    assert L.stzs_istft_stream_span(0, 0, 1, 20, 5, C.byref(n0), C.byref(n1)) == _lib.ESHAPE

@@ -1,0 +1,131 @@
+"""configs[4] long-form path: the streaming iSTFT and a 30-s target.
+
+  * chunked stzs_istft_stream == whole-utterance stzs_istft, BIT-exact, for chunkings that include
+    chunks shorter than the 3-frame halo, a 1-frame final chunk and chunks at the 256-frame block size;
+  * the iSTFT itself against torch.istft (the oracle's call, oracle/stzs_ref.py generator) at 1e-5;
+  * a 30-s v0 synthesis: synth_stream's concatenated chunks == synth()'s waveform (bit-exact), and the
+    whole pipeline vs the CPU oracle within the e2e tolerance of tests/test_gpu_stages.py (3e-1 rel-L2).
+"""
+import ctypes as C
+
+import pytest
+import torch
+
+from refops import rel_err
+
+pytestmark = pytest.mark.gpu
+
+NFFT, HOP, NCOL = 20, 5, 24
+
+
+def _post(B, Tf, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    p = torch.zeros(B, Tf, NCOL)
+    p[:, :, :11] = torch.randn(B, Tf, 11, generator=g) * 0.5
+    p[:, :, 11:22] = torch.randn(B, Tf, 11, generator=g) * 2.0
+    return p
+
+
+def _full(L, lib, post):
+    B, Tf, _ = post.shape
+    Nout = (Tf - 1) * HOP
+    wav = torch.full((B, Nout), float("nan"), device=post.device)
+    a = L.IstftArgs()
+    a.post, a.wav, a.ldp, a.bsp, a.bsw = post.data_ptr(), wav.data_ptr(), NCOL, Tf * NCOL, Nout
+    a.B, a.Tf, a.n_fft, a.hop_s = B, Tf, NFFT, HOP
+    L.check(lib.stzs_istft(C.byref(a), None), "istft")
+    return wav
+
+
+def _chunked(L, lib, post, chunks):
+    B, Tf, _ = post.shape
+    Nout = (Tf - 1) * HOP
+    wav = torch.full((B, Nout), float("nan"), device=post.device)
+    tails = [torch.full((B, 3, NCOL), float("nan"), device=post.device) for _ in range(2)]
+    n0, n1 = C.c_int64(), C.c_int64()
+    f0 = 0
+    for i, Fc in enumerate(chunks):
+        fin = int(i == len(chunks) - 1)
+        assert lib.stzs_istft_stream_span(f0, Fc, fin, NFFT, HOP, C.byref(n0), C.byref(n1)) == 3
+        a = L.IstftStreamArgs()
+        a.post = post.data_ptr() + f0 * NCOL * 4
+        a.tail_in = tails[i % 2].data_ptr() if f0 else None
+        a.tail_out = None if fin else tails[(i + 1) % 2].data_ptr()
+        a.wav = wav.data_ptr() + n0.value * 4
+        a.ldp, a.bsp, a.bsw, a.ldt = NCOL, Tf * NCOL, Nout, NCOL
+        a.B, a.f0, a.Fc, a.final_chunk, a.n_fft, a.hop_s = B, f0, Fc, fin, NFFT, HOP
+        L.check(lib.stzs_istft_stream(C.byref(a), None), "istft_stream")
+        f0 += Fc
+    assert f0 == Tf
+    return wav
+
+
+@pytest.mark.parametrize("Tf,chunks", [
+    (24001, [4800] * 5 + [1]),
+    (24001, [256] * 93 + [193]),
+    (2001, [1, 2, 3, 1, 1, 5, 700, 1288]),
+    (1025, [512, 512, 1]),
+    (600, [2, 598]),
+])
+def test_istft_stream_bitexact(gpu_device, Tf, chunks):
+    from stzs import _lib as L
+    lib = L.load()
+    post = _post(2, Tf).to(gpu_device)
+    full = _full(L, lib, post)
+    ch = _chunked(L, lib, post, chunks)
+    torch.cuda.synchronize()
+    assert torch.isfinite(full).all()
+    assert torch.equal(full, ch), (full - ch).abs().max().item()
+
+
+def test_istft_vs_torch(gpu_device):
+    from stzs import _lib as L
+    lib = L.load()
+    Tf = 4001
+    post = _post(2, Tf, seed=3)
+    full = _full(L, lib, post.to(gpu_device)).cpu()
+    mag, ph = torch.exp(post[:, :, :11]), torch.sin(post[:, :, 11:22])
+    spec = (mag * torch.exp(1j * ph)).transpose(1, 2)
+    ref = torch.istft(spec, NFFT, hop_length=HOP, win_length=NFFT, window=torch.hann_window(NFFT))
+    assert full.shape == ref.shape
+    e = rel_err(full, ref)
+    print("istft vs torch.istft rel", e)
+    assert e < 1e-5
+
+
+@pytest.fixture(scope="module")
+def v0():
+    from stzs.params import init_params
+    from stzs.spec import SPEC_V0
+    return SPEC_V0, init_params(SPEC_V0, seed=0)
+
+
+def test_longform_30s_stream(gpu_device, v0):
+    """configs[4] shape: one 30-s target (T_txt 480, 1200 aligned frames, 720 000 samples)."""
+    from oracle import stzs_ref as R
+    from stzs.engine import StyleTTSZS
+    S, P = v0
+    eng = StyleTTSZS(S, P, device=gpu_device)
+    T = 480
+    g = torch.Generator().manual_seed(77)
+    tok = torch.randint(1, S.n_symbols, (1, T), generator=g)
+    ref = torch.randn(1, 3 * S.sr, generator=g) * 0.1
+    eps = torch.randn(1, S.L_s, S.code_dim, generator=g)
+    dur = torch.tensor([[3, 2] * (T // 2)], dtype=torch.int32)
+    kw = dict(steps=2, cfg_scale=5.0, noise=eps, durations=dur, seeds=[7])
+    full = eng.synth(tok, ref, **kw)["wav"].clone()
+    parts = [(n0, w.clone()) for n0, w in eng.synth_stream(tok, ref, chunk_s=1.0, **kw)]
+    torch.cuda.synchronize()
+    assert full.shape == (1, 720000)
+    assert len(parts) == 30
+    nxt = 0
+    for n0, w in parts:
+        assert n0 == nxt
+        nxt += w.shape[1]
+    stream = torch.cat([w for _, w in parts], 1)
+    assert torch.equal(stream, full)
+    o = R.synth(P, S, tok, ref, 2, 5.0, eps, dur, seeds=[7])
+    e = rel_err(full.cpu(), o["wav"])
+    print("30-s e2e rel vs oracle", e)
+    assert torch.isfinite(full).all()
+    assert e < 3e-1
