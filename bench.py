@@ -73,6 +73,43 @@ def cpu_baseline(S, P, budget_s=15.0):
                        f"CPU oracle torch fp32, {el:.1f} s")
 
 
+def longform(S, P, dev, runs=7):
+    """configs[4] latency: one 30-s target (T_txt 480), 2-step CFG-5 sampling on fp8 e4m3 denoiser linears,
+    waveform emitted by the streaming iSTFT in 1-s chunks.  Eager launches (no graph); p50 over runs."""
+    from stzs.engine import StyleTTSZS
+    e8 = StyleTTSZS(S, P, device=dev, fp8_denoiser=True)
+    T = int(TOK_PER_S * 30)
+    g = torch.Generator().manual_seed(99)
+    tok = torch.randint(1, S.n_symbols, (1, T), generator=g).to(dev, torch.int32)
+    ref = (torch.randn(1, int(REF_S * S.sr), generator=g) * 0.1).to(dev)
+    eps = torch.randn(1, S.L_s, S.code_dim, generator=g).to(dev)
+    dur = torch.tensor([[3, 2] * (T // 2)], dtype=torch.int32).to(dev)
+    nf = int(40 * 30)
+    first, total = [], []
+    for i in range(runs + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 0
+        for j, (_, w) in enumerate(e8.synth_stream(tok, ref, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps,
+                                                   durations=dur, seeds=[3], n_frames=nf, chunk_s=1.0)):
+            if j == 0:
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+            n += w.shape[1]
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        assert n == 30 * S.sr
+        if i:
+            first.append((t1 - t0) * 1e3)
+            total.append((t2 - t0) * 1e3)
+    del e8
+    return dict(config="configs[4]: batch 1, 30-s target, 2-step CFG-5, fp8 e4m3 denoiser linears, "
+                       "streaming iSTFT in 1-s chunks, eager", audio_s=30.0,
+                p50_first_chunk_ms=round(float(np.percentile(first, 50)), 3),
+                p50_total_ms=round(float(np.percentile(total, 50)), 3),
+                realtime_factor=round(30.0 / (float(np.percentile(total, 50)) * 1e-3), 1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,6 +119,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-longform", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -194,6 +232,11 @@ def main():
         lat = dict(p50_ms=round(float(np.percentile(ts, 50)), 3), p90_ms=round(float(np.percentile(ts, 90)), 3),
                    config="batch 1, 10-step sampling, CFG 5, 5-s target, 3-s reference")
 
+    # ---- configs[4]: 30-s target, batch 1, fp8 denoiser linears, streaming iSTFT (1-s chunks) ----
+    lf = None
+    if not args.no_longform and world == 1:
+        lf = longform(S, P, dev)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(S, P)
@@ -221,6 +264,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "weight_broadcast_ms": round(bcast_ms, 3),
+            "longform": lf,
         }
         print(json.dumps(line))
     if world > 1:

@@ -32,7 +32,7 @@ extern "C" {
 #define STZS_EDTYPE (-3)  /* unsupported dtype combination */
 #define STZS_EHIP (-4)    /* HIP runtime error on launch */
 
-enum { STZS_F32 = 0, STZS_BF16 = 1, STZS_I32 = 2 };
+enum { STZS_F32 = 0, STZS_BF16 = 1, STZS_I32 = 2, STZS_F8 = 3 /* OCP e4m3fn (gfx950), with a row scale */ };
 enum { STZS_ACT_NONE = 0, STZS_ACT_LEAKY = 1, STZS_ACT_SNAKE = 2, STZS_ACT_GELU = 3, STZS_ACT_SILU = 4 };
 enum { STZS_PRO_NONE = 0, STZS_PRO_ADAIN = 1 };
 /* stzs_conv_args.flags: the caller guarantees that for a ks=1 bf16 linear every input row can be
@@ -80,6 +80,13 @@ typedef struct stzs_conv_args {
      * Plain (non-ConvTranspose, non-linear) convs only; NULL = off. */
     void* stat_part;
     int64_t stat_ld;
+    /* fp8 linears (configs[4] denoiser, in_dtype = STZS_F8): x rows are e4m3fn codes with one fp32
+     * scale per flat row (x_scale[b * T_in + t], e.g. from stzs_row_layernorm / stzs_quant_rows), the
+     * weights an e4m3fn K-step stream [co_pad/128][ci_pad/64][128][64] (stzs/weights.py pack_conv_f8)
+     * with one fp32 scale per output column (w_scale[co_pad]); acc * x_scale * w_scale enters the
+     * usual epilogue.  Plain linears only (ks = 1, flags STZS_CONV_A_DMA); NULL otherwise. */
+    const float* x_scale;
+    const float* w_scale;
 } stzs_conv_args;
 #define STZS_CONV_STAT_ROWS 64
 /* flags bit: weights packed with the 16-lane channel permutation of the MRF kernel (stzs/weights.py
@@ -123,8 +130,24 @@ typedef struct stzs_rowln_args {
     int64_t ldx, ldy, gs, bs;
     int32_t R, C, gdiv, in_dtype, out_dtype, act;
     float gadd, eps, slope, pad_f;
+    /* out_dtype = STZS_F8: y holds e4m3fn codes of y / y_scale[r], y_scale[r] the power-of-two row
+     * scale of stzs_quant_rows */
+    float* y_scale;
 } stzs_rowln_args;
 int stzs_row_layernorm(const stzs_rowln_args* a, void* stream);
+
+/* per-row fp8 quantisation with a power-of-two row scale (exact scaling, as MX block scales):
+ * scale[r] = 2^k_r, the smallest power of two with amax_r / 2^k_r <= 448 (1 for an all-zero row),
+ * y[r, c] = e4m3fn_rne(x[r, c] / scale[r]); x bf16 [R, ldx], C % 8 == 0, C <= 2048, ldy % 16 == 0.
+ * (configs[4]: attention outputs and the FFN hidden rows entering the fp8 denoiser linears) */
+typedef struct stzs_quant_args {
+    const void* x;
+    void* y;
+    float* scale;
+    int64_t ldx, ldy;
+    int32_t R, C;
+} stzs_quant_args;
+int stzs_quant_rows(const stzs_quant_args* a, void* stream);
 
 /* ---- multi-head attention, softmax(q k^T / sqrt(dh)) v, rows independent ----------------
  * q [R, Lq, ldq], k/v [R, Lk, ldk/ldv], o [R, Lq, ldo]; bf16; heads x dh = D.

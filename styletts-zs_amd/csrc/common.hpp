@@ -71,6 +71,18 @@ STZS_DEV void store8(float* p, const float* v) {
     *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
 
+// fp8 (OCP e4m3fn on gfx950): raw byte codes; per-row scaled so |v| <= 448 before conversion
+typedef uint8_t f8_t;
+// 8 floats already in [-448, 448] -> 8 e4m3fn codes (two v_cvt_pk_fp8_f32 per 4 values, RNE)
+STZS_DEV uint2 pack8f8(const float* v) {
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
+    return make_uint2((uint32_t)lo, (uint32_t)hi);
+}
+STZS_DEV float f8_clamp(float x) { return fminf(fmaxf(x, -448.f), 448.f); }
+
 STZS_DEV float act_apply(int act, float x, float slope, float alpha) {
     switch (act) {
         case STZS_ACT_LEAKY: return x >= 0.f ? x : x * slope;

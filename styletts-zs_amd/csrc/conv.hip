@@ -527,29 +527,35 @@ STZS_DEV void glds16(const void* src, void* dst) {
                                      (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
-// Pure GEMM for bf16 linears (ks = 1, no prologue): BOTH operands stream through an LDS-DMA ring,
-// one 32-wide K-step per slot (A: 128 rows x 32 k, B: 128 cols x 32 k, 8 KB each), 4 slots filled
-// three K-steps ahead.  The A image takes the same XOR swizzle as B through its per-lane SOURCE
-// addresses (LDS-DMA writes lane-linearly), so both fragment reads are conflict-free ds_read_b128.
-// Per K-step: counted vmcnt + one s_barrier, then the NEXT K-step's fragments are read between the
-// current K-step's 16 MFMAs (as csrc/mrf.hip); the body is branch-free (a fill past the end re-copies
-// the last K-step into a retired slot) and the last K-step is peeled.
+// Pure GEMM for linears (ks = 1, no prologue): BOTH operands stream through an LDS-DMA ring, one
+// 64-byte-per-row K-step per slot (bf16: 32 k; fp8: 64 k.  A: BTM rows, B: 128 cols, 8 KB each at
+// BTM = 128), 4 slots filled three K-steps ahead.  The A image takes the same XOR swizzle as B
+// through its per-lane SOURCE addresses (LDS-DMA writes lane-linearly), so both fragment reads are
+// conflict-free ds_read_b128.  Per K-step: counted vmcnt + one s_barrier, then the NEXT K-step's
+// fragments are read between the current K-step's MFMAs (as csrc/mrf.hip); the body is branch-free
+// (a fill past the end re-copies the last K-step into a retired slot) and the last K-step is peeled.
+// F8 (configs[4] denoiser): e4m3fn operands; each 16-B fragment feeds TWO v_mfma_f32_16x16x32_fp8_fp8
+// (bytes 0-7 and 8-15: both operands use the same k permutation, so the dot product is unchanged),
+// and acc * x_scale[row] * w_scale[col] enters the epilogue.
 template <int BTM>
-constexpr int gslot() { return BTM * 64 + SLOT_BYTES; }  // A (BTM rows x 32 k) + B of one K-step
-template <typename TOut, int BTM>
+constexpr int gslot() { return BTM * 64 + SLOT_BYTES; }  // A (BTM rows x 64 B) + B of one K-step
+typedef __attribute__((ext_vector_type(2))) long i64x2;
+template <typename TOut, int BTM, bool F8>
 __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     constexpr int MT = BTM / 32;           // 16-row tiles per wave (2 x 2 waves)
     constexpr int GS = gslot<BTM>();
     constexpr int AP = BTM / 64;           // A pieces (1 KB) per wave per K-step
+    constexpr int ESZ = F8 ? 1 : 2;        // operand bytes per element
+    constexpr int NMF = MT * 4 * (F8 ? 2 : 1);  // MFMAs per K-step
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
     const long row0 = (long)blockIdx.x * BTM;
     const long nR = (long)a.B * a.T_in;
-    const int NK = a.ci_pad >> 5;
-    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
-    const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x);
-    long asrc[AP];
+    const int NK = a.ci_pad / (64 / ESZ);
+    const unsigned char* Wt = reinterpret_cast<const unsigned char*>(a.w) + (long)blockIdx.y * NK * SLOT_BYTES;
+    const unsigned char* X = reinterpret_cast<const unsigned char*>(a.x);
+    long asrc[AP];  // byte offsets
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
         const int o = wave * AP * 1024 + i * 1024 + lane * 16;
@@ -557,17 +563,17 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         long R = row0 + r;
         R = R < nR ? R : nR - 1;
         const long bb = R / a.T_in;
-        asrc[i] = bb * a.bsx + (R - bb * a.T_in) * a.ldx + ((p ^ gswz(r)) << 3);
+        asrc[i] = (bb * a.bsx + (R - bb * a.T_in) * a.ldx) * ESZ + ((p ^ gswz(r)) << 4);
     }
     auto fill = [&](int k) {
         const int kc = k < NK ? k : NK - 1;
-        const bf16_t* src = Wt + (long)kc * (BCO * 32) + wave * 1024 + lane * 8;
+        const unsigned char* src = Wt + (long)kc * SLOT_BYTES + wave * 2048 + lane * 16;
         unsigned char* da = smem + (k & 3) * GS + wave * AP * 1024;
         unsigned char* db = smem + (k & 3) * GS + BTM * 64 + wave * 2048;
         glds16(src, db);
-        glds16(src + 512, db + 1024);
+        glds16(src + 1024, db + 1024);
 #pragma unroll
-        for (int i = 0; i < AP; ++i) glds16(X + asrc[i] + kc * 32, da + i * 1024);
+        for (int i = 0; i < AP; ++i) glds16(X + asrc[i] + kc * 64, da + i * 1024);
     };
     int aoff0, boff0;
     {
@@ -593,8 +599,16 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+            for (int nt = 0; nt < 4; ++nt) {
+                if constexpr (F8) {
+                    const i64x2 va = __builtin_bit_cast(i64x2, fa[mt]);
+                    const i64x2 vb = __builtin_bit_cast(i64x2, fb[nt]);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(va[0], vb[0], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(va[1], vb[1], acc[mt][nt], 0, 0, 0);
+                } else {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+                }
+            }
     };
     constexpr int PER_FILL = 2 + AP;  // LDS-DMA instructions per wave per K-step
     fill(0);
@@ -615,7 +629,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  \
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                  \
         }                                                                       \
-        __builtin_amdgcn_sched_group_barrier(0x008, MT * 4 - MT - 4, 0);        \
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF - MT - 4, 0);           \
         __builtin_amdgcn_sched_barrier(0);                                      \
         ++k;                                                                    \
     }
@@ -632,6 +646,21 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         mma(fa0, fb0);
     }
 #undef STZS_GEMM_STEP
+    if constexpr (F8) {  // dequantise: row scale (flat row, clamped like the A rows) x column scale
+        float sw[4];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) sw[nt] = a.w_scale[blockIdx.y * BCO + wc * 64 + nt * 16 + (lane & 15)];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                long R = row0 + wt * (BTM / 2) + mt * 16 + (lane >> 4) * 4 + r;
+                R = R < nR ? R : nR - 1;
+                const float sx = a.x_scale[R];
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) acc[mt][nt][r] *= sx * sw[nt];
+            }
+    }
     finish<TOut, true, BTM>(a, acc, smem, 0, 0, row0);
 }
 
@@ -641,7 +670,7 @@ size_t lds_bytes(int rows_in, int cic) {
     return main > epi ? main : epi;
 }
 
-template <typename TIn, typename TOut>
+template <typename TIn, typename TOut, bool F8 = false>
 int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     const bool flat = (a.ks == 1 && a.stride == 1 && a.pad == 0 && a.ups == 0 && a.pro_mode == STZS_PRO_NONE &&
                        a.pro_act == STZS_ACT_NONE && a.T_in == a.T_out);
@@ -653,7 +682,7 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     dim3 grid(gx, a.co_pad / BCO);
     if (flat && a.stat_part) return STZS_EINVAL;  // fused statistics: per-utterance tiles only
     void (*k)(stzs_conv_args);
-    if (flat && sizeof(TIn) == 2 && (a.flags & STZS_CONV_A_DMA) && a.pro_cscale == 1.f) {
+    if (F8 || (flat && sizeof(TIn) == 2 && (a.flags & STZS_CONV_A_DMA) && a.pro_cscale == 1.f)) {
         // 64-row tiles when 128-row tiles would leave the GPU under-filled (< 2 workgroups per CU)
         static int n_cu = 0;
         if (n_cu == 0) {
@@ -666,25 +695,29 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
         size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
         const size_t lr = 4 * (size_t)(small ? gslot<64>() : gslot<128>());
         lg = lg > lr ? lg : lr;
-        auto kg = small ? gemm_glds<TOut, 64> : gemm_glds<TOut, 128>;
+        auto kg = small ? gemm_glds<TOut, 64, F8> : gemm_glds<TOut, 128, F8>;
         if (small) grid.x = (unsigned)(((long)a.B * a.T_out + 63) / 64);
         (void)hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);
         hipLaunchKernelGGL(kg, grid, dim3(NTHR), lg, s, a);
         STZS_LAUNCH_CHECK();
         return STZS_OK;
     }
-    if (flat)
-        k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE>;
-    else if (a.pro_act == STZS_ACT_SNAKE)
-        k = conv_mfma<TIn, TOut, false, STZS_ACT_SNAKE>;
-    else if (a.pro_act == STZS_ACT_LEAKY)
-        k = conv_mfma<TIn, TOut, false, STZS_ACT_LEAKY>;
-    else
-        k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE>;
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, a);
-    STZS_LAUNCH_CHECK();
-    return STZS_OK;
+    if constexpr (F8) {
+        return STZS_EDTYPE;  // (unreachable: fp8 is a pure linear)
+    } else {
+        if (flat)
+            k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE>;
+        else if (a.pro_act == STZS_ACT_SNAKE)
+            k = conv_mfma<TIn, TOut, false, STZS_ACT_SNAKE>;
+        else if (a.pro_act == STZS_ACT_LEAKY)
+            k = conv_mfma<TIn, TOut, false, STZS_ACT_LEAKY>;
+        else
+            k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE>;
+        if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, a);
+        STZS_LAUNCH_CHECK();
+        return STZS_OK;
+    }
 }
 
 }  // namespace
@@ -716,6 +749,17 @@ extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
     if (a->stat_part && (a->ups > 0 || !epi_vec(*a) || a->stat_ld < a->Co || !stzs_aligned(a->stat_part, 8)))
         return STZS_EINVAL;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (a->in_dtype == STZS_F8) {
+        const bool lin = a->ks == 1 && a->stride == 1 && a->pad == 0 && a->ups == 0 && a->T_in == a->T_out &&
+                         a->pro_mode == STZS_PRO_NONE && a->pro_act == STZS_ACT_NONE && a->pro_cscale == 1.f;
+        if (!lin || !(a->flags & STZS_CONV_A_DMA) || (a->flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32)))
+            return STZS_EDTYPE;
+        if (!a->x_scale || !a->w_scale || a->stat_part) return STZS_EINVAL;
+        if (a->ci_pad % 64 || a->ldx % 16 || a->bsx % 16) return STZS_ESHAPE;
+        if (a->out_dtype == STZS_BF16) return launch_dt<f8_t, bf16_t, true>(*a, s);
+        if (a->out_dtype == STZS_F32) return launch_dt<f8_t, float, true>(*a, s);
+        return STZS_EDTYPE;
+    }
     if (a->flags & STZS_CONV_W_LANE16) return stzs_mrf_conv_launch(*a, s);
     if (a->flags & STZS_CONV_W_NARROW32) return stzs_narrow_conv_launch(*a, s);
     if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) return launch_dt<bf16_t, bf16_t>(*a, s);

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STZS_LIB", os.path.join(_HERE, "libstzs_hip.so"))
 
-F32, BF16, I32 = 0, 1, 2
+F32, BF16, I32, F8 = 0, 1, 2, 3
 OK, EINVAL, ESHAPE, EDTYPE, EHIP = 0, -1, -2, -3, -4
 ACT_NONE, ACT_LEAKY, ACT_SNAKE, ACT_GELU, ACT_SILU = 0, 1, 2, 3, 4
 PRO_NONE, PRO_ADAIN = 0, 1
@@ -35,7 +35,7 @@ class ConvArgs(C.Structure):
                                    "ci_pad", "co_pad", "cic", "ups", "ups_pad", "T_final", "refl", "res_tdiv",
                                    "in_dtype", "out_dtype", "pro_mode", "pro_act", "epi_act", "flags")] + \
                [(n, f32) for n in ("pro_cscale", "pro_slope", "epi_slope", "alpha", "beta", "pad_f")] + \
-               [("stat_part", vp), ("stat_ld", i64)]
+               [("stat_part", vp), ("stat_ld", i64), ("x_scale", vp), ("w_scale", vp)]
 
 
 class StatsArgs(C.Structure):
@@ -48,7 +48,11 @@ class RowLNArgs(C.Structure):
     _fields_ = [("x", vp), ("y", vp), ("G", vp), ("Bt", vp),
                 ("ldx", i64), ("ldy", i64), ("gs", i64), ("bs", i64),
                 ("R", i32), ("C", i32), ("gdiv", i32), ("in_dtype", i32), ("out_dtype", i32), ("act", i32),
-                ("gadd", f32), ("eps", f32), ("slope", f32), ("pad_f", f32)]
+                ("gadd", f32), ("eps", f32), ("slope", f32), ("pad_f", f32), ("y_scale", vp)]
+
+
+class QuantArgs(C.Structure):
+    _fields_ = [("x", vp), ("y", vp), ("scale", vp), ("ldx", i64), ("ldy", i64), ("R", i32), ("C", i32)]
 
 
 class AttnArgs(C.Structure):
@@ -121,7 +125,7 @@ class CopyArgs(C.Structure):
 
 # every exported symbol of include/stzs.h (tests check the .so exports exactly these)
 EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_chan_stats_workspace",
-           "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
+           "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
            "stzs_dn_cond", "stzs_adaln_expand", "stzs_cfg_euler",
@@ -153,6 +157,7 @@ def load():
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
         "stzs_chan_stats_final": ([P(StatsArgs), i32, vp], i32),
         "stzs_row_layernorm": ([P(RowLNArgs), vp], i32),
+        "stzs_quant_rows": ([P(QuantArgs), vp], i32),
         "stzs_attention": ([P(AttnArgs), vp], i32),
         "stzs_lstm_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_lstm": ([P(LstmArgs), vp], i32),

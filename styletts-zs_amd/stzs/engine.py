@@ -30,7 +30,7 @@ from .frontend import log_mel, mel_filterbank
 from .spec import Spec
 from .weights import ConvW, PackedModel
 
-_DT = {torch.float32: L.F32, torch.bfloat16: L.BF16}
+_DT = {torch.float32: L.F32, torch.bfloat16: L.BF16, torch.float8_e4m3fn: L.F8}
 
 
 def _rup(x, m):
@@ -103,8 +103,11 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 
 
 class StyleTTSZS:
-    def __init__(self, spec: Spec, params, device="cuda:0", fill=True):
+    def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False):
+        """fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
+        per-row activation / per-column weight scales (configs[4]); bf16 otherwise."""
         self.spec = spec
+        self.fp8_denoiser = fp8_denoiser
         self.device = torch.device(device)
         self.lib = L.load()
         L.check(self.lib.stzs_init(self.device.index or 0), "stzs_init")
@@ -146,7 +149,7 @@ class StyleTTSZS:
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
-             T_final=0, refl=0, flags=0, stats_key=None, what="conv"):
+             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
         output fused into the conv epilogue (per-tile partials) + one small finalize launch."""
         W = self.W
@@ -180,8 +183,12 @@ class StyleTTSZS:
         if gate is not None:
             a.gate, a.gate_bs = gate, gate_bs
         a.alpha, a.beta, a.epi_act, a.epi_slope = alpha, beta, epi_act, epi_slope
+        if cw.f8:
+            assert x.t.dtype == torch.float8_e4m3fn and x_scale is not None, what
+            a.x_scale, a.w_scale = x_scale.data_ptr(), self._t(cw.wscale).data_ptr()
         if (cw.ks == 1 and stride == 1 and pad == 0 and not cw.ups and pro is None and pro_act == L.ACT_NONE
-                and cscale == 1.0 and x.t.dtype == torch.bfloat16 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
+                and cscale == 1.0 and x.t.dtype in (torch.bfloat16, torch.float8_e4m3fn)
+                and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
         if getattr(cw, "lane16", False):
             flags |= L.CONV_W_LANE16  # MRF-family kernel (csrc/mrf.hip)
@@ -255,8 +262,9 @@ class StyleTTSZS:
         return mean, rstd, Cc
 
     def rowln(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=1.0, act=L.ACT_NONE, slope=0.0,
-              R=None, what="rowln"):
+              R=None, y_scale=None, what="rowln"):
         a = L.RowLNArgs()
+        a.y_scale = y_scale.data_ptr() if y_scale is not None else None
         a.x, a.y, a.G, a.Bt = x.ptr, y.ptr, G, Bt
         a.ldx, a.ldy, a.gs, a.bs = x.ld, y.ld, gs, bs
         a.R = R if R is not None else x.B * x.T
@@ -264,6 +272,14 @@ class StyleTTSZS:
         a.gadd, a.eps, a.slope = gadd, 1e-5, slope
         assert x.ld * x.T == x.bs and y.ld * y.T == y.bs
         self._call(self.lib.stzs_row_layernorm, a, what)
+
+    def quant(self, x: Act, y: Act, scale: torch.Tensor, what="quant"):
+        """bf16 rows -> e4m3fn rows + per-row scale (stzs_quant_rows)."""
+        a = L.QuantArgs()
+        a.x, a.y, a.scale, a.ldx, a.ldy = x.ptr, y.ptr, scale.data_ptr(), x.ld, y.ld
+        a.R, a.C = x.B * x.T, x.C
+        assert x.ld * x.T == x.bs and y.ld * y.T == y.bs
+        self._call(self.lib.stzs_quant_rows, a, what)
 
     def attention(self, q: Act, k: Act, v: Act, o: Act):
         S = self.spec
@@ -399,6 +415,14 @@ class StyleTTSZS:
         xa = Act(x)
         pos = Act(W.t(W.dn_pos)[None])
         fsz = 4
+        f8 = self.fp8_denoiser
+        if f8:  # e4m3fn operand rows + per-row scales for the layer linears
+            an8 = self.act("dn.a8", R, Ls, d, torch.float8_e4m3fn)
+            o8 = self.act("dn.o8", R, Ls, d, torch.float8_e4m3fn)
+            ff8 = self.act("dn.ff8", R, Ls, S.dn_ffn, torch.float8_e4m3fn)
+            s_an = self.buf("dn.a8s", (R * Ls,), torch.float32)
+            s_o = self.buf("dn.o8s", (R * Ls,), torch.float32)
+            s_ff = self.buf("dn.ff8s", (R * Ls,), torch.float32)
         for i in range(steps):
             s0 = sig[i]
             co = edm_coeffs(S, s0)
@@ -415,6 +439,9 @@ class StyleTTSZS:
             self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, what="dn.in")
             for l, lw in enumerate(W.dn_layers):
                 mb = modx[l].data_ptr()
+                if f8:
+                    self._dn_layer_f8(lw, mb, h, an8, s_an, qkv, o, o8, s_o, q, ff, ff8, s_ff, kv[l], Ls, d, fsz)
+                    continue
                 self.rowln(h, an, G=mb + d * fsz, gs=6 * d, Bt=mb, bs=6 * d, gdiv=Ls, gadd=0.0, what="ln1")
                 self.conv(lw["qkv"], an, qkv, what="qkv")
                 self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
@@ -435,6 +462,27 @@ class StyleTTSZS:
             L.check(self.lib.stzs_cfg_euler(x.data_ptr(), D.t.data_ptr(), B, N, int(cfg), float(cfg_scale),
                                             float(s0), float(sig[i + 1] - s0), self.stream()), "cfg_euler")
         return x[:B]
+
+    def _dn_layer_f8(self, lw, mb, h, an8, s_an, qkv, o, o8, s_o, q, ff, ff8, s_ff, kv, Ls, d, fsz):
+        """one denoiser layer with e4m3fn linears: the adaLN / LayerNorm rows are quantised by the norm
+        kernel itself (one scale per row), attention outputs and the GELU rows by stzs_quant_rows."""
+        W = self.W
+        self.rowln(h, an8, G=mb + d * fsz, gs=6 * d, Bt=mb, bs=6 * d, gdiv=Ls, gadd=0.0, y_scale=s_an, what="ln1")
+        self.conv(lw["qkv8"], an8, qkv, x_scale=s_an, what="qkv")
+        self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
+        self.quant(o, o8, s_o)
+        self.conv(lw["o8"], o8, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=s_o, what="sa_o")
+        self.rowln(h, an8, G=W.t(lw["ln_g"]).data_ptr(), gs=0, Bt=W.t(lw["ln_b"]).data_ptr(), bs=0, gadd=0.0,
+                   y_scale=s_an, what="ca_ln")
+        self.conv(lw["q8"], an8, q, x_scale=s_an, what="ca_q")
+        self.attention(q, kv.sl(0, d), kv.sl(d, d), o)
+        self.quant(o, o8, s_o)
+        self.conv(lw["co8"], o8, h, res=h, x_scale=s_o, what="ca_o")
+        self.rowln(h, an8, G=mb + 4 * d * fsz, gs=6 * d, Bt=mb + 3 * d * fsz, bs=6 * d, gdiv=Ls, gadd=0.0,
+                   y_scale=s_an, what="ln2")
+        self.conv(lw["ff18"], an8, ff, epi_act=L.ACT_GELU, x_scale=s_an, what="ff1")
+        self.quant(ff, ff8, s_ff)
+        self.conv(lw["ff28"], ff8, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=s_ff, what="ff2")
 
     def _conv_rows(self, cw, x: Act, dst: torch.Tensor, b0, t0, what):
         """linear over x [B, T, C] written to dst[b0 + b, t0 + t, :] (dst rows have a larger T)."""

@@ -43,6 +43,8 @@ class ConvW:
     ups: int = 0
     lane16: bool = False  # packed with the MRF kernel's channel permutation (STZS_CONV_W_LANE16)
     narrow32: bool = False  # [NK][32][32] narrow packing (STZS_CONV_W_NARROW32)
+    wscale: Optional[object] = None  # fp8 linears: per-output-column fp32 scale [co_pad]
+    f8: bool = False
 
 
 class Arena:
@@ -164,6 +166,44 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False) ->
     return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16)
 
 
+def quantize_f8_cols(w: torch.Tensor):
+    """Linear [Co, Ci] fp32 -> (e4m3fn codes [Co, Ci], per-output-channel scale [Co]):
+    scale = max|w_co| / 448 (1 for an all-zero row), codes = e4m3fn(clamp(w / scale, +-448)) (RNE)."""
+    amax = w.abs().amax(1)
+    scale = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    q = (w / scale[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    return q, scale
+
+
+def kstep_stream_f8(q: torch.Tensor) -> torch.Tensor:
+    """e4m3fn [co_pad, ci_pad] (as uint8) -> [co_pad/128, ci_pad/64, 128, 64]: the 64-k K-steps of the fp8
+    GEMM (csrc/conv.hip gemm_glds<F8>), 16-B chunk c of row r at position c ^ g((r >> 2) & 3) exactly as
+    kstep_stream (a K-step row is 64 B in both dtypes: 32 bf16 or 64 fp8 values)."""
+    co_pad, ci_pad = q.shape
+    ncot, nk = co_pad // 128, ci_pad // 64
+    t = q.view(ncot, 128, nk, 4, 16).permute(0, 2, 1, 3, 4)  # cot, kstep, r, c, 16
+    r = torch.arange(128)
+    g = torch.tensor(_GSWZ)[(r >> 2) & 3]
+    src_c = torch.arange(4)[None, :] ^ g[:, None]
+    t = t[:, :, r[:, None], src_c, :]
+    return t.reshape(ncot, nk, 128, 64).contiguous()
+
+
+def pack_conv_f8(A: Arena, name, w, b=None) -> ConvW:
+    """fp8 e4m3fn Linear [Co, Ci] for the configs[4] denoiser (include/stzs.h stzs_conv_args.w_scale)."""
+    Co, Ci = w.shape
+    ci_pad, co_pad = _rup(Ci, 64), _rup(Co, 128)
+    q, sc = quantize_f8_cols(w.float())
+    qp = torch.zeros(co_pad, ci_pad, dtype=torch.uint8)
+    qp[:Co, :Ci] = q.view(torch.uint8)
+    scp = torch.ones(co_pad)
+    scp[:Co] = sc
+    wn = A.add(name + ".wf8", kstep_stream_f8(qp))
+    sn = A.add(name + ".sf8", scp)
+    bn = A.add(name + ".bf8", b.float().clone()) if b is not None else None
+    return ConvW(wn, bn, Ci, Co, 1, ci_pad, co_pad, 64, wscale=sn, f8=True)
+
+
 @dataclass
 class NormGroup:
     """all AdaIN fc layers of one stage, packed as one linear; offsets per norm name."""
@@ -282,6 +322,10 @@ class PackedModel:
                 qkv=L(p + ".sa_qkv"), o=L(p + ".sa_o"), q=L(p + ".ca_q"), kv=L(p + ".ca_kv"), co=L(p + ".ca_o"),
                 ff1=L(p + ".ff1"), ff2=L(p + ".ff2"),
                 ln_g=A.add(p + ".ca_ln.g", P[p + ".ca_ln.g"]), ln_b=A.add(p + ".ca_ln.b", P[p + ".ca_ln.b"])))
+            # fp8 e4m3fn copies of the per-layer linears (configs[4]: StyleTTSZS(fp8_denoiser=True))
+            for key, n in (("qkv", ".sa_qkv"), ("o", ".sa_o"), ("q", ".ca_q"), ("co", ".ca_o"), ("ff1", ".ff1"),
+                           ("ff2", ".ff2")):
+                self.dn_layers[-1][key + "8"] = pack_conv_f8(A, p + n + ".f8", P[p + n + ".w"], P[p + n + ".b"])
         # --- predictor ---
         self.pr_de = [pack_lstm(A, f"pr.de{i}", P) for i in range(S.pr_layers)]
         self.pr_aln = [L(f"pr.de{i}.aln") for i in range(S.pr_layers)]
