@@ -99,6 +99,12 @@ typedef struct stzs_conv_args {
  * narrow conv of csrc/mrf.hip: 128-channel chunks, bf16 in, fp32 out, LeakyReLU / identity prologue
  * (no AdaIN), bias, alpha; no residual / gate / statistics.  (conv_post: 128 -> 22 channels) */
 #define STZS_CONV_W_NARROW32 32
+/* flags bit: PRECISE (parity) mode -- fp32 weights packed [co_pad/128][ci_pad/32][ks][128 co][32 ci]
+ * (stzs/weights.py kstep_stream_f32, cic = 32) and fp32 operands on v_mfma_f32_16x16x4_f32 (exact fp32
+ * products, fp32 accumulate), libm-accurate prologue activations; bf16|f32 in, bf16|f32 out, every
+ * conv feature except the fp8 path.  Used by StyleTTSZS(precise_decoder=True) to meet the north-star
+ * mel-L1 <= 1e-3 on the decoder (bf16 weight rounding alone costs ~1.3e-2). */
+#define STZS_CONV_W_F32 64
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------
@@ -235,7 +241,7 @@ typedef struct stzs_dwup_args {
     const float* w;   /* [C][3] */
     const float* wb;  /* [C] */
     int64_t ldx, bsx, ldy, bsy, stat_bs, gb_bs, gb_beta_off;
-    int32_t B, T, C, pad_i;
+    int32_t B, T, C, dtype; /* dtype of x and y: STZS_BF16 | STZS_F32 */
     float slope, pad_f;
 } stzs_dwup_args;
 int stzs_adain_dwup(const stzs_dwup_args* a, void* stream);
@@ -250,6 +256,7 @@ typedef struct stzs_f0n_args {
     void* y1;
     int64_t ldf, ldy0, bsy0, ldy1, bsy1;
     int32_t B, T80, cf0, cn0, cf1, cn1;
+    int32_t dtype, pad_i; /* dtype of y0 / y1: STZS_BF16 | STZS_F32 */
 } stzs_f0n_args;
 int stzs_f0n_down(const stzs_f0n_args* a, void* stream);
 
@@ -266,6 +273,7 @@ typedef struct stzs_source_args {
     int64_t ldf, ldh, bsh;
     int32_t B, T80, hop, n_fft, hop_s, nh;
     float sr, sine_amp, noise_std, voiced_thr;
+    int32_t har_dtype, pad_i; /* dtype of har: STZS_BF16 | STZS_F32 */
 } stzs_source_args;
 int stzs_harmonic_source(const stzs_source_args* a, void* stream);
 

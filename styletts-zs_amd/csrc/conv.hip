@@ -664,6 +664,99 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     finish<TOut, true, BTM>(a, acc, smem, 0, 0, row0);
 }
 
+// PRECISE (parity) mode, STZS_CONV_W_F32: fp32 operands on v_mfma_f32_16x16x4_f32 (products exact in
+// fp32, fp32 accumulate), libm-accurate prologue (act_apply).  Same 128 x 128 tile, 2 x 2 waves and
+// accumulator layout as conv_mfma (the 16x16 C/D map is dtype-independent on gfx950), so the whole
+// fused epilogue (finish) is shared.  Per 32-channel input chunk the tile rows (+ halo) are staged once
+// in fp32; per tap one [128 co][32 ci] fp32 weight K-step goes through LDS.  The 16-B fragment reads keep
+// conv_mfma's k geometry: lane l holds k = 8 (l >> 4) + j of its row/column, and MFMA j sums the four k
+// values {8 h + j}; A and B use the same map, so the eight MFMAs of a K-step cover all 32 k exactly once.
+// Not a performance path: it exists so the decoder can be run at fp32 accuracy against the oracle.
+constexpr int P32 = 36;  // fp32 LDS row pitch (32 + 4 floats)
+template <typename TIn, typename TOut>
+__global__ __launch_bounds__(NTHR, 1) void conv_f32(const stzs_conv_args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int ks = a.ks;
+    const int rows_in = (BT - 1) * a.stride + (ks - 1) * a.dil + 1;
+    float* xin = reinterpret_cast<float*>(smem);
+    float* wl = xin + rows_in * P32;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wt = wave >> 1, wc = wave & 1;
+    const int tpb = (a.T_out + BT - 1) / BT;
+    const int bq = blockIdx.x / tpb;
+    const int t0 = (blockIdx.x - bq * tpb) * BT;
+    const int nchunk = a.ci_pad / 32;
+    const float* Wt = reinterpret_cast<const float*>(a.w) + (long)blockIdx.y * nchunk * ks * (BCO * 32);
+    const TIn* X = reinterpret_cast<const TIn*>(a.x) + (long)bq * a.bsx;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int cc = 0; cc < nchunk; ++cc) {
+        __syncthreads();
+        for (int v = tid; v < rows_in * 4; v += NTHR) {
+            const int r = v >> 2, cv = v & 3;
+            const int ci = cc * 32 + cv * 8;
+            const int tin = t0 * a.stride - a.pad + r;
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = 0.f;
+            if (tin >= 0 && tin < a.T_in && ci < a.Ci) {
+                float f[8];
+                load8(X + (long)tin * a.ldx + ci, f);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int c = ci + j;
+                    if (c >= a.Ci) break;
+                    float sc = a.pro_cscale, sh = 0.f;
+                    if (a.pro_mode == STZS_PRO_ADAIN) {
+                        const float mu = a.pro_mean[(long)bq * a.stat_bs + c];
+                        const float rs = a.pro_rstd[(long)bq * a.stat_bs + c];
+                        const float g = a.pro_gb[(long)bq * a.gb_bs + c];
+                        const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + c];
+                        sc = (1.f + g) * rs;
+                        sh = be - mu * sc;
+                    }
+                    o[j] = act_apply(a.pro_act, f[j] * sc + sh, a.pro_slope, a.pro_alpha ? a.pro_alpha[c] : 1.f);
+                }
+            }
+            float* d = xin + r * P32 + cv * 8;
+            *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<float4*>(d + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        }
+        for (int tap = 0; tap < ks; ++tap) {
+            __syncthreads();  // staged rows visible; previous weight K-step consumed
+            const float* src = Wt + (long)(cc * ks + tap) * (BCO * 32);
+            for (int e = tid * 4; e < BCO * 32; e += NTHR * 4)
+                *reinterpret_cast<float4*>(wl + (e >> 5) * P32 + (e & 31)) = *reinterpret_cast<const float4*>(src + e);
+            __syncthreads();
+            const int kb = 8 * (lane >> 4);
+            float av[4][8], bv[4][8];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const float* p = xin + ((wt * 64 + mt * 16 + (lane & 15)) * a.stride + tap * a.dil) * P32 + kb;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) av[mt][j] = p[j];
+            }
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const float* p = wl + (wc * 64 + nt * 16 + (lane & 15)) * P32 + kb;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bv[nt][j] = p[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt][j], bv[nt][j], acc[mt][nt], 0, 0, 0);
+        }
+    }
+    finish<TOut, false, BT>(a, acc, smem, bq, t0, 0);
+}
+
 size_t lds_bytes(int rows_in, int cic) {
     const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + NSLOT * SLOT_BYTES + 4 * 128 * 4;
     const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
@@ -759,6 +852,26 @@ extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
         if (a->out_dtype == STZS_BF16) return launch_dt<f8_t, bf16_t, true>(*a, s);
         if (a->out_dtype == STZS_F32) return launch_dt<f8_t, float, true>(*a, s);
         return STZS_EDTYPE;
+    }
+    if (a->flags & STZS_CONV_W_F32) {
+        if (a->cic != 32 || a->ci_pad % 32 || (a->flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32)))
+            return STZS_EINVAL;
+        const int rows_in = (BT - 1) * a->stride + (a->ks - 1) * a->dil + 1;
+        const size_t main = (size_t)(rows_in + BCO) * P32 * 4;
+        const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
+        const size_t lds = main > epi ? main : epi;
+        if (lds > 160 * 1024) return STZS_ESHAPE;
+        void (*k)(stzs_conv_args) = nullptr;
+        if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32) k = conv_f32<float, float>;
+        else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_BF16) k = conv_f32<float, bf16_t>;
+        else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) k = conv_f32<bf16_t, float>;
+        else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) k = conv_f32<bf16_t, bf16_t>;
+        else return STZS_EDTYPE;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        dim3 grid((unsigned)a->B * (unsigned)((a->T_out + BT - 1) / BT), a->co_pad / BCO);
+        hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, *a);
+        STZS_LAUNCH_CHECK();
+        return STZS_OK;
     }
     if (a->flags & STZS_CONV_W_LANE16) return stzs_mrf_conv_launch(*a, s);
     if (a->flags & STZS_CONV_W_NARROW32) return stzs_narrow_conv_launch(*a, s);

@@ -111,6 +111,7 @@ __global__ __launch_bounds__(256) void dwup_kernel(const stzs_dwup_args a) {
     }
 }
 
+template <typename TO>
 __global__ __launch_bounds__(256) void f0n_kernel(const stzs_f0n_args a) {
     const int T40 = a.T80 / 2;
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -126,13 +127,13 @@ __global__ __launch_bounds__(256) void f0n_kernel(const stzs_f0n_args a) {
             on += a.wn[j] * Np[s];
         }
     }
-    bf16_t* Y0 = reinterpret_cast<bf16_t*>(a.y0) + (long)b * a.bsy0 + (long)t * a.ldy0;
-    Y0[a.cf0] = f2bf(of);
-    Y0[a.cn0] = f2bf(on);
+    TO* Y0 = reinterpret_cast<TO*>(a.y0) + (long)b * a.bsy0 + (long)t * a.ldy0;
+    DT<TO>::st(Y0 + a.cf0, of);
+    DT<TO>::st(Y0 + a.cn0, on);
     if (a.y1) {
-        bf16_t* Y1 = reinterpret_cast<bf16_t*>(a.y1) + (long)b * a.bsy1 + (long)t * a.ldy1;
-        Y1[a.cf1] = f2bf(of);
-        Y1[a.cn1] = f2bf(on);
+        TO* Y1 = reinterpret_cast<TO*>(a.y1) + (long)b * a.bsy1 + (long)t * a.ldy1;
+        DT<TO>::st(Y1 + a.cf1, of);
+        DT<TO>::st(Y1 + a.cn1, on);
     }
 }
 
@@ -183,8 +184,13 @@ extern "C" int stzs_gather_rows(const stzs_gather_args* a, void* stream) {
 extern "C" int stzs_adain_dwup(const stzs_dwup_args* a, void* stream) {
     if (!a || !a->x || !a->y || !a->mean || !a->rstd || !a->gb || !a->w || !a->wb) return STZS_EINVAL;
     if (a->B <= 0 || a->T <= 0 || a->C <= 0) return STZS_ESHAPE;
-    hipLaunchKernelGGL(dwup_kernel<bf16_t>, dim3(2 * a->T, a->B), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), *a);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (a->dtype == STZS_BF16)
+        hipLaunchKernelGGL(dwup_kernel<bf16_t>, dim3(2 * a->T, a->B), dim3(256), 0, s, *a);
+    else if (a->dtype == STZS_F32)
+        hipLaunchKernelGGL(dwup_kernel<float>, dim3(2 * a->T, a->B), dim3(256), 0, s, *a);
+    else
+        return STZS_EDTYPE;
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }
@@ -193,8 +199,13 @@ extern "C" int stzs_f0n_down(const stzs_f0n_args* a, void* stream) {
     if (!a || !a->f0 || !a->n || !a->wf || !a->wn || !a->y0) return STZS_EINVAL;
     if (a->B <= 0 || a->T80 <= 0 || a->T80 % 2) return STZS_ESHAPE;
     const long n = (long)a->B * (a->T80 / 2);
-    hipLaunchKernelGGL(f0n_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), *a);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (a->dtype == STZS_BF16)
+        hipLaunchKernelGGL(f0n_kernel<bf16_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, *a);
+    else if (a->dtype == STZS_F32)
+        hipLaunchKernelGGL(f0n_kernel<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, *a);
+    else
+        return STZS_EDTYPE;
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

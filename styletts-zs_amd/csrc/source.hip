@@ -135,7 +135,9 @@ __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args
     const int f = f0i + tid;
     if (tid < FB && f < Tf) {
         const float* s = sbuf + tid * hs;
+        const bool f32 = a.har_dtype == STZS_F32;
         bf16_t* Hh = reinterpret_cast<bf16_t*>(a.har) + (long)b * a.bsh + (long)f * a.ldh;
+        float* Hf = reinterpret_cast<float*>(a.har) + (long)b * a.bsh + (long)f * a.ldh;
         for (int kb = 0; kb < nb; ++kb) {
             float re = 0.f, im = 0.f;
             for (int i = 0; i < nfft; ++i) {
@@ -144,10 +146,18 @@ __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args
                 re += x * twc[m];
                 im -= x * tws[m];
             }
-            Hh[kb] = f2bf(re);
-            Hh[nb + kb] = f2bf(im);
+            if (f32) {
+                Hf[kb] = re;
+                Hf[nb + kb] = im;
+            } else {
+                Hh[kb] = f2bf(re);
+                Hh[nb + kb] = f2bf(im);
+            }
         }
-        for (int c = 2 * nb; c < a.ldh; ++c) Hh[c] = 0;
+        for (int c = 2 * nb; c < a.ldh; ++c) {
+            if (f32) Hf[c] = 0.f;
+            else Hh[c] = 0;
+        }
     }
 }
 
@@ -158,6 +168,7 @@ extern "C" int stzs_harmonic_source(const stzs_source_args* a, void* stream) {
     if (a->B <= 0 || a->T80 <= 0 || a->nh <= 0 || a->nh > 64 || a->n_fft <= 0 || a->n_fft > 64 || a->hop_s <= 0)
         return STZS_ESHAPE;
     if (a->ldh < 2 * (a->n_fft / 2 + 1)) return STZS_ESHAPE;
+    if (a->har_dtype != STZS_BF16 && a->har_dtype != STZS_F32) return STZS_EDTYPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int n = a->B * a->nh;
     hipLaunchKernelGGL(phase_prefix_kernel, dim3((n + 63) / 64), dim3(64), 0, s, *a);

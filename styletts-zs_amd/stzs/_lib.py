@@ -19,6 +19,7 @@ PRO_NONE, PRO_ADAIN = 0, 1
 CONV_STAT_ROWS = 64  # include/stzs.h STZS_CONV_STAT_ROWS
 CONV_W_LANE16 = 16  # include/stzs.h STZS_CONV_W_LANE16
 CONV_W_NARROW32 = 32  # include/stzs.h STZS_CONV_W_NARROW32
+CONV_W_F32 = 64  # include/stzs.h STZS_CONV_W_F32 (precise mode)
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -91,20 +92,21 @@ class GatherArgs(C.Structure):
 class DwupArgs(C.Structure):
     _fields_ = [(n, vp) for n in ("x", "y", "mean", "rstd", "gb", "w", "wb")] + \
                [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy", "stat_bs", "gb_bs", "gb_beta_off")] + \
-               [("B", i32), ("T", i32), ("C", i32), ("pad_i", i32), ("slope", f32), ("pad_f", f32)]
+               [("B", i32), ("T", i32), ("C", i32), ("dtype", i32), ("slope", f32), ("pad_f", f32)]
 
 
 class F0nArgs(C.Structure):
     _fields_ = [(n, vp) for n in ("f0", "n", "wf", "wn", "y0", "y1")] + \
                [(n, i64) for n in ("ldf", "ldy0", "bsy0", "ldy1", "bsy1")] + \
-               [(n, i32) for n in ("B", "T80", "cf0", "cn0", "cf1", "cn1")]
+               [(n, i32) for n in ("B", "T80", "cf0", "cn0", "cf1", "cn1", "dtype", "pad_i")]
 
 
 class SourceArgs(C.Structure):
     _fields_ = [(n, vp) for n in ("f0", "seeds", "merge_w", "prefix", "har")] + \
                [(n, i64) for n in ("ldf", "ldh", "bsh")] + \
                [(n, i32) for n in ("B", "T80", "hop", "n_fft", "hop_s", "nh")] + \
-               [(n, f32) for n in ("sr", "sine_amp", "noise_std", "voiced_thr")]
+               [(n, f32) for n in ("sr", "sine_amp", "noise_std", "voiced_thr")] + \
+               [("har_dtype", i32), ("pad_i", i32)]
 
 
 class IstftArgs(C.Structure):

@@ -103,15 +103,20 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 
 
 class StyleTTSZS:
-    def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False):
+    def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False):
         """fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
-        per-row activation / per-column weight scales (configs[4]); bf16 otherwise."""
+        per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
+        precise_decoder: PARITY mode -- the decoder (pre-blocks, generator, conv_post) keeps fp32 activations
+        and runs every conv on fp32 MFMA operands (STZS_CONV_W_F32) to meet the north-star mel-L1 <= 1e-3 vs
+        the fp32 oracle; slower, not the benchmark path (bf16 weights alone cost ~1.3e-2)."""
         self.spec = spec
         self.fp8_denoiser = fp8_denoiser
+        self.precise = precise_decoder
+        self.dec_dt = torch.float32 if precise_decoder else torch.bfloat16
         self.device = torch.device(device)
         self.lib = L.load()
         L.check(self.lib.stzs_init(self.device.index or 0), "stzs_init")
-        self.W = PackedModel(spec, params, self.device, fill=fill)
+        self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder)
         # hosted front end (log-mel + prompt encoder), fp32 torch on the device
         self.fe = {k: v.to(self.device).float() for k, v in params.items() if k.startswith("pe.")}
         self.mel_fb = mel_filterbank(spec.n_mels, spec.mel_nfft, spec.sr).to(self.device)
@@ -190,9 +195,12 @@ class StyleTTSZS:
                 and cscale == 1.0 and x.t.dtype in (torch.bfloat16, torch.float8_e4m3fn)
                 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
-        if getattr(cw, "lane16", False):
+        if cw.w32 is not None:  # precise mode: fp32 operands on fp32 MFMA (csrc/conv.hip conv_f32)
+            a.w, a.cic = self._t(cw.w32).data_ptr(), 32
+            flags = (flags & ~8) | L.CONV_W_F32
+        elif getattr(cw, "lane16", False):
             flags |= L.CONV_W_LANE16  # MRF-family kernel (csrc/mrf.hip)
-        if getattr(cw, "narrow32", False):
+        elif getattr(cw, "narrow32", False):
             flags |= L.CONV_W_NARROW32  # narrow conv (csrc/mrf.hip)
         a.flags = flags
         st = None
@@ -549,8 +557,13 @@ class StyleTTSZS:
         self._call(self.lib.stzs_alignment, a, "alignment")
         en = self.act("pr.en", B, T40, pin)
         self.gather(d, idx, en, pin)
-        enc_in = self.act("dec.enc_in", B, T40, S.d_txt + 2)
-        self.gather(h_txt, idx, enc_in, S.d_txt)
+        enc_in = self.act("dec.enc_in", B, T40, S.d_txt + 2, self.dec_dt)
+        if self.precise:  # gather the bf16 rows, then widen into the fp32 decoder input
+            e16 = self.act("dec.enc_in16", B, T40, S.d_txt)
+            self.gather(h_txt, idx, e16, S.d_txt)
+            self.copy2d(e16, enc_in, T40, S.d_txt)
+        else:
+            self.gather(h_txt, idx, enc_in, S.d_txt)
         xs = self.act("pr.xs", B, T40, S.pr_hid)
         self.lstm(W.pr_shared, en, xs, "pr.shared")
         sg = self.mean_rows(codes, S.style_ac, S.style_pr, "pr.sg")
@@ -579,7 +592,7 @@ class StyleTTSZS:
         a.B, a.Tsrc, a.Tdst, a.C, a.xc0, a.yc0, a.dtype = x.B, x.T, y.T, Cn, x.c0, y.c0, x.dt
         self._call(self.lib.stzs_gather_rows, a, "gather")
 
-    def blk(self, bw, x: Act, out: Act, ng, gb: torch.Tensor, key):
+    def blk(self, bw, x: Act, out: Act, ng, gb: torch.Tensor, key, dt=torch.bfloat16):
         """AdainResBlk1d: out = (conv2(act(AdaIN(conv1(up(act(AdaIN(x))))))) + sc(x)) / sqrt 2."""
         B, T = x.B, x.T
         off1, c1 = ng.offsets[bw.name + ".norm1"]
@@ -587,14 +600,14 @@ class StyleTTSZS:
         gbase, gbs = gb.data_ptr(), ng.total
         m1, r1, sb1 = self.stats(x, key + ".s1")
         To = 2 * T if bw.up else T
-        r = self.act(key + ".r", B, To, bw.dout)
+        r = self.act(key + ".r", B, To, bw.dout, dt)
         if bw.up:
-            u = self.act(key + ".u", B, To, bw.din)
+            u = self.act(key + ".u", B, To, bw.din, dt)
             a = L.DwupArgs()
             a.x, a.y, a.mean, a.rstd, a.gb = x.ptr, u.ptr, m1.data_ptr(), r1.data_ptr(), gbase + off1 * 4
             a.w, a.wb = self.W.t(bw.pool_w).data_ptr(), self.W.t(bw.pool_b).data_ptr()
             a.ldx, a.bsx, a.ldy, a.bsy, a.stat_bs, a.gb_bs, a.gb_beta_off = x.ld, x.bs, u.ld, u.bs, sb1, gbs, c1
-            a.B, a.T, a.C, a.slope = B, T, bw.din, 0.2
+            a.B, a.T, a.C, a.slope, a.dtype = B, T, bw.din, 0.2, x.dt
             self._call(self.lib.stzs_adain_dwup, a, key + ".dwup")
             _, (m2, r2, sb2) = self.conv(bw.conv1, u, r, pad=1, stats_key=key + ".s2", what=key + ".conv1")
         else:
@@ -602,7 +615,7 @@ class StyleTTSZS:
                                          pro_act=L.ACT_LEAKY, pro_slope=0.2, stats_key=key + ".s2",
                                          what=key + ".conv1")
         if bw.sc is not None:
-            scb = self.act(key + ".sc", B, T, bw.dout)
+            scb = self.act(key + ".sc", B, T, bw.dout, dt)
             self.conv(bw.sc, x, scb, what=key + ".sc")
             res = scb
         else:
@@ -622,7 +635,8 @@ class StyleTTSZS:
         gbd = self.buf("dec.gbn", (B, ng.total), torch.float32)
         self.conv(ng.lin, Act(sa[:, None]), Act(gbd[:, None]), what="dec.norms")
         dcat = S.dec_enc + 2 + S.dec_asr_res
-        cats = [self.act("dec.catA", B, T40, dcat), self.act("dec.catB", B, T40, dcat)]
+        dt = self.dec_dt
+        cats = [self.act("dec.catA", B, T40, dcat, dt), self.act("dec.catB", B, T40, dcat, dt)]
         cF, cN = S.dec_enc + S.dec_asr_res, S.dec_enc + S.dec_asr_res + 1
         for j, cat in enumerate(cats):
             a = L.F0nArgs()
@@ -630,17 +644,19 @@ class StyleTTSZS:
             a.wf, a.wn = W.t(W.dec_f0).data_ptr(), W.t(W.dec_n).data_ptr()
             a.y0, a.y1 = cat.t.data_ptr(), (enc_in.t.data_ptr() if j == 0 else None)
             a.ldf, a.ldy0, a.bsy0, a.ldy1, a.bsy1 = F0.stride(0), cat.ld, cat.bs, enc_in.ld, enc_in.bs
-            a.B, a.T80, a.cf0, a.cn0, a.cf1, a.cn1 = B, T80, cF, cN, S.d_txt, S.d_txt + 1
+            a.B, a.T80, a.cf0, a.cn0, a.cf1, a.cn1, a.dtype = B, T80, cF, cN, S.d_txt, S.d_txt + 1, cat.dt
+            assert enc_in.t.dtype == cat.t.dtype
             self._call(self.lib.stzs_f0n_down, a, "f0n_down")
             self.conv(W.dec_asr_res, Act(enc_in.t, 0, S.d_txt), cat.sl(S.dec_enc, S.dec_asr_res), what="asr_res")
-        self.blk(W.dec_blk["dec.encode"], Act(enc_in.t, 0, S.d_txt + 2), cats[0].sl(0, S.dec_enc), ng, gbd, "dec.encode")
+        self.blk(W.dec_blk["dec.encode"], Act(enc_in.t, 0, S.d_txt + 2), cats[0].sl(0, S.dec_enc), ng, gbd, "dec.encode",
+                 dt)
         src = 0
         for i in range(3):
             self.blk(W.dec_blk[f"dec.decode{i}"], Act(cats[src].t, 0, dcat), cats[1 - src].sl(0, S.dec_enc), ng, gbd,
-                     f"dec.decode{i}")
+                     f"dec.decode{i}", dt)
             src = 1 - src
-        gen_in = self.act("dec.gen_in", B, T80, S.dec_out)
-        self.blk(W.dec_blk["dec.decode3"], Act(cats[src].t, 0, dcat), gen_in, ng, gbd, "dec.decode3")
+        gen_in = self.act("dec.gen_in", B, T80, S.dec_out, dt)
+        self.blk(W.dec_blk["dec.decode3"], Act(cats[src].t, 0, dcat), gen_in, ng, gbd, "dec.decode3", dt)
         return self.generator(gen_in, F0, seeds, gbd, istft=istft)
 
     def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None, istft=True):
@@ -660,13 +676,15 @@ class StyleTTSZS:
                 sd = self._consts[skey] = host.to(self.device)
         pref = self.buf("gen.pref", (B, nh, T80), torch.float32)
         # row pitch = the noise convs' padded K (32): the 1x1 noise conv then takes the LDS-DMA GEMM path
-        har = Act(self.buf("gen.har", (B, Tf, _rup(S.har_ch, 32)), zero=True), 0, S.har_ch)
+        dt = self.dec_dt
+        har = Act(self.buf("gen.har", (B, Tf, _rup(S.har_ch, 32)), dt, zero=True), 0, S.har_ch)
         a = L.SourceArgs()
         a.f0, a.seeds, a.merge_w, a.prefix, a.har = F0.data_ptr(), sd.data_ptr(), W.t(W.src_merge).data_ptr(), \
             pref.data_ptr(), har.ptr
         a.ldf, a.ldh, a.bsh = F0.stride(0), har.ld, har.bs
         a.B, a.T80, a.hop, a.n_fft, a.hop_s, a.nh = B, T80, S.hop, S.n_fft, S.istft_hop, nh
         a.sr, a.sine_amp, a.noise_std, a.voiced_thr = float(S.sr), S.sine_amp, S.noise_std, S.voiced_threshold
+        a.har_dtype = har.dt
         self._call(self.lib.stzs_harmonic_source, a, "harmonic_source")
         if trace is not None:
             trace["har"] = har
@@ -676,14 +694,14 @@ class StyleTTSZS:
             c = S.gen_ch[i]
             last = i == n_up - 1
             Tn = Tcur * r + (1 if last else 0)
-            xsrc = self.act(f"gen.xsrc{i}", B, Tn, c)
+            xsrc = self.act(f"gen.xsrc{i}", B, Tn, c, dt)
             if not last:
                 sf0 = int(np.prod(S.up_rates[i + 1:]))
                 self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, stride=sf0, pad=(sf0 + 1) // 2,
                           what=f"noise_conv{i}")
             else:
                 self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, what=f"noise_conv{i}")
-            xu = self.act(f"gen.x{i}", B, Tn, c)
+            xu = self.act(f"gen.x{i}", B, Tn, c, dt)
             self.conv(W.ups[i], x, xu, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=(k - r) // 2, T_final=Tcur * r,
                       refl=1 if last else 0, res=xsrc, what=f"ups{i}")
             if trace is not None:
@@ -744,10 +762,11 @@ class StyleTTSZS:
         S, W = self.spec, self.W
         B, T, c = x.B, x.T, x.C
         gbase, gbs = gbd.data_ptr(), ng.total
-        xs = self.act(f"gen.xs{i}", B, T, c)
-        bufA = self.act(f"gen.ba{i}", B, T, c)
-        bufB = self.act(f"gen.bb{i}", B, T, c)
-        t1 = self.act(f"gen.t1_{i}", B, T, c)
+        dt = x.t.dtype
+        xs = self.act(f"gen.xs{i}", B, T, c, dt)
+        bufA = self.act(f"gen.ba{i}", B, T, c, dt)
+        bufB = self.act(f"gen.bb{i}", B, T, c, dt)
+        t1 = self.act(f"gen.t1_{i}", B, T, c, dt)
         mx, rx, sb = self.stats(x, f"gen.sx{i}")
         nk = len(S.rb_kernels)
         for j, res in enumerate(W.rb[i]):

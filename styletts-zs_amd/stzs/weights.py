@@ -45,6 +45,7 @@ class ConvW:
     narrow32: bool = False  # [NK][32][32] narrow packing (STZS_CONV_W_NARROW32)
     wscale: Optional[object] = None  # fp8 linears: per-output-column fp32 scale [co_pad]
     f8: bool = False
+    w32: Optional[object] = None  # precise mode: fp32 K-step stream (STZS_CONV_W_F32), unpermuted
 
 
 class Arena:
@@ -106,6 +107,14 @@ def kstep_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
     return t.reshape(ncot, nchunk * ks * kpc, 128, 32).contiguous()
 
 
+def kstep_stream_f32(wp: torch.Tensor) -> torch.Tensor:
+    """[ks, co_pad, ci_pad] fp32 -> [co_pad/128, ci_pad/32, ks, 128, 32]: the precise-mode conv's K-steps
+    (csrc/conv.hip conv_f32) in its loop order (32-channel chunk, tap), natural row / channel order."""
+    ks, co_pad, ci_pad = wp.shape
+    t = wp.float().view(ks, co_pad // 128, 128, ci_pad // 32, 32).permute(1, 3, 0, 2, 4)
+    return t.contiguous()
+
+
 def lane16_perm() -> torch.Tensor:
     """packed row rr = wc*64 + nt*16 + g*4 + r of a 128-column tile holds output channel
     wc*64 + g*16 + nt*4 + r: the MRF kernel's swapped-operand accumulators then give each lane 16
@@ -129,9 +138,10 @@ def narrow32_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
     return t.reshape(nchunk * ks * kpc, 32, 32).contiguous()
 
 
-def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False) -> ConvW:
+def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f32=False) -> ConvW:
     """w: Conv1d [Co, Ci, k] / Linear [Co, Ci] / ConvTranspose1d [Ci, Co, 2*ups] (ups > 0).
-    lane16: the MRF kernel's layout (Ci % 128 == 0, Co % 16 == 0, plain conv)."""
+    lane16: the MRF kernel's layout (Ci % 128 == 0, Co % 16 == 0, plain conv).
+    f32: also pack the precise-mode fp32 stream (ConvW.w32)."""
     if ups:
         Ci, Co, k = w.shape
         assert k == 2 * ups
@@ -152,18 +162,19 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False) ->
     co_pad = _rup(ncol, 128)
     wp = torch.zeros(ks, co_pad, ci_pad)
     wp[:, :ncol, :Ci] = wk
+    w32 = A.add(name + ".w32", kstep_stream_f32(wp)) if f32 else None
     if narrow32:
         assert not ups and cic == 128 and Co <= 32, (name, Ci, Co)
         wn = A.add(name + ".wpk", narrow32_stream(wp[:, :32], cic).to(torch.bfloat16))
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True)
+        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True, w32=w32)
     if lane16:
         assert cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, perm].reshape(ks, co_pad, ci_pad)
     wn = A.add(name + ".wpk", kstep_stream(wp, cic).to(torch.bfloat16))
     bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16)
+    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16, w32=w32)
 
 
 def quantize_f8_cols(w: torch.Tensor):
@@ -212,7 +223,7 @@ class NormGroup:
     total: int
 
 
-def pack_norm_group(A: Arena, name, P, norm_names, style_dim) -> NormGroup:
+def pack_norm_group(A: Arena, name, P, norm_names, style_dim, f32=False) -> NormGroup:
     ws, bs, offs, off = [], [], {}, 0
     for n in norm_names:
         w, b = P[n + ".w"], P[n + ".b"]
@@ -222,7 +233,7 @@ def pack_norm_group(A: Arena, name, P, norm_names, style_dim) -> NormGroup:
         bs.append(b)
     W = torch.cat(ws, 0)
     Bv = torch.cat(bs, 0)
-    return NormGroup(pack_conv(A, name, W, Bv), offs, off)
+    return NormGroup(pack_conv(A, name, W, Bv, f32=f32), offs, off)
 
 
 @dataclass
@@ -273,11 +284,11 @@ def _lane16_ok(w) -> bool:
     return Ci > 64 and Co % 16 == 0
 
 
-def pack_blk(A: Arena, P, name, up=False) -> BlkW:
+def pack_blk(A: Arena, P, name, up=False, f32=False) -> BlkW:
     w1, w2 = P[name + ".conv1.w"], P[name + ".conv2.w"]
-    c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1))
-    c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2))
-    sc = pack_conv(A, name + ".sc", P[name + ".sc.w"]) if name + ".sc.w" in P else None
+    c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1), f32=f32)
+    c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2), f32=f32)
+    sc = pack_conv(A, name + ".sc", P[name + ".sc.w"], f32=f32) if name + ".sc.w" in P else None
     pw = pb = None
     if up:
         pw = A.add(name + ".poolw", P[name + ".pool.w"].reshape(-1, 3).float())
@@ -290,8 +301,10 @@ def pack_blk(A: Arena, P, name, up=False) -> BlkW:
 class PackedModel:
     """All hot-path weights of spec v0 in kernel layouts, resident in one device arena."""
 
-    def __init__(self, spec: Spec, P, device, fill=True):
+    def __init__(self, spec: Spec, P, device, fill=True, precise=False):
+        """precise: also pack fp32 streams of every decoder conv (StyleTTSZS(precise_decoder=True))."""
         S = self.spec = spec
+        f32 = precise
         A = self.arena = Arena()
         d = S.dn_d
         # --- text encoder ---
@@ -344,20 +357,21 @@ class PackedModel:
         # --- decoder ---
         self.dec_f0 = A.add("dec.f0c", torch.cat([P["dec.f0_conv.w"].reshape(-1), P["dec.f0_conv.b"]]).float())
         self.dec_n = A.add("dec.nc", torch.cat([P["dec.n_conv.w"].reshape(-1), P["dec.n_conv.b"]]).float())
-        self.dec_asr_res = pack_conv(A, "dec.asr_res", P["dec.asr_res.w"], P["dec.asr_res.b"])
+        self.dec_asr_res = pack_conv(A, "dec.asr_res", P["dec.asr_res.w"], P["dec.asr_res.b"], f32=f32)
         dec_norms = []
         self.dec_blk = {}
         for nm, up in [("dec.encode", False), ("dec.decode0", False), ("dec.decode1", False),
                        ("dec.decode2", False), ("dec.decode3", True)]:
-            self.dec_blk[nm] = pack_blk(A, P, nm, up=up)
+            self.dec_blk[nm] = pack_blk(A, P, nm, up=up, f32=f32)
             dec_norms += blk_norms(nm)
         self.src_merge = A.add("gen.src_merge", torch.cat([P["gen.src_merge.w"].reshape(-1), P["gen.src_merge.b"]]).float())
         self.noise_conv, self.ups, self.rb = [], [], []
         for i, (r, k) in enumerate(zip(S.up_rates, S.up_kernels)):
-            self.noise_conv.append(pack_conv(A, f"gen.noise_conv{i}", P[f"gen.noise_conv{i}.w"], P[f"gen.noise_conv{i}.b"]))
+            self.noise_conv.append(pack_conv(A, f"gen.noise_conv{i}", P[f"gen.noise_conv{i}.w"], P[f"gen.noise_conv{i}.b"],
+                                             f32=f32))
             wu = P[f"gen.ups{i}.w"]  # ConvTranspose1d [Ci, Co, 2r]
             self.ups.append(pack_conv(A, f"gen.ups{i}", wu, P[f"gen.ups{i}.b"], ups=r,
-                                      lane16=wu.shape[0] > 64 and wu.shape[1] % 16 == 0))
+                                      lane16=wu.shape[0] > 64 and wu.shape[1] % 16 == 0, f32=f32))
             stage = []
             for j, kr in enumerate(S.rb_kernels):
                 res = []
@@ -365,8 +379,8 @@ class PackedModel:
                     p = f"gen.rb{i}.{j}.{m}"
                     l16 = S.gen_ch[i] % 128 == 0 and (kr - 1) * dil <= 64  # persistent MRF kernel
                     res.append(dict(
-                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16),
-                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"], lane16=l16),
+                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16, f32=f32),
+                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"], lane16=l16, f32=f32),
                         a1=A.add(p + ".a1", P[p + ".alpha1"].float()), a2=A.add(p + ".a2", P[p + ".alpha2"].float()),
                         n1=p + ".n1", n2=p + ".n2", k=kr, dil=dil))
                     dec_norms += [p + ".n1", p + ".n2"]
@@ -374,8 +388,8 @@ class PackedModel:
             self.rb.append(stage)
         wpost = P["gen.conv_post.w"]
         self.conv_post = pack_conv(A, "gen.conv_post", wpost, P["gen.conv_post.b"],
-                                   narrow32=wpost.shape[1] > 64 and wpost.shape[0] <= 32)
-        self.dec_norm = pack_norm_group(A, "dec.norms", P, dec_norms, S.style_ac)
+                                   narrow32=wpost.shape[1] > 64 and wpost.shape[0] <= 32, f32=f32)
+        self.dec_norm = pack_norm_group(A, "dec.norms", P, dec_norms, S.style_ac, f32=f32)
         A.finalize(device, fill=fill)
         self.device = device
 

@@ -380,6 +380,7 @@ def test_harmonic_source_vs_oracle(eng, tiny_params):
     a.ldf, a.ldh, a.bsh = T80, 24, Tf * 24
     a.B, a.T80, a.hop, a.n_fft, a.hop_s, a.nh = B, T80, S.hop, S.n_fft, S.istft_hop, S.harmonic_num + 1
     a.sr, a.sine_amp, a.noise_std, a.voiced_thr = float(S.sr), S.sine_amp, S.noise_std, S.voiced_threshold
+    a.har_dtype = L.BF16
     eng._call(eng.lib.stzs_harmonic_source, a, "src")
     har = h.t[:, :, :22].float().cpu().transpose(1, 2)
     e = max_rel(har, ref)
