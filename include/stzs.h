@@ -307,6 +307,39 @@ int stzs_istft_stream(const stzs_istft_stream_args* a, void* stream);
 /* -> halo (>= 0) or a negative error; [*n0, *n1) = output samples of the chunk */
 int stzs_istft_stream_span(int f0, int Fc, int final_chunk, int n_fft, int hop_s, int64_t* n0, int64_t* n1);
 
+/* ---- reference-prompt front end (csrc/frontend.hip) -------------------------
+ * log-mel of the 3-s reference = stzs_stft_frames -> stzs_conv1d (bf16 DFT GEMM against the cos | -sin
+ * basis, fp32 out) -> stzs_log_mel; the prompt encoder's k5 convs run on stzs_conv1d, its adaptive
+ * average pooling on stzs_pool_rows. */
+/* y[b, t, m] = bf16(window[m] * x[reflect(t * hop + (n_fft - win) / 2 + m - n_fft / 2)]) for m < win,
+ * 0 for win <= m < ldy: the windowed STFT frames of torch.stft(center=True, pad_mode="reflect") */
+typedef struct stzs_frames_args {
+    const float* wav;      /* [B, ldw] f32, N samples each */
+    const float* window;   /* [win] f32 (periodic Hann) */
+    void* y;               /* [B, F, ldy] bf16, F = N / hop + 1 */
+    int64_t ldw, ldy, bsy;
+    int32_t B, N, F, n_fft, win, hop;
+} stzs_frames_args;
+int stzs_stft_frames(const stzs_frames_args* a, void* stream);
+/* y[b, t, m] = log(max(sum_{k0 <= k < k1} fb[m][k] (re_k^2 + im_k^2), 1e-5)), [k0, k1) = ranges[m] */
+typedef struct stzs_logmel_args {
+    const float* spec;     /* [B, F, lds] f32: nbin real parts | nbin imaginary parts */
+    const float* fb;       /* [n_mels][nbin] f32 mel filterbank */
+    const int32_t* ranges; /* [n_mels][2] nonzero bin range of each filter */
+    void* y;               /* [B, F, ldy] bf16 | f32 */
+    int64_t lds, bss, ldy, bsy;
+    int32_t B, F, nbin, n_mels, out_dtype, pad_i;
+} stzs_logmel_args;
+int stzs_log_mel(const stzs_logmel_args* a, void* stream);
+/* adaptive average pooling over time: y[b, i, c] = mean_{floor(iT/L) <= t < ceil((i+1)T/L)} x[b, t, c] */
+typedef struct stzs_pool_args {
+    const void* x;
+    void* y;
+    int64_t ldx, bsx, ldy, bsy;
+    int32_t B, T, L, C, in_dtype, out_dtype;
+} stzs_pool_args;
+int stzs_pool_rows(const stzs_pool_args* a, void* stream);
+
 /* ---- sampler glue ---- */
 /* c[r, j] = silu(pool[r, j] + temb[j]) -> bf16 */
 int stzs_dn_cond(const float* pool, const float* temb, void* c, int R, int D, void* stream);

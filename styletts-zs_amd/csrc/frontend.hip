@@ -1,0 +1,112 @@
+// Reference-prompt front end in HIP (log-mel + prompt encoder), so that a whole
+// synth() runs on libstzs_hip.so kernels only.  The oracle's restatement: oracle/stzs_ref.py prompt_encoder
+// (torch.stft center=True / reflect pad, periodic Hann window of win samples centred in n_fft, power,
+// HTK mel filterbank, log(clamp(., 1e-5)), two k5 convs + LeakyReLU(0.2), adaptive average pooling to L_s
+// rows, projection).
+//
+//   stzs_stft_frames : reflect-padded, windowed frames as bf16 GEMM rows [B, F, ldy] (HBM-bound copy);
+//                      the DFT itself is a bf16 MFMA GEMM through stzs_conv1d against a cos | -sin basis
+//                      (stzs/weights.py dft_basis), fp32 out;
+//   stzs_log_mel     : |X|^2 of the (re | im) rows, sparse mel filterbank (per-bin [k0, k1) ranges), log;
+//   stzs_pool_rows   : adaptive average pooling over time (torch.nn.functional.adaptive_avg_pool1d bounds).
+#include "common.hpp"
+
+namespace {
+
+__global__ __launch_bounds__(256) void frames_kernel(const stzs_frames_args a) {
+    const int t = blockIdx.x, b = blockIdx.y;
+    const float* X = a.wav + (long)b * a.ldw;
+    bf16_t* Y = reinterpret_cast<bf16_t*>(a.y) + (long)b * a.bsy + (long)t * a.ldy;
+    const int off = (a.n_fft - a.win) / 2;  // window centred in the n_fft frame
+    for (int m = threadIdx.x; m < a.ldy; m += 256) {
+        float v = 0.f;
+        if (m < a.win) {
+            long j = (long)t * a.hop + off + m - a.n_fft / 2;  // sample index before reflect padding
+            if (j < 0) j = -j;
+            if (j >= a.N) j = 2L * (a.N - 1) - j;
+            v = a.window[m] * X[j];
+        }
+        Y[m] = f2bf(v);
+    }
+}
+
+__global__ __launch_bounds__(256) void log_mel_kernel(const stzs_logmel_args a) {
+    extern __shared__ float pw[];
+    const long r = (long)blockIdx.y * a.F + blockIdx.x;  // b * F + t
+    const float* S = a.spec + (long)blockIdx.y * a.bss + (long)blockIdx.x * a.lds;
+    for (int k = threadIdx.x; k < a.nbin; k += 256) {
+        const float re = S[k], im = S[a.nbin + k];
+        pw[k] = re * re + im * im;
+    }
+    __syncthreads();
+    for (int m = threadIdx.x; m < a.n_mels; m += 256) {
+        const int k0 = a.ranges[2 * m], k1 = a.ranges[2 * m + 1];
+        const float* w = a.fb + (long)m * a.nbin;
+        float acc = 0.f;
+        for (int k = k0; k < k1; ++k) acc = fmaf(w[k], pw[k], acc);
+        const float v = logf(fmaxf(acc, 1e-5f));
+        const long o = (long)blockIdx.y * a.bsy + (long)blockIdx.x * a.ldy + m;
+        if (a.out_dtype == STZS_BF16) reinterpret_cast<bf16_t*>(a.y)[o] = f2bf(v);
+        else reinterpret_cast<float*>(a.y)[o] = v;
+    }
+    (void)r;
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void pool_kernel(const stzs_pool_args a) {
+    const int i = blockIdx.x, b = blockIdx.y;
+    const int s = (int)(((long)i * a.T) / a.L);
+    const int e = (int)(((long)(i + 1) * a.T + a.L - 1) / a.L);
+    const TI* X = reinterpret_cast<const TI*>(a.x) + (long)b * a.bsx;
+    TO* Y = reinterpret_cast<TO*>(a.y) + (long)b * a.bsy + (long)i * a.ldy;
+    const float inv = 1.f / (float)(e - s);
+    for (int c = threadIdx.x; c < a.C; c += 256) {
+        float acc = 0.f;
+        for (int t = s; t < e; ++t) acc += DT<TI>::ld(X + (long)t * a.ldx + c);
+        DT<TO>::st(Y + c, acc * inv);
+    }
+}
+
+}  // namespace
+
+extern "C" int stzs_stft_frames(const stzs_frames_args* a, void* stream) {
+    if (!a || !a->wav || !a->window || !a->y) return STZS_EINVAL;
+    if (a->B <= 0 || a->N < 2 || a->F <= 0 || a->hop <= 0 || a->win <= 0 || a->win > a->n_fft || a->ldy < a->win ||
+        a->ldy % 8 || a->n_fft / 2 >= a->N)
+        return STZS_ESHAPE;  // reflect padding needs N > n_fft / 2 (as torch)
+    if ((long)(a->F - 1) * a->hop > (long)a->N + a->n_fft) return STZS_ESHAPE;
+    hipLaunchKernelGGL(frames_kernel, dim3(a->F, a->B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), *a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_log_mel(const stzs_logmel_args* a, void* stream) {
+    if (!a || !a->spec || !a->y || !a->fb || !a->ranges) return STZS_EINVAL;
+    if (a->B <= 0 || a->F <= 0 || a->nbin <= 0 || a->nbin > 8192 || a->n_mels <= 0 || a->lds < 2 * a->nbin ||
+        a->ldy < a->n_mels)
+        return STZS_ESHAPE;
+    if (a->out_dtype != STZS_BF16 && a->out_dtype != STZS_F32) return STZS_EDTYPE;
+    hipLaunchKernelGGL(log_mel_kernel, dim3(a->F, a->B), dim3(256), (size_t)a->nbin * 4,
+                       reinterpret_cast<hipStream_t>(stream), *a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_pool_rows(const stzs_pool_args* a, void* stream) {
+    if (!a || !a->x || !a->y) return STZS_EINVAL;
+    if (a->B <= 0 || a->T <= 0 || a->L <= 0 || a->C <= 0) return STZS_ESHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    dim3 g(a->L, a->B);
+    if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16)
+        hipLaunchKernelGGL((pool_kernel<bf16_t, bf16_t>), g, dim3(256), 0, s, *a);
+    else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32)
+        hipLaunchKernelGGL((pool_kernel<bf16_t, float>), g, dim3(256), 0, s, *a);
+    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32)
+        hipLaunchKernelGGL((pool_kernel<float, float>), g, dim3(256), 0, s, *a);
+    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_BF16)
+        hipLaunchKernelGGL((pool_kernel<float, bf16_t>), g, dim3(256), 0, s, *a);
+    else
+        return STZS_EDTYPE;
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}

@@ -120,6 +120,22 @@ class IstftStreamArgs(C.Structure):
                 ("B", i32), ("f0", i32), ("Fc", i32), ("final_chunk", i32), ("n_fft", i32), ("hop_s", i32)]
 
 
+class FramesArgs(C.Structure):
+    _fields_ = [("wav", vp), ("window", vp), ("y", vp), ("ldw", i64), ("ldy", i64), ("bsy", i64)] + \
+               [(n, i32) for n in ("B", "N", "F", "n_fft", "win", "hop")]
+
+
+class LogMelArgs(C.Structure):
+    _fields_ = [("spec", vp), ("fb", vp), ("ranges", vp), ("y", vp)] + \
+               [(n, i64) for n in ("lds", "bss", "ldy", "bsy")] + \
+               [(n, i32) for n in ("B", "F", "nbin", "n_mels", "out_dtype", "pad_i")]
+
+
+class PoolArgs(C.Structure):
+    _fields_ = [("x", vp), ("y", vp)] + [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy")] + \
+               [(n, i32) for n in ("B", "T", "L", "C", "in_dtype", "out_dtype")]
+
+
 class CopyArgs(C.Structure):
     _fields_ = [("x", vp), ("y", vp)] + [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy")] + \
                [(n, i32) for n in ("B", "R", "C", "in_dtype", "out_dtype", "pad_i")]
@@ -130,6 +146,7 @@ EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_ch
            "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
+           "stzs_stft_frames", "stzs_log_mel", "stzs_pool_rows",
            "stzs_dn_cond", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed"]
 
@@ -173,7 +190,10 @@ def load():
         "stzs_istft": ([P(IstftArgs), vp], i32),
         "stzs_istft_stream": ([P(IstftStreamArgs), vp], i32),
         "stzs_istft_stream_span": ([i32, i32, i32, i32, i32, P(i64), P(i64)], i32),
-        "stzs_dn_cond": ([vp, vp, vp, i32, i32, vp], i32),
+        "stzs_stft_frames": ([P(FramesArgs), vp], i32),
+        "stzs_log_mel": ([P(LogMelArgs), vp], i32),
+        "stzs_pool_rows": ([P(PoolArgs), vp], i32),
+        "stzs_dn_cond":([vp, vp, vp, i32, i32, vp], i32),
         "stzs_adaln_expand": ([vp, vp, vp, i32, i32, i32, i32, C.c_uint32, vp], i32),
         "stzs_cfg_euler": ([vp, vp, i32, i32, i32, f32, f32, f32, vp], i32),
         "stzs_state_init": ([vp, vp, i32, i32, i32, f32, vp], i32),

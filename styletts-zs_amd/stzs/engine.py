@@ -10,10 +10,10 @@ API (the upstream inference API is "Under construction",
     pro   = eng.predict_prosody(h_txt, codes, durations)               # (b) duration/prosody
     wav   = eng.decode(pro, codes, seeds)                              # (c) iSTFT decoder
 
-Every hot-path FLOP runs in a hand-written gfx950 kernel reached through the C-ABI; PyTorch only
-provides device memory (caching allocator), the stream, and hosts the front ends that SURVEY §8(f)
-lists as "next" (log-mel + prompt encoder).  Buffers are cached per shape so a whole synth() can
-be captured into one HIP graph (`capture()`), which removes all host launch overhead.
+Every FLOP of synth() -- including the reference-prompt front end (log-mel + prompt encoder, SURVEY
+§8(f) rank 1) -- runs in a hand-written gfx950 kernel reached through the C-ABI; PyTorch only
+provides device memory (caching allocator) and the stream.  Buffers are cached per shape so a whole
+synth() can be captured into one HIP graph (`capture()`), which removes all host launch overhead.
 """
 from __future__ import annotations
 
@@ -23,10 +23,8 @@ from dataclasses import dataclass
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 from . import _lib as L
-from .frontend import log_mel, mel_filterbank
 from .spec import Spec
 from .weights import ConvW, PackedModel
 
@@ -117,9 +115,6 @@ class StyleTTSZS:
         self.lib = L.load()
         L.check(self.lib.stzs_init(self.device.index or 0), "stzs_init")
         self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder)
-        # hosted front end (log-mel + prompt encoder), fp32 torch on the device
-        self.fe = {k: v.to(self.device).float() for k, v in params.items() if k.startswith("pe.")}
-        self.mel_fb = mel_filterbank(spec.n_mels, spec.mel_nfft, spec.sr).to(self.device)
         self._bufs = {}
         self._consts = {}
         self._ws = None
@@ -342,15 +337,50 @@ class StyleTTSZS:
                        act=L.ACT_LEAKY, slope=0.2, what=f"te.ln{i}")
         return e
 
+    def log_mel(self, wav: torch.Tensor, dtype=torch.bfloat16) -> Act:
+        """reference wav fp32 [B, N] (device) -> log-mel [B, N/hop + 1, n_mels]:
+        windowed reflect-padded frames -> bf16 DFT GEMM on MFMA (cos | -sin basis, fp32 out) -> power, sparse
+        mel filterbank, log (csrc/frontend.hip)."""
+        S, W = self.spec, self.W
+        B, N = wav.shape
+        Fr = N // S.hop + 1
+        dft = W.fe_dft
+        frames = self.act("fe.frames", B, Fr, dft.ci_pad)
+        a = L.FramesArgs()
+        a.wav, a.window, a.y = wav.data_ptr(), W.t(W.fe_win).data_ptr(), frames.ptr
+        a.ldw, a.ldy, a.bsy = N, frames.ld, frames.bs
+        a.B, a.N, a.F, a.n_fft, a.win, a.hop = B, N, Fr, S.mel_nfft, S.mel_win, S.hop
+        self._call(self.lib.stzs_stft_frames, a, "stft_frames")
+        nbin = S.mel_nfft // 2 + 1
+        spec = self.act("fe.spec", B, Fr, 2 * nbin, torch.float32)
+        self.conv(dft, Act(frames.t, 0, S.mel_win), spec, what="fe.dft")
+        mel = self.act("fe.mel", B, Fr, S.n_mels, dtype)
+        a = L.LogMelArgs()
+        a.spec, a.fb, a.ranges, a.y = spec.ptr, W.t(W.fe_fb).data_ptr(), W.t(W.fe_rng).data_ptr(), mel.ptr
+        a.lds, a.bss, a.ldy, a.bsy = spec.ld, spec.bs, mel.ld, mel.bs
+        a.B, a.F, a.nbin, a.n_mels, a.out_dtype = B, Fr, nbin, S.n_mels, mel.dt
+        self._call(self.lib.stzs_log_mel, a, "log_mel")
+        return mel
+
     def prompt_encode(self, ref_wav: torch.Tensor) -> torch.Tensor:
-        """hosted front end (torch fp32): ref wav [B, N] -> codes [B, L_s, code]."""
-        S, P = self.spec, self.fe
-        mel = log_mel(ref_wav.float(), S, self.mel_fb)
-        x = F.leaky_relu(F.conv1d(mel, P["pe.conv0.w"], P["pe.conv0.b"], padding=2), 0.2)
-        x = F.leaky_relu(F.conv1d(x, P["pe.conv1.w"], P["pe.conv1.b"], padding=2), 0.2)
-        x = F.adaptive_avg_pool1d(x, S.L_s).transpose(1, 2)
-        out = self.buf("prompt", (x.shape[0], S.L_s, S.code_dim), torch.float32)
-        torch.addmm(P["pe.proj.b"], x.reshape(-1, x.shape[-1]), P["pe.proj.w"].t(), out=out.view(-1, S.code_dim))
+        """reference-prompt front end on HIP: ref wav [B, N] -> codes fp32 [B, L_s, code].
+        log-mel -> 2 x (k5 conv + LeakyReLU 0.2) -> adaptive average pool to L_s rows -> projection."""
+        S, W = self.spec, self.W
+        wav = ref_wav.to(self.device, torch.float32).contiguous()
+        B = wav.shape[0]
+        mel = self.log_mel(wav)
+        Fr = mel.T
+        c0 = self.act("fe.c0", B, Fr, S.pe_ch)
+        c1 = self.act("fe.c1", B, Fr, S.pe_ch)
+        self.conv(W.pe_conv0, mel, c0, pad=2, epi_act=L.ACT_LEAKY, epi_slope=0.2, what="pe.conv0")
+        self.conv(W.pe_conv1, c0, c1, pad=2, epi_act=L.ACT_LEAKY, epi_slope=0.2, what="pe.conv1")
+        pooled = self.act("fe.pool", B, S.L_s, S.pe_ch)
+        a = L.PoolArgs()
+        a.x, a.y, a.ldx, a.bsx, a.ldy, a.bsy = c1.ptr, pooled.ptr, c1.ld, c1.bs, pooled.ld, pooled.bs
+        a.B, a.T, a.L, a.C, a.in_dtype, a.out_dtype = B, Fr, S.L_s, S.pe_ch, L.BF16, L.BF16
+        self._call(self.lib.stzs_pool_rows, a, "pool_rows")
+        out = self.buf("prompt", (B, S.L_s, S.code_dim), torch.float32)
+        self.conv(W.pe_proj, pooled, Act(out), what="pe.proj")
         return out
 
     # ------------------------------------------------------------------ (a) style diffusion

@@ -21,6 +21,7 @@ from typing import Optional
 
 import torch
 
+from .frontend import mel_filterbank
 from .spec import Spec
 
 ALIGN = 256
@@ -215,6 +216,17 @@ def pack_conv_f8(A: Arena, name, w, b=None) -> ConvW:
     return ConvW(wn, bn, Ci, Co, 1, ci_pad, co_pad, 64, wscale=sn, f8=True)
 
 
+def dft_basis(n_fft: int, win: int) -> torch.Tensor:
+    """Linear [2 * nbin, win]: rows k < nbin = cos(2 pi k n / n_fft), rows nbin + k = -sin(...), n = (n_fft - win) / 2
+    + m the position of window sample m inside the frame -> (Re | Im) of the n_fft-point DFT of a windowed
+    frame (torch.stft's zero-padded centred window; the window itself is applied by stzs_stft_frames)."""
+    nbin = n_fft // 2 + 1
+    n = torch.arange(win, dtype=torch.float64) + (n_fft - win) // 2
+    k = torch.arange(nbin, dtype=torch.float64)[:, None]
+    ang = 2.0 * math.pi * ((k * n[None, :]) % n_fft) / n_fft
+    return torch.cat([torch.cos(ang), -torch.sin(ang)], 0).float()
+
+
 @dataclass
 class NormGroup:
     """all AdaIN fc layers of one stage, packed as one linear; offsets per norm name."""
@@ -311,6 +323,21 @@ class PackedModel:
         self.te_emb = A.add("te.emb", P["te.emb"].float())
         self.te_conv = [pack_conv(A, f"te.conv{i}", P[f"te.conv{i}.w"], P[f"te.conv{i}.b"]) for i in range(S.te_layers)]
         self.te_ln = [(A.add(f"te.ln{i}.g", P[f"te.ln{i}.g"]), A.add(f"te.ln{i}.b", P[f"te.ln{i}.b"])) for i in range(S.te_layers)]
+        # --- reference-prompt front end (csrc/frontend.hip): DFT basis, window, mel filterbank, encoder ---
+        self.fe_dft = pack_conv(A, "fe.dft", dft_basis(S.mel_nfft, S.mel_win))
+        self.fe_win = A.add("fe.win", torch.hann_window(S.mel_win).float())
+        fb = mel_filterbank(S.n_mels, S.mel_nfft, S.sr)
+        nz = fb > 0
+        rng = torch.zeros(S.n_mels, 2, dtype=torch.int32)
+        for m in range(S.n_mels):
+            idx = nz[m].nonzero()
+            if len(idx):
+                rng[m, 0], rng[m, 1] = int(idx[0]), int(idx[-1]) + 1
+        self.fe_fb = A.add("fe.fb", fb.contiguous())
+        self.fe_rng = A.add("fe.fbr", rng)
+        self.pe_conv0 = pack_conv(A, "pe.conv0", P["pe.conv0.w"], P["pe.conv0.b"])
+        self.pe_conv1 = pack_conv(A, "pe.conv1", P["pe.conv1.w"], P["pe.conv1.b"])
+        self.pe_proj = pack_conv(A, "pe.proj", P["pe.proj.w"], P["pe.proj.b"])
         # --- denoiser ---
         L = lambda n: pack_conv(A, n, P[n + ".w"], P[n + ".b"])
         self.dn_in = L("dn.in_proj")

@@ -49,7 +49,8 @@ STRUCTS = {
     "stzs_attn_args": "AttnArgs", "stzs_lstm_args": "LstmArgs", "stzs_prprep_args": "PrPrepArgs",
     "stzs_dur_args": "DurArgs", "stzs_align_args": "AlignArgs", "stzs_gather_args": "GatherArgs",
     "stzs_dwup_args": "DwupArgs", "stzs_f0n_args": "F0nArgs", "stzs_source_args": "SourceArgs",
-    "stzs_istft_args": "IstftArgs", "stzs_istft_stream_args": "IstftStreamArgs", "stzs_quant_args": "QuantArgs", "stzs_copy_args": "CopyArgs",
+    "stzs_istft_args": "IstftArgs", "stzs_istft_stream_args": "IstftStreamArgs", "stzs_quant_args": "QuantArgs", "stzs_frames_args": "FramesArgs",
+    "stzs_logmel_args": "LogMelArgs", "stzs_pool_args": "PoolArgs", "stzs_copy_args": "CopyArgs",
 }
 
 
