@@ -820,6 +820,15 @@ class StyleTTSZS:
         return xs
 
     # ------------------------------------------------------------------ end to end
+    def twin(self) -> "StyleTTSZS":
+        """a second engine on the SAME packed weights with its own buffer cache: two twins can synthesize
+        two utterance batches concurrently on two streams (their graphs replay side by side, so one batch's
+        latency-bound phases -- LSTM recurrences, statistics, small GEMMs -- overlap the other's convs)."""
+        t = object.__new__(StyleTTSZS)
+        t.__dict__.update(self.__dict__)
+        t._bufs, t._consts, t._ws, t.launches, t.timer = {}, {}, None, 0, None
+        return t
+
     def capture(self, fn):
         """Capture `fn()` into one HIP graph.  fn must be replay-safe: device-resident inputs, cached
         buffers (a warm-up call on a side stream allocates them), no host syncs.  -> (graph, fn's output)"""
