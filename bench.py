@@ -122,6 +122,7 @@ def main():
     ap.add_argument("--no-longform", action="store_true")
     ap.add_argument("--streams", type=int, default=2,
                     help="split the per-GPU batch over this many concurrently replayed graphs (engine twins)")
+    ap.add_argument("--stagger", type=int, default=1, help="start shard j > 0 one front phase late")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,40 +166,63 @@ def main():
             print(f"[bench] graph capture failed ({type(e).__name__}: {e}); eager", file=sys.stderr)
             graph = None
     run = graph.replay if graph is not None else step
-    nstream = args.streams if (graph is not None and args.streams > 1 and B % args.streams == 0) else 1
+    nstream = min(args.streams, B) if (graph is not None and args.streams > 1) else 1
     if nstream > 1:
-        # the batch as `nstream` equal shards on engine twins (shared weights, own buffers), one graph each,
-        # replayed side by side on their own streams: one shard's latency-bound phases (LSTM recurrences,
-        # statistics, small GEMMs) overlap another's convs.  Same total work per step.
-        b = B // nstream
-        graphs = []
+        # the batch as `nstream` (near-)equal shards on engine twins (shared weights, own buffers), each captured as
+        # two graphs -- front (text, prompt, style diffusion, prosody) and back (decoder) -- replayed on its
+        # own stream; shard j > 0 starts one front phase behind shard 0, so one shard's latency-bound front
+        # (LSTM recurrences, small GEMMs) runs beside another's decoder convs.  A step is still one front +
+        # one back of every shard (64 utterances per GPU); steps are not joined, the timed region ends with
+        # a synchronize after the last one.
+        sizes = [B // nstream + (1 if i < B % nstream else 0) for i in range(nstream)]
+        pairs = []
         for i in range(nstream):
             tw = eng.twin()
-            sl = slice(i * b, (i + 1) * b)
-            fn = (lambda tw=tw, sl=sl: tw.synth(tok_d[sl], ref_d[sl], steps=STEPS_THROUGHPUT, cfg_scale=CFG,
-                                                noise=eps_d[sl], durations=dur_d[sl], seeds=seeds[sl],
-                                                n_frames=n_frames))
-            fn()
-            graphs.append(tw.capture(fn)[0])
+            sl = slice(sum(sizes[:i]), sum(sizes[:i + 1]))
+            st_ = {}
+
+            def front(tw=tw, sl=sl, st_=st_):
+                h = tw.text_encode(tok_d[sl])
+                pr = tw.prompt_encode(ref_d[sl])
+                codes = tw.sample_style(h, pr, eps_d[sl], STEPS_THROUGHPUT, CFG)
+                st_["codes"], st_["pro"] = codes, tw.predict_prosody(h, codes, dur_d[sl], n_frames)
+
+            def back(tw=tw, sl=sl, st_=st_):
+                return tw.decode(st_["pro"], st_["codes"], seeds[sl])
+            front()
+            back()
+            ga = tw.capture(front)[0]
+            gb = tw.capture(back)[0]
+            pairs.append((ga, gb))
         streams = [torch.cuda.Stream(dev) for _ in range(nstream)]
 
-        def run():
+        def run_steps(k):
             cur = torch.cuda.current_stream(dev)
-            for st, g in zip(streams, graphs):
+            for st in streams:
                 st.wait_stream(cur)
-                with torch.cuda.stream(st):
-                    g.replay()
+            ev = torch.cuda.Event()
+            for i in range(k):
+                for j, (st, (ga, gb)) in enumerate(zip(streams, pairs)):
+                    with torch.cuda.stream(st):
+                        if i == 0 and j > 0 and args.stagger:
+                            st.wait_event(ev)
+                        ga.replay()
+                        if i == 0 and j == 0:
+                            ev.record(st)
+                        gb.replay()
             for st in streams:
                 cur.wait_stream(st)
-    for _ in range(args.warmup):
-        run()
+    else:
+        def run_steps(k):
+            for _ in range(k):
+                run()
+    run_steps(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
+    run_steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -284,7 +308,8 @@ def main():
             "data": "synthetic (seeded tokens 16/s, 3-s noise reference, forced [3,2] durations); random-init weights",
             "config": {"workload": "configs[2]: batch 64/GPU, 5-s targets, 2-step distilled style diffusion, CFG 5",
                        "global_batch": world * B, "seq_len": n_frames, "parallelism": f"dp{world} (utterance shards)",
-                       "spec": S.name, "graph": graph is not None, "streams": nstream},
+                       "spec": S.name, "graph": graph is not None, "streams": nstream,
+                       "stagger": bool(args.stagger and nstream > 1)},
             "audio_s_per_s_per_gpu": round(value / world, 2),
             "p50_latency_ms": lat["p50_ms"] if lat else None,
             "latency": lat,
