@@ -535,6 +535,21 @@ class StyleTTSZS:
     def predict_prosody(self, h_txt: Act, codes: torch.Tensor, durations=None, n_frames=None):
         """durations: optional int tensor [B, T_txt] (host or device); n_frames: their per-utterance sum if
         known (avoids the device->host sync, e.g. under graph capture).  Returns dict of device tensors."""
+        du = self.predict_durations(h_txt, codes, durations)
+        if n_frames is not None:
+            T40 = int(n_frames)
+        else:
+            if durations is not None and durations.device.type == "cpu":
+                tot = durations.to(torch.int64).sum(1)
+            else:
+                tot = du["dur"].to(torch.int64).sum(1).cpu()  # host sync: the frame count sizes every later buffer
+            assert int(tot.min()) == int(tot.max()), \
+                "one batch must share its total frame count (stzs.scheduler.BucketScheduler groups by it)"
+            T40 = int(tot[0])
+        return self.prosody_frames(h_txt, codes, du["d"], du["dur"], T40, du)
+
+    def predict_durations(self, h_txt: Act, codes: torch.Tensor, durations=None) -> dict:
+        """a5-a6: DurationEncoder + duration LSTM + head -> dict(dur int32 [B, T], dsum, logits, d) (device)."""
         S, W = self.spec, self.W
         B, T = h_txt.B, h_txt.T
         pin = S.pr_in
@@ -571,15 +586,14 @@ class StyleTTSZS:
             dur.data_ptr(), dsum.data_ptr()
         a.ldl, a.bsl, a.B, a.T, a.nbins = logits.ld, logits.bs, B, T, S.dur_bins
         self._call(self.lib.stzs_durations, a, "durations")
-        if n_frames is not None:
-            T40 = int(n_frames)
-        else:
-            if durations is not None and durations.device.type == "cpu":
-                tot = durations.to(torch.int64).sum(1)
-            else:
-                tot = dur.to(torch.int64).sum(1).cpu()  # host sync: the frame count sizes every later buffer
-            assert int(tot.min()) == int(tot.max()), "one batch must share its total frame count (§8(f) bucketing)"
-            T40 = int(tot[0])
+        return dict(dur=dur, dsum=dsum, logits=logits, d=d)
+
+    def prosody_frames(self, h_txt: Act, codes: torch.Tensor, d: Act, dur: torch.Tensor, T40: int,
+                       extra: dict = None) -> dict:
+        """a7-a8 for a batch sharing T40 aligned frames: alignment, gathers, shared LSTM, F0 / N curves."""
+        S, W = self.spec, self.W
+        B, T = h_txt.B, h_txt.T
+        pin = S.pr_in
         idx = self.buf("pr.idx", (B, T40), torch.int32)
         total = self.buf("pr.total", (B,), torch.int32)
         a = L.AlignArgs()
@@ -612,8 +626,8 @@ class StyleTTSZS:
             self.blk(W.pr_blk[f"pr.{br}1"], y0, y1, ng, gbp, f"pr.{br}1")
             self.blk(W.pr_blk[f"pr.{br}2"], y1, y2, ng, gbp, f"pr.{br}2")
             self.conv(W.pr_blk[f"pr.{br}_proj"], y2, Act(out, 0, 1), what=f"pr.{br}_proj")
-        return dict(dur=dur, dsum=dsum, logits=logits, idx=idx, T40=T40, en=en, asr_buf=enc_in, d=d,
-                    F0=F0[:, :, 0], N=Nn[:, :, 0])
+        out = dict(extra or {}, dur=dur, idx=idx, T40=T40, en=en, asr_buf=enc_in, d=d, F0=F0[:, :, 0], N=Nn[:, :, 0])
+        return out
 
     def gather(self, x: Act, idx, y: Act, Cn):
         a = L.GatherArgs()
