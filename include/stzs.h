@@ -343,6 +343,9 @@ int stzs_pool_rows(const stzs_pool_args* a, void* stream);
 /* ---- sampler glue ---- */
 /* c[r, j] = silu(pool[r, j] + temb[j]) -> bf16 */
 int stzs_dn_cond(const float* pool, const float* temb, void* c, int R, int D, void* stream);
+/* the same for every sampler step at once: c[s][r][j] = silu(pool[r][j] + temb[s][j]), s < steps (the
+ * step-invariant conditioning of a whole sampling run in one launch instead of one per NFE) */
+int stzs_dn_cond_steps(const float* pool, const float* temb, void* c, int R, int D, int steps, void* stream);
 /* out[l][r][j] = mod[r][j] + (table ? table[l][j] : 0) + ((j / D) in scale_mask ? 1 : 0) */
 int stzs_adaln_expand(const float* mod, const float* table, float* out, int R, int D, int nchunk,
                       int nlayers, unsigned scale_mask, void* stream);

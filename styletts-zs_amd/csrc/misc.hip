@@ -10,11 +10,15 @@
 
 namespace {
 
-__global__ void dn_cond_kernel(const float* pool, const float* temb, bf16_t* c, int R, int D) {
+// c[s][r][j] = silu(pool[r][j] + temb[s][j]) for all sampler steps s at once
+__global__ void dn_cond_kernel(const float* pool, const float* temb, bf16_t* c, int R, int D, int steps) {
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (long)R * D) return;
-    const int j = (int)(i % D);
-    const float x = pool[i] + temb[j];
+    const long rd = (long)R * D;
+    if (i >= rd * steps) return;
+    const int s = (int)(i / rd);
+    const long rj = i - s * rd;
+    const int j = (int)(rj % D);
+    const float x = pool[rj] + temb[(long)s * D + j];
     c[i] = f2bf(x / (1.f + expf(-x)));
 }
 
@@ -93,7 +97,17 @@ extern "C" int stzs_dn_cond(const float* pool, const float* temb, void* c, int R
     if (!pool || !temb || !c) return STZS_EINVAL;
     if (R <= 0 || D <= 0) return STZS_ESHAPE;
     hipLaunchKernelGGL(dn_cond_kernel, dim3(nblk((long)R * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                       pool, temb, reinterpret_cast<bf16_t*>(c), R, D);
+                       pool, temb, reinterpret_cast<bf16_t*>(c), R, D, 1);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_dn_cond_steps(const float* pool, const float* temb, void* c, int R, int D, int steps,
+                                  void* stream) {
+    if (!pool || !temb || !c) return STZS_EINVAL;
+    if (R <= 0 || D <= 0 || steps <= 0) return STZS_ESHAPE;
+    hipLaunchKernelGGL(dn_cond_kernel, dim3(nblk((long)R * D * steps)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), pool, temb, reinterpret_cast<bf16_t*>(c), R, D, steps);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

@@ -147,7 +147,7 @@ EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_ch
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
            "stzs_stft_frames", "stzs_log_mel", "stzs_pool_rows",
-           "stzs_dn_cond", "stzs_adaln_expand", "stzs_cfg_euler",
+           "stzs_dn_cond", "stzs_dn_cond_steps", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed"]
 
 _lib = None
@@ -193,6 +193,7 @@ def load():
         "stzs_stft_frames": ([P(FramesArgs), vp], i32),
         "stzs_log_mel": ([P(LogMelArgs), vp], i32),
         "stzs_pool_rows": ([P(PoolArgs), vp], i32),
+        "stzs_dn_cond_steps": ([vp, vp, vp, i32, i32, i32, vp], i32),
         "stzs_dn_cond":([vp, vp, vp, i32, i32, vp], i32),
         "stzs_adaln_expand": ([vp, vp, vp, i32, i32, i32, i32, C.c_uint32, vp], i32),
         "stzs_cfg_euler": ([vp, vp, i32, i32, i32, f32, f32, f32, vp], i32),

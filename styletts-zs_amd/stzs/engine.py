@@ -149,7 +149,7 @@ class StyleTTSZS:
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
-             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, what="conv"):
+             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
         output fused into the conv epilogue (per-tile partials) + one small finalize launch."""
         W = self.W
@@ -220,6 +220,8 @@ class StyleTTSZS:
             tm["rec"].append((what, e0, e1, flops, byt))
         else:
             self._call(self.lib.stzs_conv1d, a, what)
+        if post_ln is not None:  # the LayerNorm that consumes this linear's output (stzs_rowln_args)
+            self._call(self.lib.stzs_row_layernorm, post_ln, what + ".ln")
         if st is None:
             return y
         slab, Cc, mean, rstd = st
@@ -438,11 +440,23 @@ class StyleTTSZS:
         self.launches += 1
         L.check(self.lib.stzs_state_init(x.data_ptr(), eps.data_ptr(), B, N, int(cfg), float(sig[0]), self.stream()),
                 "state_init")
-        cb = self.buf("dn.cb", (R, d), torch.bfloat16)
-        mod = self.buf("dn.mod", (R, 6 * d), torch.float32)
-        fmod = self.buf("dn.fmod", (R, 2 * d), torch.float32)
-        modx = self.buf("dn.modx", (S.dn_layers, R, 6 * d), torch.float32)
-        fmodx = self.buf("dn.fmodx", (1, R, 2 * d), torch.float32)
+        # step-invariant conditioning of the whole run, all steps at once (rows s * R + r): adaLN-single
+        # input, its two projections and the per-layer expansion -> 5 launches total instead of 5 per NFE
+        cb = self.buf("dn.cb", (steps * R, d), torch.bfloat16)
+        mod = self.buf("dn.mod", (steps * R, 6 * d), torch.float32)
+        fmod = self.buf("dn.fmod", (steps * R, 2 * d), torch.float32)
+        modx = self.buf("dn.modx", (S.dn_layers, steps * R, 6 * d), torch.float32)
+        fmodx = self.buf("dn.fmodx", (1, steps * R, 2 * d), torch.float32)
+        self.launches += 1
+        L.check(self.lib.stzs_dn_cond_steps(pool.data_ptr(), temb.t.data_ptr(), cb.data_ptr(), R, d, steps,
+                                            self.stream()), "dn_cond_steps")
+        self.conv(W.dn_ada, Act(cb[:, None]), Act(mod[:, None]), what="dn.ada")
+        self.conv(W.dn_final_ada, Act(cb[:, None]), Act(fmod[:, None]), what="dn.final_ada")
+        self.launches += 2
+        L.check(self.lib.stzs_adaln_expand(mod.data_ptr(), W.t(W.dn_table).data_ptr(), modx.data_ptr(), steps * R, d,
+                                           6, S.dn_layers, 0b010010, self.stream()), "adaln_expand")
+        L.check(self.lib.stzs_adaln_expand(fmod.data_ptr(), None, fmodx.data_ptr(), steps * R, d, 2, 1, 0b10,
+                                           self.stream()), "adaln_expand.f")
         h = self.act("dn.h", R, Ls, d, torch.float32)
         an = self.act("dn.a", R, Ls, d)
         qkv = self.act("dn.qkv", R, Ls, 3 * d)
@@ -464,63 +478,62 @@ class StyleTTSZS:
         for i in range(steps):
             s0 = sig[i]
             co = edm_coeffs(S, s0)
-            self.launches += 1
-            L.check(self.lib.stzs_dn_cond(pool.data_ptr(), temb.t.data_ptr() + i * d * fsz, cb.data_ptr(), R, d,
-                                          self.stream()), "dn_cond")
-            self.conv(W.dn_ada, Act(cb[:, None]), Act(mod[:, None]), what="dn.ada")
-            self.conv(W.dn_final_ada, Act(cb[:, None]), Act(fmod[:, None]), what="dn.final_ada")
-            self.launches += 2
-            L.check(self.lib.stzs_adaln_expand(mod.data_ptr(), W.t(W.dn_table).data_ptr(), modx.data_ptr(), R, d, 6,
-                                               S.dn_layers, 0b010010, self.stream()), "adaln_expand")
-            L.check(self.lib.stzs_adaln_expand(fmod.data_ptr(), None, fmodx.data_ptr(), R, d, 2, 1, 0b10,
-                                               self.stream()), "adaln_expand.f")
             self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, what="dn.in")
+            if f8:
+                ain, sin, sfx = an8, s_an, "8"
+            else:
+                ain, sin, sfx = an, None, ""
+            # adaLN / LayerNorm rows of this step: ln1_l, ca_ln_l, ln2_l for every layer, then lnf; each one
+            # after the first is launched right behind the residual linear that produces its input (post_ln).
+            # (Fusing them into that linear's epilogue -- last-arriving tile of a row block, sc1 hand-off --
+            # was tried: bit-identical but 1.6x slower at batch 1, the block's rows then normalise on one CU.)
+            lns = []
             for l, lw in enumerate(W.dn_layers):
-                mb = modx[l].data_ptr()
-                if f8:
-                    self._dn_layer_f8(lw, mb, h, an8, s_an, qkv, o, o8, s_o, q, ff, ff8, s_ff, kv[l], Ls, d, fsz)
-                    continue
-                self.rowln(h, an, G=mb + d * fsz, gs=6 * d, Bt=mb, bs=6 * d, gdiv=Ls, gadd=0.0, what="ln1")
-                self.conv(lw["qkv"], an, qkv, what="qkv")
+                mb = modx[l, i * R].data_ptr()  # this step's rows of layer l's modulation
+                lns.append(self._ln_args(h, ain, G=mb + d * fsz, gs=6 * d, Bt=mb, bs=6 * d, gdiv=Ls, y_scale=sin))
+                lns.append(self._ln_args(h, ain, G=W.t(lw["ln_g"]).data_ptr(), Bt=W.t(lw["ln_b"]).data_ptr(),
+                                         y_scale=sin))
+                lns.append(self._ln_args(h, ain, G=mb + 4 * d * fsz, gs=6 * d, Bt=mb + 3 * d * fsz, bs=6 * d, gdiv=Ls,
+                                         y_scale=sin))
+            fb = fmodx[0, i * R].data_ptr()
+            lns.append(self._ln_args(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls))
+            self._call(self.lib.stzs_row_layernorm, lns[0], "ln1")
+            for l, lw in enumerate(W.dn_layers):
+                mb = modx[l, i * R].data_ptr()
+                self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, what="qkv")
                 self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
-                self.conv(lw["o"], o, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, what="sa_o")
-                self.rowln(h, an, G=W.t(lw["ln_g"]).data_ptr(), gs=0, Bt=W.t(lw["ln_b"]).data_ptr(), bs=0,
-                           gadd=0.0, what="ca_ln")
-                self.conv(lw["q"], an, q, what="ca_q")
+                xo, so = (o8, s_o) if f8 else (o, None)
+                if f8:
+                    self.quant(o, o8, s_o)
+                self.conv(lw["o" + sfx], xo, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=so,
+                          post_ln=lns[3 * l + 1], what="sa_o")
+                self.conv(lw["q" + sfx], ain, q, x_scale=sin, what="ca_q")
                 self.attention(q, kv[l].sl(0, d), kv[l].sl(d, d), o)
-                self.conv(lw["co"], o, h, res=h, what="ca_o")
-                self.rowln(h, an, G=mb + 4 * d * fsz, gs=6 * d, Bt=mb + 3 * d * fsz, bs=6 * d, gdiv=Ls, gadd=0.0,
-                           what="ln2")
-                self.conv(lw["ff1"], an, ff, epi_act=L.ACT_GELU, what="ff1")
-                self.conv(lw["ff2"], ff, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, what="ff2")
-            fb = fmodx.data_ptr()
-            self.rowln(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls, gadd=0.0, what="lnf")
+                if f8:
+                    self.quant(o, o8, s_o)
+                self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=lns[3 * l + 2], what="ca_o")
+                self.conv(lw["ff1" + sfx], ain, ff, epi_act=L.ACT_GELU, x_scale=sin, what="ff1")
+                xf, sf = (ff8, s_ff) if f8 else (ff, None)
+                if f8:
+                    self.quant(ff, ff8, s_ff)
+                self.conv(lw["ff2" + sfx], xf, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=sf,
+                          post_ln=lns[3 * l + 3], what="ff2")
             self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], what="dn.out")
             self.launches += 1
             L.check(self.lib.stzs_cfg_euler(x.data_ptr(), D.t.data_ptr(), B, N, int(cfg), float(cfg_scale),
                                             float(s0), float(sig[i + 1] - s0), self.stream()), "cfg_euler")
         return x[:B]
 
-    def _dn_layer_f8(self, lw, mb, h, an8, s_an, qkv, o, o8, s_o, q, ff, ff8, s_ff, kv, Ls, d, fsz):
-        """one denoiser layer with e4m3fn linears: the adaLN / LayerNorm rows are quantised by the norm
-        kernel itself (one scale per row), attention outputs and the GELU rows by stzs_quant_rows."""
-        W = self.W
-        self.rowln(h, an8, G=mb + d * fsz, gs=6 * d, Bt=mb, bs=6 * d, gdiv=Ls, gadd=0.0, y_scale=s_an, what="ln1")
-        self.conv(lw["qkv8"], an8, qkv, x_scale=s_an, what="qkv")
-        self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
-        self.quant(o, o8, s_o)
-        self.conv(lw["o8"], o8, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=s_o, what="sa_o")
-        self.rowln(h, an8, G=W.t(lw["ln_g"]).data_ptr(), gs=0, Bt=W.t(lw["ln_b"]).data_ptr(), bs=0, gadd=0.0,
-                   y_scale=s_an, what="ca_ln")
-        self.conv(lw["q8"], an8, q, x_scale=s_an, what="ca_q")
-        self.attention(q, kv.sl(0, d), kv.sl(d, d), o)
-        self.quant(o, o8, s_o)
-        self.conv(lw["co8"], o8, h, res=h, x_scale=s_o, what="ca_o")
-        self.rowln(h, an8, G=mb + 4 * d * fsz, gs=6 * d, Bt=mb + 3 * d * fsz, bs=6 * d, gdiv=Ls, gadd=0.0,
-                   y_scale=s_an, what="ln2")
-        self.conv(lw["ff18"], an8, ff, epi_act=L.ACT_GELU, x_scale=s_an, what="ff1")
-        self.quant(ff, ff8, s_ff)
-        self.conv(lw["ff28"], ff8, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=s_ff, what="ff2")
+    def _ln_args(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=0.0, y_scale=None):
+        """stzs_rowln_args of a modulated LayerNorm x -> y (launched by stzs_row_layernorm, or fused into a
+        GEMM epilogue as stzs_conv_args.post_ln)."""
+        a = L.RowLNArgs()
+        a.x, a.y, a.G, a.Bt = x.ptr, y.ptr, G, Bt
+        a.ldx, a.ldy, a.gs, a.bs = x.ld, y.ld, gs, bs
+        a.R, a.C, a.gdiv, a.in_dtype, a.out_dtype, a.act = x.B * x.T, x.C, gdiv, x.dt, y.dt, L.ACT_NONE
+        a.gadd, a.eps, a.slope = gadd, 1e-5, 0.0
+        a.y_scale = y_scale.data_ptr() if y_scale is not None else None
+        return a
 
     def _conv_rows(self, cw, x: Act, dst: torch.Tensor, b0, t0, what):
         """linear over x [B, T, C] written to dst[b0 + b, t0 + t, :] (dst rows have a larger T)."""

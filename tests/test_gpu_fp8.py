@@ -158,3 +158,4 @@ def test_sample_style_fp8_vs_oracle(gpu_device, spec):
         print(f"fp8 sampler {spec} steps={steps} cfg={cfg}: rel-L2 {e:.3e}")
         assert torch.isfinite(got).all()
         assert e < tol
+

@@ -1,0 +1,30 @@
+"""configs[1] latency probe: batch 1, 10-step CFG-5, 5-s target, graph-replayed N times (for rocprofv3)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts-zs_amd")]
+import torch  # noqa: E402
+
+from bench import CFG, STEPS_LATENCY, make_inputs  # noqa: E402
+from stzs.engine import StyleTTSZS  # noqa: E402
+from stzs.params import init_params  # noqa: E402
+from stzs.spec import SPEC_V0 as S  # noqa: E402
+
+eng = StyleTTSZS(S, init_params(S, 0), device="cuda:0")
+tok, ref, eps, dur = (t.cuda() for t in make_inputs(S, 1, 1000))
+nf = int(dur[0].sum())
+one = lambda: eng.synth(tok, ref, steps=STEPS_LATENCY, cfg_scale=CFG, noise=eps, durations=dur, seeds=[7], n_frames=nf)
+one()
+g, _ = eng.capture(one)
+n = int(os.environ.get("N", 20))
+ts = []
+for _ in range(n):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    ts.append((time.perf_counter() - t0) * 1e3)
+ts.sort()
+print(f"latency p50 {ts[len(ts) // 2]:.3f} ms  min {ts[0]:.3f}  launches/synth {eng.launches // 2}")
