@@ -38,3 +38,34 @@ for n in (1, 100):
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / 20
     print(f"graph of {n} dependent tiny launches: {el * 1e6:.1f} us per replay, {el * 1e6 / n:.2f} us per launch")
+
+# two independent chains captured on two streams: do graph branches run concurrently on replay?
+x2 = torch.randn(1, 50, 256, device="cuda:0")
+y2 = torch.empty(1, 256, device="cuda:0")
+side = torch.cuda.Stream()
+
+
+def chain2(n):
+    cur = torch.cuda.current_stream()
+    side.wait_stream(cur)
+    s = C.c_void_p(cur.cuda_stream)
+    s2 = C.c_void_p(side.cuda_stream)
+    for _ in range(n):
+        L.check(lib.stzs_mean_rows(x.data_ptr(), y.data_ptr(), 1, 50, 256, 50 * 256, 0, 256, 256, s))
+        L.check(lib.stzs_mean_rows(x2.data_ptr(), y2.data_ptr(), 1, 50, 256, 50 * 256, 0, 256, 256, s2))
+    cur.wait_stream(side)
+
+
+chain2(100)
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    chain2(100)
+g.replay()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(20):
+    g.replay()
+torch.cuda.synchronize()
+el = (time.perf_counter() - t0) / 20
+print(f"graph of 2 x 100 launches on two captured streams: {el * 1e6:.1f} us per replay")
