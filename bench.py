@@ -243,6 +243,10 @@ def main():
     bsum = sum(r[3] for r in rec)
     nl = max(len(rec), 1)
     achieved = (fsum / nl) / (tsum / nl) / 1e12 if tsum > 0 else 0.0
+    # per launch t_roof = max(F / P_mfma, B_alg / BW_hbm); aggregate = sum t_roof / sum t_meas
+    # (the k3 convs are HBM-bound at 128 channels, the k7 / k11 ones MFMA-bound)
+    t_roof = sum(max(r[2] / (PEAK_BF16_TFLOPS * 1e12), r[3] / (PEAK_HBM_GBS * 1e9)) for r in rec)
+    n_hbm = sum(1 for r in rec if r[3] / (PEAK_HBM_GBS * 1e9) > r[2] / (PEAK_BF16_TFLOPS * 1e12))
     # HBM bytes per launch from the committed PMC passes of this workload (tools/pmc_bench.sh)
     traffic, tsrc = None, None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_mrf.json")
@@ -254,6 +258,7 @@ def main():
                 alg_bytes_per_launch=round(bsum / nl),
                 kernel="mrf_conv (generator MRF convs)", launches=len(rec),
                 avg_launch_us=round(tsum / nl * 1e6, 2), alg_gflop_per_launch=round(fsum / nl / 1e9, 3),
+                time_frac=round(t_roof / tsum, 4) if tsum > 0 else None, hbm_bound_launches=n_hbm,
                 alg_hbm_gbs=round(bsum / tsum / 1e9, 1) if tsum > 0 else None)
 
     # ---- p50 latency, configs[1]: batch 1, 10-step CFG-5 ----
