@@ -120,6 +120,13 @@ class StyleTTSZS:
         self._ws = None
         self.launches = 0
 
+    @classmethod
+    def from_checkpoint(cls, path: str, device="cuda:0", **kw) -> "StyleTTSZS":
+        """engine on the parameters of a safetensors checkpoint (stzs/checkpoint.py), spec from its metadata."""
+        from .checkpoint import load_params
+        params, spec = load_params(path)
+        return cls(spec, params, device=device, **kw)
+
     # ------------------------------------------------------------------ plumbing
     def stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

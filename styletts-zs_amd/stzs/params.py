@@ -76,8 +76,29 @@ class _Init:
             self.conv(name + ".sc", dout, din, 1, bias=False)
 
 
+class _Shapes(_Init):
+    """declares every parameter as a meta tensor (shape only, no values, no generator draws)"""
+
+    def uni(self, name, shape, bound):
+        self.p[name] = torch.empty(shape, device="meta")
+
+    def nrm(self, name, shape, std, mean=0.0):
+        self.p[name] = torch.empty(shape, device="meta")
+
+    def const(self, name, shape, v):
+        self.p[name] = torch.empty(shape, device="meta")
+
+
 def init_params(spec: Spec, seed: int = 0) -> "OrderedDict[str, torch.Tensor]":
-    I = _Init(seed)
+    return _declare(_Init(seed), spec)
+
+
+def param_shapes(spec: Spec) -> "OrderedDict[str, torch.Size]":
+    """name -> shape of every parameter of `spec`, in declaration order (checkpoint validation)."""
+    return OrderedDict((k, v.shape) for k, v in _declare(_Shapes(0), spec).items())
+
+
+def _declare(I: _Init, spec: Spec) -> "OrderedDict[str, torch.Tensor]":
     S = spec
     sty = S.style_ac
     # ---- text encoder (front end; StyleTTS2 TextEncoder CNN part) ----
