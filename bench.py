@@ -110,6 +110,30 @@ def longform(S, P, dev, runs=7):
                 realtime_factor=round(30.0 / (float(np.percentile(total, 50)) * 1e-3), 1))
 
 
+def precise_mode(S, P, dev, B=16, steps=5):
+    """throughput of the precise decoder mode (fp32 activations + fp32-MFMA convs, the mode that meets the
+    north-star mel-L1 <= 1e-3: tests/test_gpu_precise.py), same workload shape at batch 16, graph-replayed."""
+    from stzs.engine import StyleTTSZS
+    ep = StyleTTSZS(S, P, device=dev, precise_decoder=True)
+    tok, ref, eps, dur = (t.to(dev) for t in make_inputs(S, B, 7))
+    nf = int(dur[0].sum())
+    fn = lambda: ep.synth(tok, ref, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps, durations=dur,
+                          seeds=list(range(B)), n_frames=nf)
+    fn()
+    g, _ = ep.capture(fn)
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    del g, ep
+    torch.cuda.empty_cache()
+    return dict(config=f"batch {B}, 5-s targets, 2-step CFG-5, fp32 decoder (precise mode)",
+                audio_s_per_s=round(B * TARGET_S / el, 1), ms_per_step=round(el * 1e3, 2))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +144,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-longform", action="store_true")
+    ap.add_argument("--no-precise", action="store_true")
     ap.add_argument("--streams", type=int, default=2,
                     help="split the per-GPU batch over this many concurrently replayed graphs (engine twins)")
     ap.add_argument("--stagger", type=int, default=1, help="start shard j > 0 one front phase late")
@@ -292,6 +317,9 @@ def main():
     lf = None
     if not args.no_longform and world == 1:
         lf = longform(S, P, dev)
+    pr = None
+    if not args.no_precise and world == 1:
+        pr = precise_mode(S, P, dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -322,6 +350,7 @@ def main():
             "cpu_baseline": cpu,
             "weight_broadcast_ms": round(bcast_ms, 3),
             "longform": lf,
+            "precise_decoder": pr,
         }
         print(json.dumps(line))
     if world > 1:

@@ -115,14 +115,17 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
             const int base = ((s - 1) & 1) * MROWS * H * 2;
             constexpr int NWT = MROWS * NKS * 32 / 8;          // 16-B words of h (H = 32 NKS)
             constexpr int NW = (NWT + 511) / 512;              // per thread
+            // only the group's valid rows (a batch-1 group moves 1/64 of the slab); rows >= nrows of the A
+            // tile stay as zeroed at s = 0 and only feed gate rows no cell reads
+            const int nwt = nrows * (NKS * 32 / 8);
             u32x4 v[NW];
 #pragma unroll
-            for (int i = 0; i < NW; ++i)  // (NWT % 512 == 0 at H >= 64; the clamp keeps H = 32 in bounds)
-                v[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + ((tid + i * 512) % NWT) * 16, 0, 16);
+            for (int i = 0; i < NW; ++i)  // uniform guard; the modulo keeps every address inside the rows
+                if (i * 512 < nwt) v[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + ((tid + i * 512) % nwt) * 16, 0, 16);
 #pragma unroll
             for (int i = 0; i < NW; ++i) {
                 const int e = tid + i * 512, r = (e * 8) / H, k = (e * 8) - r * H;
-                if (e < NWT) *reinterpret_cast<u32x4*>(As + r * hp + k) = v[i];
+                if (e < nwt) *reinterpret_cast<u32x4*>(As + r * hp + k) = v[i];
             }
         }
         __syncthreads();
