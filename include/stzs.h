@@ -91,7 +91,7 @@ typedef struct stzs_conv_args {
 #define STZS_CONV_STAT_ROWS 64
 /* flags bit: weights packed with the 16-lane channel permutation of the MRF kernel (stzs/weights.py
  * pack_conv(lane16=True)): inside each 128-column tile, packed row wc*64 + nt*16 + g*4 + r holds
- * output channel wc*64 + g*16 + nt*4 + r.  Selects the persistent MRF conv (csrc/mrf.hip): Snake
+ * output channel wc*64 + g*16 + nt*4 + r.  Selects the MRF conv (csrc/mrf.hip): AdaIN + Snake / LeakyReLU
  * prologue, bf16 in/out, Ci % 128 == 0, Co % 16 == 0, stride 1, no gate/ups/epilogue activation. */
 #define STZS_CONV_W_LANE16 16
 /* flags bit: narrow weights (Co <= 32) packed as [NK][32][32] K-steps with packed row nt*16 + g*4 + r
@@ -105,6 +105,9 @@ typedef struct stzs_conv_args {
  * conv feature except the fp8 path.  Used by StyleTTSZS(precise_decoder=True) to meet the north-star
  * mel-L1 <= 1e-3 on the decoder (bf16 weight rounding alone costs ~1.3e-2). */
 #define STZS_CONV_W_F32 64
+/* flags bit (diagnostic): keep the dispatcher's linear workgroup order on the LANE16 / NARROW32 kernels
+ * instead of the XCD-aware remap (neighbouring time tiles on one L2); results are identical either way. */
+#define STZS_CONV_LINEAR_IDS 128
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------

@@ -25,6 +25,15 @@ STZS_DEV uint32_t pack2bf(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
 
+// XCD-aware bijective remap of a linear workgroup id: the dispatcher deals ids round-robin over the 8 XCDs
+// (id % 8 labels the blocks that share an L2), so give each such group a CONTIGUOUS range of tiles --
+// neighbouring time tiles then share their dilation halos (and weight K-steps) in one L2.  Speed only: any
+// bijection is correct (cdna_hip_programming.md T1, bijective form for nwg % 8 != 0).
+STZS_DEV int xcd_remap(int bid, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
 template <typename T> struct DT;
 template <> struct DT<float> {
     static STZS_DEV float ld(const float* p) { return *p; }

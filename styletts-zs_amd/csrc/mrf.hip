@@ -54,11 +54,15 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
     const int tpb = (a.T_out + BT - 1) / BT;
-    const int bq = blockIdx.x / tpb;
-    const int t0 = (blockIdx.x - bq * tpb) * BT;
+    const int nx = gridDim.x;
+    const int lin = (a.flags & STZS_CONV_LINEAR_IDS) ? blockIdx.y * nx + blockIdx.x
+                                                      : xcd_remap(blockIdx.y * nx + blockIdx.x, nx * gridDim.y);
+    const int by = lin / nx, bx = lin - by * nx;  // (co tile, utterance x time tile)
+    const int bq = bx / tpb;
+    const int t0 = (bx - bq * tpb) * BT;
     const int nchunk = a.ci_pad >> 7;
     const int NK = nchunk * ks * 4;
-    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
+    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)by * NK * (BCO * 32);
     auto fill = [&](int k) {  // k >= NK: a harmless re-copy (clamped source) into a retired slot
         const bf16_t* src = Wt + (long)(k < NK ? k : NK - 1) * (BCO * 32) + wave * 1024 + lane * 8;
         unsigned char* dst = ring + (k & (NSL - 1)) * SLOT + wave * 2048;
@@ -231,7 +235,7 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
     // Co + channel (a 16-channel group never straddles phases, Co % 16 == 0): t = q*ups + p - ups_pad,
     // valid in [0, T_final), shifted by refl (ReflectionPad(1,0)).
     const int gq = lane >> 4, n = lane & 15;
-    const int co0 = blockIdx.y * BCO + wc * 64 + gq * 16;
+    const int co0 = by * BCO + wc * 64 + gq * 16;
     const int ph = a.ups > 0 ? co0 / a.Co : 0;
     const bool col_ok = a.ups > 0 ? co0 < a.ups * a.Co : co0 < a.Co;
     const int cof = col_ok ? co0 - ph * a.Co : 0;  // channel of this lane group's first value
@@ -380,8 +384,9 @@ __global__ __launch_bounds__(NTH, 2) void narrow_conv(const stzs_conv_args a) {
     unsigned char* ring = smem + ((rows_in * P + 15) & ~15);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tpb = (a.T_out + NBT - 1) / NBT;
-    const int bq = blockIdx.x / tpb;
-    const int t0 = (blockIdx.x - bq * tpb) * NBT;
+    const int bx = (a.flags & STZS_CONV_LINEAR_IDS) ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+    const int bq = bx / tpb;
+    const int t0 = (bx - bq * tpb) * NBT;
     const int nchunk = a.ci_pad >> 7;
     const int NK = nchunk * ks * 4;
     const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w);

@@ -20,6 +20,7 @@ CONV_STAT_ROWS = 64  # include/stzs.h STZS_CONV_STAT_ROWS
 CONV_W_LANE16 = 16  # include/stzs.h STZS_CONV_W_LANE16
 CONV_W_NARROW32 = 32  # include/stzs.h STZS_CONV_W_NARROW32
 CONV_W_F32 = 64  # include/stzs.h STZS_CONV_W_F32 (precise mode)
+CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD remap)
 
 vp = C.c_void_p
 i64 = C.c_int64

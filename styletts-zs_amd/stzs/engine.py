@@ -224,7 +224,7 @@ class StyleTTSZS:
             # algorithmic bytes: input tile once + output once (+ residual/acc reads), bf16/f32 as stored
             byt = x.B * x.T * x.C * x.t.element_size() + y.B * a.T_out * (cw.ups or 1) * cw.Co * y.t.element_size() * (
                 1 + (res is not None) + (acc_in is not None))
-            tm["rec"].append((what, e0, e1, flops, byt))
+            tm["rec"].append((what, e0, e1, flops, byt, (cw.ks, dil, a.T_out, cw.Co)))
         else:
             self._call(self.lib.stzs_conv1d, a, what)
         if post_ln is not None:  # the LayerNorm that consumes this linear's output (stzs_rowln_args)
@@ -255,7 +255,7 @@ class StyleTTSZS:
     def stop_timer(self):
         tm, self.timer = self.timer, None
         torch.cuda.synchronize(self.device)
-        out = [(w, e0.elapsed_time(e1) * 1e-3, f, b) for (w, e0, e1, f, b) in tm["rec"]]
+        out = [(w, e0.elapsed_time(e1) * 1e-3, f, b, shp) for (w, e0, e1, f, b, shp) in tm["rec"]]
         return out
 
     def stats(self, x: Act, key):

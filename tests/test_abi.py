@@ -84,13 +84,12 @@ def test_ctypes_structs_match_c_layout():
 
 def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
     """the product path refuses to run without the HIP library (no silent CPU fallback)."""
-    import importlib
     from stzs import _lib
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(_lib.StzsError):
         _lib.load()
-    importlib.reload(_lib)
+    # (monkeypatch restores the loaded handle; a module reload here would orphan its ctypes argtypes)
 
 
 def test_product_never_imports_oracle():
@@ -118,3 +117,54 @@ def test_istft_stream_spans_tile_the_output(Tf, chunks):
         f0 += Fc
     assert nxt == (Tf - 1) * 5
     assert L.stzs_istft_stream_span(0, 0, 1, 20, 5, C.byref(n0), C.byref(n1)) == _lib.ESHAPE
+
+
+_STRUCT_CALLS = [  # entry point, ctypes struct, extra int arguments between the struct and the stream
+    ("stzs_conv1d", "ConvArgs", ()), ("stzs_chan_stats", "StatsArgs", ()),
+    ("stzs_chan_stats_final", "StatsArgs", (64,)), ("stzs_row_layernorm", "RowLNArgs", ()),
+    ("stzs_quant_rows", "QuantArgs", ()), ("stzs_attention", "AttnArgs", ()), ("stzs_lstm", "LstmArgs", ()),
+    ("stzs_predictor_prep", "PrPrepArgs", ()), ("stzs_durations", "DurArgs", ()),
+    ("stzs_alignment", "AlignArgs", ()), ("stzs_gather_rows", "GatherArgs", ()),
+    ("stzs_adain_dwup", "DwupArgs", ()), ("stzs_f0n_down", "F0nArgs", ()),
+    ("stzs_harmonic_source", "SourceArgs", ()), ("stzs_istft", "IstftArgs", ()),
+    ("stzs_istft_stream", "IstftStreamArgs", ()), ("stzs_stft_frames", "FramesArgs", ()),
+    ("stzs_log_mel", "LogMelArgs", ()), ("stzs_pool_rows", "PoolArgs", ()), ("stzs_copy2d", "CopyArgs", ()),
+]
+
+
+@pytest.mark.parametrize("name,struct,extra", _STRUCT_CALLS)
+def test_entry_points_reject_before_launch(name, struct, extra):
+    """SURVEY §8(b) 'Errors': every compute entry point validates its arguments before any HIP call, so a
+    bad call returns a code (never launches, never crashes) -- checkable without a GPU.  NULL args and
+    NULL required pointers -> STZS_EINVAL; every pointer set but an empty batch / zero sizes ->
+    STZS_ESHAPE."""
+    from stzs import _lib
+    L = _lib.load()
+    fn = getattr(L, name)
+    S = getattr(_lib, struct)
+    assert fn(None, *extra, None) == _lib.EINVAL
+    a = S()  # all zero: required pointers NULL
+    assert fn(C.byref(a), *extra, None) == _lib.EINVAL
+    for f, ct in S._fields_:
+        if ct is C.c_void_p:  # (every pointer field of the bindings is a void*)
+            setattr(a, f, 0x1000)
+    if name == "stzs_conv1d":
+        a.cic = 128  # (the K-step width is validated first: EINVAL)
+    assert fn(C.byref(a), *extra, None) == _lib.ESHAPE  # sizes all 0: rejected, nothing dereferenced
+
+
+def test_scalar_entry_points_reject_before_launch():
+    from stzs import _lib
+    L = _lib.load()
+    p = C.c_void_p(0x1000)
+    E, S = _lib.EINVAL, _lib.ESHAPE
+    assert L.stzs_dn_cond(None, p, p, 1, 1, None) == E and L.stzs_dn_cond(p, p, p, 0, 1, None) == S
+    assert L.stzs_dn_cond_steps(p, None, p, 1, 1, 1, None) == E and L.stzs_dn_cond_steps(p, p, p, 1, 1, 0, None) == S
+    assert L.stzs_adaln_expand(None, p, p, 1, 1, 1, 1, 0, None) == E
+    assert L.stzs_adaln_expand(p, p, p, 1, 1, 33, 1, 0, None) == S  # nchunk <= 32
+    assert L.stzs_cfg_euler(p, None, 1, 1, 0, 1.0, 1.0, 0.5, None) == E
+    assert L.stzs_cfg_euler(p, p, 1, 1, 0, 1.0, 0.0, 0.5, None) == S  # sigma must be > 0
+    assert L.stzs_state_init(None, p, 1, 1, 0, 1.0, None) == E and L.stzs_state_init(p, p, 0, 1, 0, 1.0, None) == S
+    assert L.stzs_mean_rows(p, None, 1, 1, 8, 8, 0, 8, 8, None) == E
+    assert L.stzs_mean_rows(p, p, 1, 0, 8, 8, 0, 8, 8, None) == S
+    assert L.stzs_embed(p, p, None, 1, 1, 8, 8, None) == E and L.stzs_embed(p, p, p, 1, 0, 8, 8, None) == S

@@ -1,5 +1,5 @@
 """Microbenchmark of the MRF conv shapes (stage 1: B=64, T=24001, C=128) with ablation flags.
-flags: 1 = skip input staging, 2 = skip K loop, 4 = skip epilogue stores."""
+flags: 1 = skip input staging, 2 = one tap only, 4 = skip epilogue stores, 128 = no XCD remap."""
 import math
 import os
 import sys
@@ -20,7 +20,7 @@ B = int(os.environ.get("B", 64))
 cases = [(24001, 128, 3, 1), (24001, 128, 11, 5), (4000, 256, 3, 1), (4000, 256, 11, 5)]
 if os.environ.get("CASE"):
     cases = [cases[int(os.environ["CASE"])]]
-FLAGS = [int(f, 0) for f in os.environ.get("FLAGS", "0,1,2,4,3,6,5,7").split(",")]
+FLAGS = [int(f, 0) for f in os.environ.get("FLAGS", "0,128,1,2,4,3,6,5,7").split(",")]
 for (T, C, k, dil) in cases:
     w = torch.randn(C, C, k) / math.sqrt(C * k)
     A = Arena()
