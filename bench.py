@@ -56,6 +56,28 @@ def make_inputs(S, B, seed):
     return tok, ref, eps, dur
 
 
+def rank_weights(S, rank, world, dev):
+    """The packed weights every rank synthesizes with.  Rank 0 owns the parameters (seeded init); every other
+    rank packs a placeholder arena of the same layout (seed 1: different bytes) and receives rank 0's with
+    ONE broadcast of the arena (RCCL over xGMI on the GPU node; gloo in tests/test_dist.py).
+    -> (PackedModel, broadcast wall ms)"""
+    from stzs.params import init_params
+    from stzs.weights import PackedModel
+    W = PackedModel(S, init_params(S, seed=0 if rank == 0 else 1), dev)
+    ms = 0.0
+    if world > 1:
+        from stzs.dist import broadcast_weights
+        ms = broadcast_weights(W, src=0)
+    return W, ms
+
+
+def rank_inputs(S, B, rank):
+    """this rank's shard of the global batch: utterances [rank*B, (rank+1)*B), their inputs and seeds."""
+    tok, ref, eps, dur = make_inputs(S, B, seed=rank)
+    seeds = [rank * B + i for i in range(B)]
+    return tok, ref, eps, dur, seeds
+
+
 def cpu_baseline(S, P, budget_s=15.0):
     from oracle import stzs_ref as R
     nthr = min(16, len(os.sched_getaffinity(0)))
@@ -163,18 +185,14 @@ def main():
     from stzs.spec import SPEC_V0
     S = SPEC_V0
     # rank 0 owns the weights; every other rank receives them with ONE RCCL broadcast of the arena
-    P = init_params(S, seed=0 if rank == 0 else 1)
-    eng = StyleTTSZS(S, P, device=dev)
-    bcast_ms = 0.0
-    if world > 1:
-        from stzs.dist import broadcast_weights
-        bcast_ms = broadcast_weights(eng, src=0)
+    W, bcast_ms = rank_weights(S, rank, world, dev)
+    eng = StyleTTSZS(S, None, device=dev, packed=W)
+    P = init_params(S, seed=0) if rank == 0 and world == 1 else None  # host params: CPU baseline / extra modes
 
     B = args.batch
-    tok, ref, eps, dur = make_inputs(S, B, seed=rank)
+    tok, ref, eps, dur, seeds = rank_inputs(S, B, rank)
     tok_d, ref_d, eps_d, dur_d = (t.to(dev) for t in (tok, ref, eps, dur))
     n_frames = int(dur[0].sum())
-    seeds = [rank * B + i for i in range(B)]
 
     def step():
         return eng.synth(tok_d, ref_d, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps_d, durations=dur_d,

@@ -1,10 +1,11 @@
 """Multi-GPU plumbing: utterances shard embarrassingly across ranks, one process
-per GPU; the ONLY collective is the initial weight broadcast from rank 0 — the whole packed arena
-(one contiguous uint8 buffer) in a single RCCL broadcast over xGMI, plus the small hosted front-end
-tensors.  No collective runs on the synthesis data path.  The same code runs under gloo on CPU
-(tests/test_dist.py)."""
+per GPU; the ONLY collective is the initial weight broadcast from rank 0 -- the whole packed arena
+(one contiguous uint8 buffer holding every parameter the engine reads, front end included) in a
+single RCCL broadcast over xGMI.  No collective runs on the synthesis data path.  The same code runs
+under gloo on CPU (tests/test_dist.py)."""
 from __future__ import annotations
 
+import hashlib
 import time
 
 import torch
@@ -22,14 +23,30 @@ def broadcast_arena(buf: torch.Tensor, src: int = 0):
     dist.broadcast(buf, src=src)
 
 
-def broadcast_weights(eng, src: int = 0) -> float:
-    """broadcast the engine's weight arena (+ front-end params) from `src`; returns wall ms."""
-    if eng.device.type == "cuda":
-        torch.cuda.synchronize(eng.device)
+def _packed(obj):
+    """StyleTTSZS engine or PackedModel -> PackedModel."""
+    return obj.W if hasattr(obj, "W") else obj
+
+
+def broadcast_weights(obj, src: int = 0) -> float:
+    """Broadcast the weight arena of an engine (or a PackedModel) from `src`; returns wall ms.
+
+    The arena is the engine's complete parameter state: every packed conv / linear / LSTM / norm table
+    and the front-end constants (DFT basis, window, filterbank) live in it (stzs/weights.py:PackedModel),
+    and the engine derives nothing else from host parameters.  So after this call all ranks hold
+    byte-identical weights, which `arena_digest` checks."""
+    W = _packed(obj)
+    dev = W.arena.buf.device
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    broadcast_arena(eng.W.arena.buf, src)
-    for k in sorted(eng.fe):
-        dist.broadcast(eng.fe[k], src=src)
-    if eng.device.type == "cuda":
-        torch.cuda.synchronize(eng.device)
+    broadcast_arena(W.arena.buf, src)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     return (time.perf_counter() - t0) * 1e3
+
+
+def arena_digest(obj) -> str:
+    """sha256 of the arena bytes (host copy; for tests / start-up checks, not the data path)."""
+    buf = _packed(obj).arena.buf
+    return hashlib.sha256(buf.detach().cpu().numpy().tobytes()).hexdigest()

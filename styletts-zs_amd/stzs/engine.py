@@ -101,8 +101,10 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 
 
 class StyleTTSZS:
-    def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False):
-        """fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
+    def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
+                 packed: PackedModel = None):
+        """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
+        fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
         precise_decoder: PARITY mode -- the decoder (pre-blocks, generator, conv_post) keeps fp32 activations
         and runs every conv on fp32 MFMA operands (STZS_CONV_W_F32) to meet the north-star mel-L1 <= 1e-3 vs
@@ -114,7 +116,12 @@ class StyleTTSZS:
         self.device = torch.device(device)
         self.lib = L.load()
         L.check(self.lib.stzs_init(self.device.index or 0), "stzs_init")
-        self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder)
+        if packed is not None:
+            assert packed.spec == spec and packed.arena.buf.device == self.device and packed.precise == precise_decoder, \
+                "packed model: spec / device / precise mode differ"
+            self.W = packed
+        else:
+            self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder)
         self._bufs = {}
         self._consts = {}
         self._ws = None

@@ -419,6 +419,7 @@ class PackedModel:
         self.dec_norm = pack_norm_group(A, "dec.norms", P, dec_norms, S.style_ac, f32=f32)
         A.finalize(device, fill=fill)
         self.device = device
+        self.precise = precise
 
     def t(self, name):
         return self.arena[name]

@@ -39,6 +39,24 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+def _bench_worker(rank, world, port, out):
+    """bench.py's world > 1 set-up path (rank_weights -> stzs.dist.broadcast_weights, rank_inputs), up to the
+    first GPU call, on CPU under gloo."""
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from stzs.dist import arena_digest
+    from stzs.spec import SPEC_TINY
+    W, ms = bench.rank_weights(SPEC_TINY, rank, world, torch.device("cpu"))
+    tok, ref, eps, dur, seeds = bench.rank_inputs(SPEC_TINY, 4, rank)
+    out[rank] = dict(digest=arena_digest(W), ms=ms, seeds=seeds, tok=tok.tolist(),
+                     eps=hashlib.sha256(eps.numpy().tobytes()).hexdigest(), nframes=int(dur[0].sum()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def test_gloo_weight_broadcast_and_shards():
     world = 2
     port = _free_port()
@@ -49,6 +67,48 @@ def test_gloo_weight_broadcast_and_shards():
     assert b0 != b1            # different initial bytes
     assert a0 == a1 == b0      # rank 1 now holds rank 0's arena
     assert (lo0, hi0, lo1, hi1) == (0, 256, 256, 512)
+
+
+def test_gloo_bench_rank_setup():
+    """bench.py world-2 set-up under gloo: both ranks end with rank 0's arena (byte-identical to packing the
+    seed-0 parameters directly), i.e. identical weights for synthesis; their input shards and source-noise
+    seeds are disjoint."""
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    from stzs.dist import arena_digest
+    from stzs.params import init_params
+    from stzs.spec import SPEC_TINY
+    from stzs.weights import PackedModel
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bench_worker, args=(world, port, out), nprocs=world, join=True)
+    r0, r1 = out[0], out[1]
+    want = arena_digest(PackedModel(SPEC_TINY, init_params(SPEC_TINY, seed=0), "cpu"))
+    assert r0["digest"] == r1["digest"] == want
+    assert r1["ms"] >= 0.0
+    assert set(r0["seeds"]).isdisjoint(r1["seeds"]) and r0["seeds"] == [0, 1, 2, 3]
+    assert r0["tok"] != r1["tok"] and r0["eps"] != r1["eps"]
+    assert r0["nframes"] == r1["nframes"]
+
+
+def test_broadcast_weights_accepts_engine_like():
+    """broadcast_weights takes an engine (anything with .W) or a PackedModel; world 1 (gloo) is a no-op copy."""
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    from stzs.dist import _packed
+    from stzs.params import init_params
+    from stzs.spec import SPEC_TINY
+    from stzs.weights import PackedModel
+
+    W = PackedModel(SPEC_TINY, init_params(SPEC_TINY, seed=0), "cpu")
+
+    class Eng:
+        pass
+    e = Eng()
+    e.W = W
+    assert _packed(e) is W and _packed(W) is W
 
 
 def test_shard_range_partition():
