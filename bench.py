@@ -10,7 +10,7 @@ workload: one "step" = one synth() of a batch of 64 utterances per GPU (BASELINE
 latency : configs[1] (batch 1, 10-step CFG-5 sampling) timed per utterance; p50/p90 reported.
 timing  : W warm-up steps, then K steps bracketed by barrier + synchronize, max over ranks.
           The synth() of a step is replayed from one captured HIP graph (all ~1000 launches).
-roofline: the dominant kernel (mrf_conv on the generator MRF convs, 89% of decoder FLOPs) timed
+roofline: the dominant kernel (the generator MRF convs -- mrfv_conv at stage 1, mrf_conv at stage 0 -- 89% of decoder FLOPs) timed
           per launch with HIP events on its own stream in an instrumented eager pass right after
           the timed region; achieved = algorithmic FLOP / average launch time (bound: MFMA).
 cpu     : the CPU oracle (oracle/stzs_ref.py, torch fp32) on a bounded sample of the same
@@ -299,7 +299,8 @@ def main():
     roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                 frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=traffic, traffic_src=tsrc,
                 alg_bytes_per_launch=round(bsum / nl),
-                kernel="mrf_conv (generator MRF convs)", launches=len(rec),
+                kernel="generator MRF convs: mrfv_conv (stage 1, csrc/mrfv.hip) + mrf_conv (stage 0, csrc/mrf.hip)",
+                launches=len(rec),
                 avg_launch_us=round(tsum / nl * 1e6, 2), alg_gflop_per_launch=round(fsum / nl / 1e9, 3),
                 time_frac=round(t_roof / tsum, 4) if tsum > 0 else None, hbm_bound_launches=n_hbm,
                 alg_hbm_gbs=round(bsum / tsum / 1e9, 1) if tsum > 0 else None)

@@ -108,6 +108,12 @@ typedef struct stzs_conv_args {
 /* flags bit (diagnostic): keep the dispatcher's linear workgroup order on the LANE16 / NARROW32 kernels
  * instead of the XCD-aware remap (neighbouring time tiles on one L2); results are identical either way. */
 #define STZS_CONV_LINEAR_IDS 128
+/* flags bit: weights packed in MFMA fragment order for the register-direct MRF conv (csrc/mrfv.hip,
+ * stzs/weights.py pack_conv(frag32=True)): [co_pad/128][ci_pad/128][ks][4 k-steps][4 waves][2][64 lanes][8]
+ * bf16, packed row w*32 + nt*16 + g*4 + r of a 128-column tile holding output channel w*32 + g*8 + nt*4 + r.
+ * Same prologue / epilogue contract as STZS_CONV_W_LANE16 with ks in {3, 7, 11} (Snake) or ks = 3
+ * (LeakyReLU / identity), Co % 8 == 0; bit-identical results, no weight ring and no K-loop barrier. */
+#define STZS_CONV_W_FRAG32 256
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------
@@ -177,7 +183,7 @@ int stzs_attention(const stzs_attn_args* a, void* stream);
  * (stzs/weights.py lstm_frags); H % 32 == 0, H <= 256; h written bf16 to y[b, t, dir*H + j].
  * Launches H/32 x ndir x ceil(B/64) co-resident workgroups that exchange h_t every step through
  * `xchg` (write-through stores + agent-scope arrival counters in `sync`); spins are bounded and a
- * timeout sets the last word of `sync` instead of hanging.
+ * timeout ORs STZS_STATUS_LSTM_TIMEOUT into `*status` (and the last word of `sync`) instead of hanging.
  * (DurationEncoder BiLSTMs, duration LSTM, shared LSTM) */
 typedef struct stzs_lstm_args {
     const float* gx;
@@ -187,7 +193,14 @@ typedef struct stzs_lstm_args {
     void* sync;  /* workspace: 4096 bytes of arrival counters (zeroed by the call itself) */
     int64_t ldg, bsg, ldy, bsy;
     int32_t B, T, H, ndir;
+    /* optional caller-owned status word: a spin that times out ORs STZS_STATUS_LSTM_TIMEOUT into it (the
+     * h-states of that call are then wrong).  Never cleared by the library, so one word can collect the
+     * status of every launch of a captured graph; the caller reads it after the work (StyleTTSZS raises). */
+    uint32_t* status;
+    uint32_t spin_limit; /* polls before a spin times out; 0 = default (1 << 22). Tests force small values. */
+    uint32_t pad_u;
 } stzs_lstm_args;
+#define STZS_STATUS_LSTM_TIMEOUT 1u
 size_t stzs_lstm_workspace(int B, int H, int ndir);
 int stzs_lstm(const stzs_lstm_args* a, void* stream);
 

@@ -818,7 +818,8 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
 int stzs_mrf_conv_launch(const stzs_conv_args& a, hipStream_t s);     // csrc/mrf.hip
 int stzs_narrow_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrf.hip
 
-extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
+// the dispatcher proper; csrc/dispatch.hip routes the register-direct MRF form before it
+__attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args* a, void* stream) {
     if (!a || !a->x || !a->w || !a->y) return STZS_EINVAL;
     if (a->cic != 32 && a->cic != 64 && a->cic != 128) return STZS_EINVAL;
     if (a->B <= 0 || a->T_in <= 0 || a->T_out <= 0 || a->Ci <= 0 || a->Co <= 0 || a->ks <= 0 || a->dil <= 0 ||

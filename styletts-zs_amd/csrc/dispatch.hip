@@ -1,0 +1,25 @@
+// stzs_conv1d entry (include/stzs.h): argument checks shared by every conv form, then the
+// register-direct MRF conv (csrc/mrfv.hip) for STZS_CONV_W_FRAG32 weights, the general dispatcher
+// (csrc/conv.hip) for everything else.  Kept in its own translation unit so that adding a kernel
+// form does not rebuild conv.hip.
+#include "common.hpp"
+
+int stzs_conv1d_core(const stzs_conv_args* a, void* stream);           // csrc/conv.hip
+int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/mrfv.hip
+
+extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
+    if (a && (a->flags & STZS_CONV_W_FRAG32)) {
+        if (!a->x || !a->w || !a->y) return STZS_EINVAL;
+        if (a->flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 | STZS_CONV_W_F32 | STZS_CONV_A_DMA))
+            return STZS_EINVAL;
+        if (a->B <= 0 || a->T_in <= 0 || a->T_out <= 0 || a->Ci <= 0 || a->Co <= 0 || a->dil <= 0) return STZS_ESHAPE;
+        if (a->ci_pad < a->Ci || a->co_pad < a->Co) return STZS_ESHAPE;
+        if (a->ldx % 8 || a->bsx % 8 || a->ldx < ((a->Ci + 7) / 8) * 8) return STZS_ESHAPE;
+        if (!stzs_aligned(a->x, 16) || !stzs_aligned(a->w, 16) || !stzs_aligned(a->y, 16)) return STZS_EINVAL;
+        if (a->pro_mode == STZS_PRO_ADAIN && (!a->pro_mean || !a->pro_rstd || !a->pro_gb)) return STZS_EINVAL;
+        if (a->in_dtype == STZS_F8 || a->x_scale) return STZS_EDTYPE;
+        if (a->stat_part && !stzs_aligned(a->stat_part, 8)) return STZS_EINVAL;
+        return stzs_mrfv_conv_launch(*a, reinterpret_cast<hipStream_t>(stream));
+    }
+    return stzs_conv1d_core(a, stream);
+}

@@ -28,14 +28,15 @@ constexpr unsigned SPIN_LIMIT = 1u << 22;
 typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
-STZS_DEV unsigned poll_ge(gu32* ctr, unsigned target, gu32* err) {
+STZS_DEV unsigned poll_ge(gu32* ctr, unsigned target, gu32* err, gu32* status, unsigned limit) {
     unsigned v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     while (v < target) {
         __builtin_amdgcn_s_sleep(1);
         v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (++spins > SPIN_LIMIT) {
+        if (++spins > limit) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (status) __hip_atomic_fetch_or(status, STZS_STATUS_LSTM_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return 0;
         }
     }
@@ -69,6 +70,8 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     // the slab through a buffer descriptor: 16-B write-through (sc1, aux 16) stores and loads
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(X, 0, 2 * MROWS * H * 2, 0x00020000);
     gu32* err = (gu32*)(a.sync) + 1023;
+    gu32* status = (gu32*)a.status;
+    const unsigned limit = a.spin_limit ? a.spin_limit : SPIN_LIMIT;
 
     // W_hh^T fragments of this wave's gate (g = wave) for the workgroup's 32 units, in registers
     const bf16_t* Wd = reinterpret_cast<const bf16_t*>(a.whhT) + (long)dir * (G4 / 16) * NKS * 512;
@@ -108,7 +111,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         if (s == 0) {
             for (int e = tid; e < MROWS * hp / 8; e += 512) reinterpret_cast<uint4*>(As)[e] = make_uint4(0, 0, 0, 0);
         } else {
-            if (tid == 0 && s_ok) s_ok = poll_ge(ctr, (unsigned)(P * s), err);  // after a timeout: no more spins
+            if (tid == 0 && s_ok) s_ok = poll_ge(ctr, (unsigned)(P * s), err, status, limit);  // after a timeout: no more spins
             PROF(1)
             __syncthreads();
             // h_{s-1}: MROWS x H bf16 = H/8 16-B words per row, all of this thread's sc1 loads in flight
@@ -198,7 +201,8 @@ extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     const int P = a->H / UNITS;
     if (groups * a->ndir > 63 || P * a->ndir * groups > 256) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // counters (and the error word) zeroed per call: a memset node under graph capture
+    // counters (and the per-call error word) zeroed per call: a memset node under graph capture; the
+    // caller's status word (a->status) accumulates over calls and is never cleared here
     if (hipMemsetAsync(a->sync, 0, 4096, s) != hipSuccess) return STZS_EHIP;
     const int hp = a->H + 8;
     const size_t lds = ((MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4;

@@ -1,0 +1,338 @@
+// The MRF conv, register-direct weight form (SURVEY.md §8(a) a12 -- the generator's AdaINResBlock1
+// convs -- and the k3 convs of the decoder / predictor AdaIN residual blocks, a9).
+//
+// Same arithmetic as csrc/mrf.hip (same K order per output element, same staged bf16 operands, so the
+// two kernels are bit-identical), different data movement:
+//  * the 4 waves of a 256-thread workgroup split the 128 OUTPUT CHANNELS (32 each) instead of a 2 x 2
+//    grid, so every wave needs every time row of the staged input tile (8 B-fragments per K-step from
+//    LDS, 50% of the LDS read rate at the MFMA rate) but only ITS 32 channels of the weights: 2
+//    A-fragments per K-step, read straight into VGPRs with one coalesced 16-B load per lane each
+//    (weights packed in fragment order, STZS_CONV_W_FRAG32) and prefetched two K-steps ahead;
+//  * so the K loop has no weight ring, no LDS-DMA and no barrier at all -- the only barriers are the
+//    two around the staging of each 128-channel input chunk;
+//  * LDS = the staged input tile only (<= 48 KB), several workgroups per CU: one workgroup's staging
+//    (HBM latency + the AdaIN / Snake VALU work) overlaps the others' MFMAs.
+// Epilogue straight from the accumulators: lane (g, n) holds 8 consecutive channels (packed row
+// w*32 + nt*16 + 4g + r <-> channel w*32 + g*8 + nt*4 + r) of one time row -> 16-B residual /
+// accumulate loads and stores; fused InstanceNorm statistics per 64-row chunk as in mrf.hip.
+#include "common.hpp"
+
+#ifndef STZS_MRFV_OCC
+#define STZS_MRFV_OCC 2
+#endif
+#ifndef STZS_MRFV_OCC1
+#define STZS_MRFV_OCC1 3
+#endif
+
+namespace {
+
+constexpr int NTH = 256;
+constexpr int BT = 128, BCO = 128;
+constexpr int P = 272;  // staged input row pitch, bytes (conflict-free ds_read_b128)
+constexpr int SB = 12;  // staged 16-B vectors per thread: 16 rows x 12 = 192 >= rows_in
+#ifndef STZS_MRFV_SBB
+#define STZS_MRFV_SBB 12
+#endif
+constexpr int SBB = STZS_MRFV_SBB;  // loads per staging batch (SB / SBB batches)
+constexpr int CS_BYTES = 5 * 128 * 4;  // per-channel prologue constants
+
+STZS_DEV float row_sum16(float x) {  // sum over the 16 lanes of a DPP row (VALU only)
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, true));
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, true));
+    return x;
+}
+
+// NCH = 1: exactly one 128-channel input chunk (the stage-1 generator convs): the accumulators are not live
+// during the staging, so the kernel fits 3 workgroups per CU; NCH = 0: any number of chunks, 2 per CU.
+template <int PACT, bool HR, bool HA, int KS, int NCH>
+__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NKC = KS * 4;  // 32-wide K-steps per 128-channel chunk
+    const int dil = a.dil;
+    const int rows_in = BT + (KS - 1) * dil;
+    float* cs = reinterpret_cast<float*>(smem + ((rows_in * P + 15) & ~15));
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tpb = (a.T_out + BT - 1) / BT;
+    const int nx = gridDim.x;
+    const int lin = (a.flags & STZS_CONV_LINEAR_IDS) ? blockIdx.y * nx + blockIdx.x
+                                                      : xcd_remap(blockIdx.y * nx + blockIdx.x, nx * gridDim.y);
+    const int by = lin / nx, bx = lin - by * nx;  // (co tile, utterance x time tile)
+    const int bq = bx / tpb;
+    const int t0 = (bx - bq * tpb) * BT;
+    const int nchunk = NCH ? NCH : a.ci_pad >> 7;
+    // weights: [co tile][chunk][tap][kq][wave][nt][lane][8] bf16 -> 512 bf16x8 per K-step
+    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + ((long)by * nchunk * NKC) * 512 + wave * 128 + lane;
+    auto wload = [&](bf16x8 (&w)[2], int kk) {
+        const bf16x8* p = Wf + (long)kk * 512;
+        w[0] = p[0];
+        w[1] = p[64];
+    };
+    f32x4 acc[2][8];
+
+    const int xoff0 = (lane & 15) * P + (lane >> 4) * 16;
+    const int dP = dil * P;
+    const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x) + (long)bq * a.bsx;
+    const int cv = tid & 15, rsub = tid >> 4;
+    bf16x8 wf[3][2];
+    bf16x8 xf[8];
+
+    for (int cc = 0; cc < nchunk; ++cc) {
+        const int kb = cc * NKC;
+        wload(wf[0], kb);  // the chunk's first two weight K-steps fly during the staging
+        wload(wf[1], kb + 1);
+        __syncthreads();  // every wave is done reading the previous chunk's tile and constants
+#ifndef STZS_MRFV_NOSTAGE
+        if (!(a.flags & 1)) {
+#else
+        if (0) {
+#endif
+            const int c = cc * 128 + cv * 8;
+            const bool c_ok = c < a.Ci;  // vectors past Ci (ci_pad > Ci) are zero; weights there are 0
+            const int cl = c_ok ? c : 0;
+            // per-channel constants (128 threads):  t = x*ka + kb (revolutions of cos(2 a y)),
+            // out = cos(t) * km + (x*ksc + ksh)  [Snake]   or   out = act(x*ksc + ksh)
+            if (tid < 128) {
+                const int ch = cc * 128 + tid;
+                const bool ok = ch < a.Ci;
+                float sc = 0.f, sh = 0.f;
+                if (ok && a.pro_mode == STZS_PRO_ADAIN) {
+                    const float mu = a.pro_mean[(long)bq * a.stat_bs + ch];
+                    const float rs = a.pro_rstd[(long)bq * a.stat_bs + ch];
+                    const float gm = a.pro_gb[(long)bq * a.gb_bs + ch];
+                    const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + ch];
+                    sc = (1.f + gm) * rs;
+                    sh = be - mu * sc;
+                } else if (ok) {
+                    sc = a.pro_cscale;
+                }
+                if constexpr (PACT == STZS_ACT_SNAKE) {
+                    const float al = ok ? a.pro_alpha[ch] : 1.f;
+                    const float h = 0.5f / al;
+                    const float w = al * 0.318309886183790672f;  // a / pi
+                    cs[tid] = sc * w;
+                    cs[128 + tid] = sh * w;
+                    cs[256 + tid] = sc;
+                    cs[384 + tid] = sh + h;
+                    cs[512 + tid] = -h;
+                } else {
+                    cs[256 + tid] = sc;
+                    cs[384 + tid] = sh;
+                }
+            }
+            // the tile's rows (+ dilation halo) in SB / SBB batches of SBB 16-B loads per thread
+#pragma unroll
+            for (int bt = 0; bt < SB / SBB; ++bt) {
+                uint4 raw[SBB];
+#pragma unroll
+                for (int i = 0; i < SBB; ++i) {  // 32-bit offsets from the utterance base (SGPR): saddr loads
+                    int tin = t0 - a.pad + rsub + 16 * (bt * SBB + i);
+                    tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+                    const unsigned off = (unsigned)(tin * (int)a.ldx + cl) * 2u;
+                    raw[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(X) + off);
+                }
+                if (bt == 0) __syncthreads();  // constants visible
+                // pair-major: the constants of one channel pair (10 registers) at a time, each vector's
+                // pair transformed in place (the staging holds only the raw vectors + one pair's constants)
+                const float slope = a.pro_slope;
+                uint32_t* rw = reinterpret_cast<uint32_t*>(raw);
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    __builtin_amdgcn_sched_barrier(0);  // keep one pair's constants live at a time
+                    const int c0 = cv * 8 + 2 * p;
+                    const f32x2 ksc = *reinterpret_cast<const f32x2*>(cs + 256 + c0);
+                    const f32x2 ksh = *reinterpret_cast<const f32x2*>(cs + 384 + c0);
+                    f32x2 ka = {0.f, 0.f}, kbv = {0.f, 0.f}, km = {0.f, 0.f};
+                    if constexpr (PACT == STZS_ACT_SNAKE) {
+                        ka = *reinterpret_cast<const f32x2*>(cs + c0);
+                        kbv = *reinterpret_cast<const f32x2*>(cs + 128 + c0);
+                        km = *reinterpret_cast<const f32x2*>(cs + 512 + c0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < SBB; ++i) {
+                        const uint32_t w = rw[4 * i + p];
+                        const f32x2 x = f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)};
+                        f32x2 y = x * ksc + ksh;  // v_pk_fma_f32
+                        if constexpr (PACT == STZS_ACT_SNAKE) {
+                            const f32x2 t = x * ka + kbv;
+                            const f32x2 cz = f32x2{__builtin_amdgcn_cosf(t.x), __builtin_amdgcn_cosf(t.y)};
+                            y = cz * km + y;
+                        } else if constexpr (PACT == STZS_ACT_LEAKY) {
+                            y.x = y.x >= 0.f ? y.x : y.x * slope;
+                            y.y = y.y >= 0.f ? y.y : y.y * slope;
+                        }
+                        const int tin = t0 - a.pad + rsub + 16 * (bt * SBB + i);  // zero padding / channels past Ci
+                        const bool ok = c_ok && tin >= 0 && tin < a.T_in;
+                        rw[4 * i + p] = ok ? pack2bf(y.x, y.y) : 0u;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < SBB; ++i) {
+                    const int r = rsub + 16 * (bt * SBB + i);
+                    if (r < rows_in) *reinterpret_cast<uint4*>(smem + r * P + cv * 16) = raw[i];
+                }
+            }
+        }
+        __syncthreads();
+        if (cc == 0) {  // (after the first staging: the accumulators are not live across it)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        // K loop: no barrier.  K-step s = tap*4 + kq reads input rows t + tap*dil, channels kq*32 ..
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
+#pragma unroll
+        for (int s = 0; s < NKC; ++s) {
+            if (s + 2 < NKC) wload(wf[(s + 2) % 3], kb + s + 2);
+            const int sn = s + 1;
+            const int offn = (sn >> 2) * dP + (sn & 3) * 64;
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % 3][0], xf[mt], acc[0][mt], 0, 0, 0);
+                acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % 3][1], xf[mt], acc[1][mt], 0, 0, 0);
+                if (sn < NKC) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + offn + mt * 16 * P);
+            }
+            if (s + 2 < NKC) {
+                __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // the two weight loads first
+            }
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                if (sn < NKC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (a.flags & 4) return;
+
+    // ---------------- epilogue: lane (g, n): time t = t0 + mt*16 + n, channels co0 .. co0 + 7
+    const int g = lane >> 4, n = lane & 15;
+    const int co0 = by * BCO + wave * 32 + g * 8;
+    const bool col_ok = co0 < a.Co;
+    const int coc = col_ok ? co0 : 0;
+    float bias[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
+    const bool stat = a.stat_part != nullptr;
+    bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
+    const int nch = (a.T_out + 63) / 64;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // two 64-row halves: one statistics partial each
+        float ss[8], sq[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
+        uint4 rr[4], aa[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int t = t0 + (h * 4 + m) * 16 + n;
+            const int tc = t < a.T_out ? t : a.T_out - 1;
+            if constexpr (HR)
+                rr[m] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr +
+                                                        (long)(tc / a.res_tdiv) * a.ldr + coc);
+            if constexpr (HA)
+                aa[m] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(a.acc_in) + (long)bq * a.bsa +
+                                                        (long)tc * a.lda + coc);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int mt = h * 4 + m;
+            const int t = t0 + mt * 16 + n;
+            const bool ok = col_ok && t < a.T_out;
+            float v[8];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[nt][mt][r] + bias[nt * 4 + r];
+            if constexpr (HR) {
+                float f[8];
+                unpack8(rr[m], f);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] += f[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] *= a.alpha;
+            if constexpr (HA) {
+                float f[8];
+                unpack8(aa[m], f);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = fmaf(a.beta, f[i], v[i]);
+            }
+            const uint4 o = pack8(v);
+            if (ok) *reinterpret_cast<uint4*>(Y + (long)bq * a.bsy + (long)t * a.ldy + coc) = o;
+            if (stat && ok) {  // statistics of the stored (bf16-rounded) values
+                float f[8];
+                unpack8(o, f);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    ss[i] += f[i];
+                    sq[i] = fmaf(f[i], f[i], sq[i]);
+                }
+            }
+        }
+        if (stat) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                ss[i] = row_sum16(ss[i]);
+                sq[i] = row_sum16(sq[i]);
+            }
+            const int r0 = t0 + h * 64;
+            if (n == 0 && col_ok && r0 < a.T_out) {
+                float* Pp = reinterpret_cast<float*>(a.stat_part) + (((long)bq * nch + r0 / 64) * a.stat_ld + co0) * 2;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    Pp[2 * i] = ss[i];
+                    Pp[2 * i + 1] = sq[i];
+                }
+            }
+        }
+    }
+}
+
+template <int PACT, bool HR, bool HA, int NCH>
+void (*pick_ks(int ks))(stzs_conv_args) {
+    switch (ks) {
+        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH>;
+        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH>;
+        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH>;
+        default: return nullptr;
+    }
+}
+template <int PACT, bool HR, bool HA>
+void (*pick(int ks, bool one))(stzs_conv_args) {
+    return one ? pick_ks<PACT, HR, HA, 1>(ks) : pick_ks<PACT, HR, HA, 0>(ks);
+}
+
+}  // namespace
+
+// internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32 weights
+__attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s) {
+    const int rows_in = BT + (a.ks - 1) * a.dil;
+    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || rows_in > 16 * SB ||
+        a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.gate || a.epi_act != STZS_ACT_NONE || a.ups ||
+        a.refl || a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv <= 0)) ||
+        (a.acc_in && (a.lda % 8 || a.bsa % 8)) || (a.stat_part && a.stat_ld < a.Co))
+        return STZS_ESHAPE;
+    if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
+    const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + CS_BYTES;
+    void (*k)(stzs_conv_args) = nullptr;
+    const bool R = a.res != nullptr, A = a.acc_in != nullptr;
+    if (a.pro_act == STZS_ACT_SNAKE) {
+        const bool one = a.ci_pad == 128;
+        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one))
+              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one));
+    } else if (!A && a.ks == 3) {  // the AdaIN residual blocks of the decoder / prosody predictor
+        if (a.pro_act == STZS_ACT_LEAKY)
+            k = R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0>;
+        else if (a.pro_act == STZS_ACT_NONE)
+            k = R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0>;
+    }
+    if (!k) return STZS_ESHAPE;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / BCO);
+    hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}

@@ -19,6 +19,7 @@ PRO_NONE, PRO_ADAIN = 0, 1
 CONV_STAT_ROWS = 64  # include/stzs.h STZS_CONV_STAT_ROWS
 CONV_W_LANE16 = 16  # include/stzs.h STZS_CONV_W_LANE16
 CONV_W_NARROW32 = 32  # include/stzs.h STZS_CONV_W_NARROW32
+CONV_W_FRAG32 = 256  # include/stzs.h STZS_CONV_W_FRAG32
 CONV_W_F32 = 64  # include/stzs.h STZS_CONV_W_F32 (precise mode)
 CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD remap)
 
@@ -66,7 +67,11 @@ class AttnArgs(C.Structure):
 class LstmArgs(C.Structure):
     _fields_ = [("gx", vp), ("whhT", vp), ("y", vp), ("xchg", vp), ("sync", vp),
                 ("ldg", i64), ("bsg", i64), ("ldy", i64), ("bsy", i64),
-                ("B", i32), ("T", i32), ("H", i32), ("ndir", i32)]
+                ("B", i32), ("T", i32), ("H", i32), ("ndir", i32),
+                ("status", vp), ("spin_limit", C.c_uint32), ("pad_u", C.c_uint32)]
+
+
+STATUS_LSTM_TIMEOUT = 1  # include/stzs.h STZS_STATUS_LSTM_TIMEOUT
 
 
 class PrPrepArgs(C.Structure):

@@ -126,6 +126,21 @@ class StyleTTSZS:
         self._consts = {}
         self._ws = None
         self.launches = 0
+        self.lstm_spin_limit = 0  # 0 = the library default; tests force tiny values
+        # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
+        # graph-replayed); check_status() reads it and raises
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    def check_status(self, reset=True):
+        """raise RuntimeError if any LSTM exchange since the last check timed out (its h-states are wrong).
+        Synchronizes the device (one 4-B copy)."""
+        v = int(self.status.item())
+        if reset and v:
+            self.status.zero_()
+        if v & L.STATUS_LSTM_TIMEOUT:
+            raise RuntimeError("stzs_lstm: exchange spin timed out (LSTM workgroups not co-resident?); "
+                               "the prosody outputs of this call are invalid")
+        return v
 
     @classmethod
     def from_checkpoint(cls, path: str, device="cuda:0", **kw) -> "StyleTTSZS":
@@ -207,6 +222,8 @@ class StyleTTSZS:
         if cw.w32 is not None:  # precise mode: fp32 operands on fp32 MFMA (csrc/conv.hip conv_f32)
             a.w, a.cic = self._t(cw.w32).data_ptr(), 32
             flags = (flags & ~8) | L.CONV_W_F32
+        elif getattr(cw, "frag32", False):
+            flags |= L.CONV_W_FRAG32  # register-direct MRF kernel (csrc/mrfv.hip)
         elif getattr(cw, "lane16", False):
             flags |= L.CONV_W_LANE16  # MRF-family kernel (csrc/mrf.hip)
         elif getattr(cw, "narrow32", False):
@@ -320,6 +337,7 @@ class StyleTTSZS:
         a.xchg, a.sync = xchg.data_ptr(), sync.data_ptr()
         a.ldg, a.bsg, a.ldy, a.bsy = gx.ld, gx.bs, y.ld, y.bs
         a.B, a.T, a.H, a.ndir = x.B, x.T, lw.H, 2
+        a.status, a.spin_limit = self.status.data_ptr(), self.lstm_spin_limit
         self._call(self.lib.stzs_lstm, a, key + ".rec")
         return y
 
@@ -868,6 +886,7 @@ class StyleTTSZS:
         t = object.__new__(StyleTTSZS)
         t.__dict__.update(self.__dict__)
         t._bufs, t._consts, t._ws, t.launches, t.timer = {}, {}, None, 0, None
+        t.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         return t
 
     def capture(self, fn):

@@ -47,6 +47,7 @@ class ConvW:
     wscale: Optional[object] = None  # fp8 linears: per-output-column fp32 scale [co_pad]
     f8: bool = False
     w32: Optional[object] = None  # precise mode: fp32 K-step stream (STZS_CONV_W_F32), unpermuted
+    frag32: bool = False  # fragment-order packing of the register-direct MRF kernel (STZS_CONV_W_FRAG32)
 
 
 class Arena:
@@ -124,6 +125,25 @@ def lane16_perm() -> torch.Tensor:
     return (rr & 64) + ((rr >> 2) & 3) * 16 + ((rr >> 4) & 3) * 4 + (rr & 3)
 
 
+def frag32_perm() -> torch.Tensor:
+    """packed row rr = w*32 + nt*16 + g*4 + r of a 128-column tile holds output channel w*32 + g*8 + nt*4 + r:
+    in the register-direct MRF kernel (csrc/mrfv.hip) wave w owns packed rows [32w, 32w + 32) and its
+    swapped-operand accumulators then give lane group g 8 consecutive channels of one time step."""
+    rr = torch.arange(128)
+    return (rr & 96) + ((rr >> 2) & 3) * 8 + ((rr >> 4) & 1) * 4 + (rr & 3)
+
+
+def frag32_stream(wp: torch.Tensor) -> torch.Tensor:
+    """[ks, co_pad, ci_pad] (rows already frag32-permuted) -> [co_pad/128, ci_pad/128 * ks * 4 * 512, 8]: per
+    (co tile, 128-channel chunk, tap, 32-wide k-step) the 16x16x32 A-fragments of the 4 waves x 2 row tiles in
+    lane order -- lane l = g*16 + i holds packed row w*32 + nt*16 + i, channels kq*32 + 8g .. + 8 -- so each
+    fragment is one coalesced 16-B load per lane (include/stzs.h STZS_CONV_W_FRAG32)."""
+    ks, co_pad, ci_pad = wp.shape
+    t = wp.reshape(ks, co_pad // 128, 4, 2, 16, ci_pad // 128, 4, 4, 8)  # tap, cot, w, nt, i, chunk, kq, g, e
+    t = t.permute(1, 5, 0, 6, 2, 3, 7, 4, 8)                              # cot, chunk, tap, kq, w, nt, g, i, e
+    return t.reshape(co_pad // 128, -1, 8).contiguous()
+
+
 def narrow32_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
     """[ks, 32, ci_pad] -> [NK, 32, 32] K-steps for the narrow conv (csrc/mrf.hip narrow_conv): packed row
     rr = nt*16 + g*4 + r holds output channel g*8 + nt*4 + r; 16-B chunks XOR-swizzled as kstep_stream."""
@@ -139,7 +159,7 @@ def narrow32_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
     return t.reshape(nchunk * ks * kpc, 32, 32).contiguous()
 
 
-def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f32=False) -> ConvW:
+def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f32=False, frag32=False) -> ConvW:
     """w: Conv1d [Co, Ci, k] / Linear [Co, Ci] / ConvTranspose1d [Ci, Co, 2*ups] (ups > 0).
     lane16: the MRF kernel's layout (Ci % 128 == 0, Co % 16 == 0, plain conv).
     f32: also pack the precise-mode fp32 stream (ConvW.w32)."""
@@ -169,6 +189,12 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
         wn = A.add(name + ".wpk", narrow32_stream(wp[:, :32], cic).to(torch.bfloat16))
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
         return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True, w32=w32)
+    if frag32:
+        assert not ups and cic == 128 and Co % 8 == 0 and ks in (3, 7, 11), (name, Ci, Co, ks)
+        wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, frag32_perm()].reshape(ks, co_pad, ci_pad)
+        wn = A.add(name + ".wfr", frag32_stream(wp).to(torch.bfloat16))
+        bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
+        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, 0, False, w32=w32, frag32=True)
     if lane16:
         assert cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
@@ -404,10 +430,15 @@ class PackedModel:
                 res = []
                 for m, dil in enumerate(S.rb_dils):
                     p = f"gen.rb{i}.{j}.{m}"
-                    l16 = S.gen_ch[i] % 128 == 0 and (kr - 1) * dil <= 64  # persistent MRF kernel
+                    l16 = S.gen_ch[i] % 128 == 0 and (kr - 1) * dil <= 64  # MRF kernel (csrc/mrf.hip)
+                    # one 128-channel input chunk: the register-direct MRF kernel (csrc/mrfv.hip), 3 workgroups
+                    # per CU; bit-identical to mrf.hip, 8-18% faster on the stage-1 shapes (tools/mrfv_bench.py)
+                    fr = S.gen_ch[i] == 128 and kr in (3, 7, 11) and (kr - 1) * dil <= 64
                     res.append(dict(
-                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16, f32=f32),
-                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"], lane16=l16, f32=f32),
+                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16 and not fr, frag32=fr,
+                                     f32=f32),
+                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"], lane16=l16 and not fr, frag32=fr,
+                                     f32=f32),
                         a1=A.add(p + ".a1", P[p + ".alpha1"].float()), a2=A.add(p + ".a2", P[p + ".alpha2"].float()),
                         n1=p + ".n1", n2=p + ".n2", k=kr, dil=dil))
                     dec_norms += [p + ".n1", p + ".n2"]

@@ -197,12 +197,7 @@ MRF_CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", MRF_CASES)
-def test_mrf_persistent_conv(eng, case):
-    """MRF-family conv (csrc/mrf.hip, STZS_CONV_W_LANE16 weights): AdaIN + Snake / LeakyReLU / identity
-    prologue, residual (at t / res_tdiv) / alpha / acc_in epilogue and fused statistics vs the fp32
-    reference.  tolerance: max-abs error <= 1.5e-2 of max|ref| (bf16 output); statistics 1e-5 of the
-    stored tensor."""
+def _run_mrf(eng, case, form):
     B, T, Ci, Co, k, dil, act, hr, ha, st, tdiv = case
     g = torch.Generator().manual_seed(B * T + Ci + k)
     pad = dil * (k - 1) // 2
@@ -222,7 +217,11 @@ def test_mrf_persistent_conv(eng, case):
     osc = 1 / 3 if ha else (0.7071 if hr else 1.0)
     ref = conv_ref(x, w, b, pad=pad, dil=dil, stride=1, sc=sc, sh=sh, pro_act=None if act == "none" else act,
                    slope=0.2, alpha=alpha, res=res, res_tdiv=tdiv, out_scale=osc, acc_in=acc, beta=1.0)
-    cw, _A = _pack(w, b, lane16=True)
+    from stzs.weights import Arena, pack_conv
+    A = Arena()
+    cw = pack_conv(A, "t", w, b, lane16=form == "lane16", frag32=form == "frag32")
+    A.finalize("cuda:0")
+    cw.w, cw.b = A[cw.w], A[cw.b]
     from stzs import _lib as L
     xd = _act(_dev_ntc(x, (Ci + 7) // 8 * 8), Ci)
     yd = _act(torch.zeros(B, T, Co, dtype=torch.bfloat16, device="cuda:0"))
@@ -233,17 +232,40 @@ def test_mrf_persistent_conv(eng, case):
     pa = {"snake": L.ACT_SNAKE, "leaky": L.ACT_LEAKY, "none": L.ACT_NONE}[act]
     out = eng.conv(cw, xd, yd, pad=pad, dil=dil, pro=pro, pro_act=pa, pro_slope=0.2,
                    pro_alpha=keep[3] if act == "snake" else None, res=rd, res_tdiv=tdiv, alpha=osc, acc_in=ad,
-                   beta=1.0, stats_key="t.mrfst" if st else None)
-    got = yd.t.float().cpu()
+                   beta=1.0, stats_key=f"t.mrfst.{form}" if st else None)
+    stats = (out[1][0].clone().cpu(), out[1][1].clone().cpu()) if st else None
+    return yd.t.float().cpu(), stats, ref
+
+
+@pytest.mark.parametrize("form", ["lane16", "frag32"])
+@pytest.mark.parametrize("case", MRF_CASES)
+def test_mrf_persistent_conv(eng, case, form):
+    """MRF-family conv -- lane16: csrc/mrf.hip (LDS-DMA weight ring); frag32: csrc/mrfv.hip (register-direct
+    weight fragments) -- AdaIN + Snake / LeakyReLU / identity prologue, residual (at t / res_tdiv) / alpha /
+    acc_in epilogue and fused statistics vs the fp32 reference.  tolerance: max-abs error <= 1.5e-2 of
+    max|ref| (bf16 output); statistics 1e-5 of the stored tensor."""
+    st = case[9]
+    got, stats, ref = _run_mrf(eng, case, form)
     e = max_rel(got, ref)
-    print(case, "max_rel", e, "rel_l2", rel_err(got, ref))
+    print(case, form, "max_rel", e, "rel_l2", rel_err(got, ref))
     assert e < 1.5e-2
     if st:
-        _, (m, r, _) = out
-        y = yd.t.double().cpu()
+        m, r = stats
+        y = got.double()
         mr, vr = y.mean(1), y.var(1, unbiased=False)
-        assert float(((m.cpu().double() - mr).abs() / (mr.abs() + vr.sqrt())).max()) < 1e-5
-        assert max_rel(r.cpu(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
+        assert float(((m.double() - mr).abs() / (mr.abs() + vr.sqrt())).max()) < 1e-5
+        assert max_rel(r, 1 / torch.sqrt(vr + 1e-5)) < 1e-5
+
+
+@pytest.mark.parametrize("case", MRF_CASES)
+def test_mrf_frag32_bit_identical(eng, case):
+    """the register-direct kernel accumulates every output in the same K order from the same staged bf16
+    operands as the LDS-ring kernel: outputs and fused statistics are bit-identical (tolerance 0)."""
+    a, sa, _ = _run_mrf(eng, case, "lane16")
+    b, sb, _ = _run_mrf(eng, case, "frag32")
+    assert torch.equal(a, b)
+    if sa is not None:
+        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
 
 
 @pytest.mark.parametrize("B,T,Ci,Co,k", [(2, 3001, 128, 22, 7), (1, 300, 256, 32, 3), (3, 257, 128, 8, 7)])
@@ -314,6 +336,64 @@ def test_lstm(eng, tiny_params):
     e = max_rel(y.t.float().cpu(), ref)
     print("lstm", e)
     assert e < 2e-2
+
+
+def _v0_lstm(In=640, H=256, seed=9):
+    """random LSTM parameters at the v0 predictor width (pr_in 640 -> 2 x 256) and their packing."""
+    from stzs.weights import Arena, pack_lstm
+    g = torch.Generator().manual_seed(seed)
+    k = 1.0 / math.sqrt(H)
+    P = {}
+    for sfx in ("", "_rev"):
+        P["t.w_ih" + sfx] = (torch.rand(4 * H, In, generator=g) * 2 - 1) * k
+        P["t.w_hh" + sfx] = (torch.rand(4 * H, H, generator=g) * 2 - 1) * k
+        P["t.b_ih" + sfx] = (torch.rand(4 * H, generator=g) * 2 - 1) * k
+        P["t.b_hh" + sfx] = (torch.rand(4 * H, generator=g) * 2 - 1) * k
+    A = Arena()
+    lw = pack_lstm(A, "t", P)
+    A.finalize("cuda:0")
+    lw.ih.w, lw.ih.b, lw.whhT = A[lw.ih.w], A[lw.ih.b], A[lw.whhT]
+    return P, lw, A
+
+
+@pytest.mark.parametrize("B,T", [(64, 80), (40, 23), (1, 80)])
+def test_lstm_v0_width(eng, B, T):
+    """the benchmarked LSTM shape: H = 256 (8 exchanging workgroups per direction), up to 64 utterances per
+    group (4 MFMA row tiles, multi-row exchange loads) vs torch.nn.LSTM on identical bf16 inputs.
+    tolerance: max-abs error <= 2e-2 of max|ref| (bf16 h exchanged every step, fp32 cell state)."""
+    from oracle.stzs_ref import bilstm
+    from stzs.engine import Act
+    P, lw, _A = _v0_lstm()
+    g = torch.Generator().manual_seed(B * 1000 + T)
+    x = bf(torch.randn(B, T, 640, generator=g))
+    ref = bilstm(x, P, "t")
+    y = Act(torch.zeros(B, T, 512, dtype=torch.bfloat16, device="cuda:0"))
+    eng.lstm(lw, Act(x.to(torch.bfloat16).cuda()), y, f"t.lstm{B}")
+    assert eng.check_status() == 0
+    e = max_rel(y.t.float().cpu(), ref)
+    print("lstm v0", B, T, e, rel_err(y.t.float().cpu(), ref))
+    assert e < 2e-2
+
+
+def test_lstm_timeout_surfaces(eng):
+    """a spin that times out (forced: spin limit 1 poll) ORs STZS_STATUS_LSTM_TIMEOUT into the engine's
+    status word; check_status() raises on it and clears it, and a normal run afterwards is clean."""
+    from stzs.engine import Act
+    _P, lw, _A = _v0_lstm()
+    x = Act(torch.randn(8, 200, 640).to(torch.bfloat16).cuda())
+    y = Act(torch.zeros(8, 200, 512, dtype=torch.bfloat16, device="cuda:0"))
+    eng.check_status()
+    eng.lstm_spin_limit = 1
+    try:
+        for _ in range(3):  # 8 workgroups per direction x 199 hand-offs: some consumer always waits > 1 poll
+            eng.lstm(lw, x, y, "t.lstm_to")
+    finally:
+        eng.lstm_spin_limit = 0
+    with pytest.raises(RuntimeError, match="spin timed out"):
+        eng.check_status()
+    assert eng.check_status() == 0  # cleared by the raising check
+    eng.lstm(lw, x, y, "t.lstm_to")
+    assert eng.check_status() == 0
 
 
 def test_durations_alignment_gather_exact(eng):
