@@ -210,6 +210,7 @@ def main():
             graph = None
     run = graph.replay if graph is not None else step
     nstream = min(args.streams, B) if (graph is not None and args.streams > 1) else 1
+    twins = [eng]
     if nstream > 1:
         # the batch as `nstream` (near-)equal shards on engine twins (shared weights, own buffers), each captured as
         # two graphs -- front (text, prompt, style diffusion, prosody) and back (decoder) -- replayed on its
@@ -221,6 +222,7 @@ def main():
         pairs = []
         for i in range(nstream):
             tw = eng.twin()
+            twins.append(tw)
             sl = slice(sum(sizes[:i]), sum(sizes[:i + 1]))
             st_ = {}
 
@@ -276,6 +278,8 @@ def main():
         el = float(t.item())
     total_audio = world * B * audio_s * args.steps
     value = total_audio / el
+    # the LSTM exchange's spin-timeout words of every engine that ran (a timeout = wrong prosody, reported)
+    lstm_timeouts = sum(1 for tw in twins if int(tw.status.item()) != 0)
 
     # ---- roofline of the dominant kernel: instrumented eager pass, events on the kernel's stream ----
     eng.start_timer({"rb.c1", "rb.c2"})
@@ -368,6 +372,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "weight_broadcast_ms": round(bcast_ms, 3),
+            "lstm_timeouts": lstm_timeouts,
             "longform": lf,
             "precise_decoder": pr,
         }

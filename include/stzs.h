@@ -114,6 +114,12 @@ typedef struct stzs_conv_args {
  * Same prologue / epilogue contract as STZS_CONV_W_LANE16 with ks in {3, 7, 11} (Snake) or ks = 3
  * (LeakyReLU / identity), Co % 8 == 0; bit-identical results, no weight ring and no K-loop barrier. */
 #define STZS_CONV_W_FRAG32 256
+/* flags bit (FRAG32 weights): run the k3 single-chunk RESIDUAL convs on the persistent LDS-DMA-pipelined kernel
+ * (csrc/mrfp.hip) instead of the one-tile-per-workgroup register-direct one (csrc/mrfv.hip); bit-identical
+ * results.  Opt-in: per launch it is faster (stage-1 c2 324 vs 352 us, c2 + accumulate 298 vs 351 us), but in
+ * the two-stream bench the step time is unchanged and its resident persistent workgroups can hold back the
+ * co-resident LSTM launch of the concurrent stream. */
+#define STZS_CONV_MRF_PIPE 512
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------
@@ -190,7 +196,9 @@ typedef struct stzs_lstm_args {
     const void* whhT;
     void* y;
     void* xchg;  /* workspace: stzs_lstm_workspace(B, H, ndir) bytes, zero-initialised once */
-    void* sync;  /* workspace: 4096 bytes of arrival counters (zeroed by the call itself) */
+    void* sync;  /* workspace: 4096 bytes of arrival counters, zero-initialised ONCE by the caller; every call
+                  * leaves them zeroed (its last workgroup resets them), so no per-call memset is needed.
+                  * Calls sharing one sync buffer must be stream-ordered. */
     int64_t ldg, bsg, ldy, bsy;
     int32_t B, T, H, ndir;
     /* optional caller-owned status word: a spin that times out ORs STZS_STATUS_LSTM_TIMEOUT into it (the
@@ -355,6 +363,24 @@ typedef struct stzs_pool_args {
     int32_t B, T, L, C, in_dtype, out_dtype;
 } stzs_pool_args;
 int stzs_pool_rows(const stzs_pool_args* a, void* stream);
+
+/* ---- discrete style codes (README.md:5 "fixed-length time-varying discrete style codes") ----
+ * product vector quantiser over rows of C = G * dg fp32 values: group g of row r takes the codebook entry
+ *   k* = argmin_k d_k,  d_k = sum_{j < dg} (x[r, g*dg + j] - cb[g][k][j])^2
+ * accumulated serially over j with separately rounded IEEE sub / mul / add (no FMA contraction), the first
+ * minimum winning a tie -- so the indices are bit-exact against the oracle (oracle/stzs_ref.py quantize_codes).
+ * idx[r * ldi + g] = k*, y[r * ldy + g*dg + j] = cb[g][k*][j] (dequantised codes; y may alias x when ldy == ldx).
+ * lookup != 0: idx is an INPUT (teacher-forced discrete codes, clamped to [0, K)), only y is written and x is
+ * unused.  dg in {4, 8, 16}. */
+typedef struct stzs_vq_args {
+    const float* x;
+    const float* codebook; /* [G][K][dg] fp32 */
+    int32_t* idx;
+    float* y;
+    int64_t ldx, ldi, ldy;
+    int32_t R, G, K, dg, lookup, pad_i;
+} stzs_vq_args;
+int stzs_code_quantize(const stzs_vq_args* a, void* stream);
 
 /* ---- sampler glue ---- */
 /* c[r, j] = silu(pool[r, j] + temb[j]) -> bf16 */

@@ -8,7 +8,8 @@
 //                      the DFT itself is a bf16 MFMA GEMM through stzs_conv1d against a cos | -sin basis
 //                      (stzs/weights.py dft_basis), fp32 out;
 //   stzs_log_mel     : |X|^2 of the (re | im) rows, sparse mel filterbank (per-bin [k0, k1) ranges), log;
-//   stzs_pool_rows   : adaptive average pooling over time (torch.nn.functional.adaptive_avg_pool1d bounds).
+//   stzs_pool_rows   : adaptive average pooling over time (torch.nn.functional.adaptive_avg_pool1d bounds);
+//   stzs_code_quantize: the discrete style codes (README.md:5) -- product VQ of the projected prompt rows.
 #include "common.hpp"
 
 namespace {
@@ -67,7 +68,62 @@ __global__ __launch_bounds__(256) void pool_kernel(const stzs_pool_args a) {
     }
 }
 
+// One lane per (row, group), one wave per 64 rows of one group: every lane of a wave scans the same codebook,
+// so its entries are wave-uniform (scalar loads).  The distance is summed serially with explicitly rounded
+// sub / mul / add (the oracle's order); strict < keeps the first minimum.  ~R*G*K*dg*3 flops: negligible.
+template <int DG>
+__global__ __launch_bounds__(64) void vq_kernel(const stzs_vq_args a) {
+    const int r = blockIdx.x * 64 + threadIdx.x, g = blockIdx.y;
+    if (r >= a.R) return;  // no barriers in this kernel
+    const float* cb = a.codebook + (long)g * a.K * DG;
+    int best = 0;
+    if (!a.lookup) {
+        float x[DG];
+        const float* X = a.x + (long)r * a.ldx + g * DG;
+#pragma unroll
+        for (int j = 0; j < DG; ++j) x[j] = X[j];
+        float bd = __builtin_inff();
+        for (int k = 0; k < a.K; ++k) {
+            const float* c = cb + (long)k * DG;
+            float d = 0.f;
+#pragma unroll
+            for (int j = 0; j < DG; ++j) {
+                const float t = __fsub_rn(x[j], c[j]);
+                d = __fadd_rn(d, __fmul_rn(t, t));
+            }
+            if (d < bd) {
+                bd = d;
+                best = k;
+            }
+        }
+        a.idx[(long)r * a.ldi + g] = best;
+    } else {
+        best = min(max(a.idx[(long)r * a.ldi + g], 0), a.K - 1);
+    }
+    const float* c = cb + (long)best * DG;
+    float* Y = a.y + (long)r * a.ldy + g * DG;
+#pragma unroll
+    for (int j = 0; j < DG; ++j) Y[j] = c[j];
+}
+
 }  // namespace
+
+extern "C" int stzs_code_quantize(const stzs_vq_args* a, void* stream) {
+    if (!a || !a->codebook || !a->idx || !a->y || (!a->lookup && !a->x)) return STZS_EINVAL;
+    if (a->R <= 0 || a->G <= 0 || a->K <= 0 || a->ldi < a->G || a->ldy < (long)a->G * a->dg ||
+        (!a->lookup && a->ldx < (long)a->G * a->dg))
+        return STZS_ESHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    dim3 g((a->R + 63) / 64, a->G);
+    switch (a->dg) {
+        case 4: hipLaunchKernelGGL(vq_kernel<4>, g, dim3(64), 0, s, *a); break;
+        case 8: hipLaunchKernelGGL(vq_kernel<8>, g, dim3(64), 0, s, *a); break;
+        case 16: hipLaunchKernelGGL(vq_kernel<16>, g, dim3(64), 0, s, *a); break;
+        default: return STZS_ESHAPE;
+    }
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
 
 extern "C" int stzs_stft_frames(const stzs_frames_args* a, void* stream) {
     if (!a || !a->wav || !a->window || !a->y) return STZS_EINVAL;

@@ -183,6 +183,22 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         for (int i = 1; i < 6; ++i) ((unsigned long long*)a.sync)[256 + i] = pt[i];
 #endif
 #undef PROF
+    // leave the counters zeroed for the next call: the LAST workgroup to finish (told by its add to the
+    // done word) resets every arrival counter, the error word and the done word with agent-scope atomic
+    // stores.  Every other workgroup's last poll returned before its done add, so nothing reads a counter
+    // after its reset.  (A per-call hipMemsetAsync of the counters is NOT coherent with the pollers' sc1
+    // loads when replayed from a HIP graph: measured, every replay read stale counters, tools/lstm_det.py.)
+    __syncthreads();
+    if (tid == 0) {
+        gu32* done = (gu32*)(a.sync) + 1020;
+        const unsigned nwg = gridDim.x * gridDim.y * gridDim.z;
+        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
+            for (unsigned i = 0; i < gridDim.y * gridDim.z; ++i)
+                __hip_atomic_store((gu32*)(a.sync) + i * 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(err, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 }  // namespace
@@ -201,9 +217,8 @@ extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     const int P = a->H / UNITS;
     if (groups * a->ndir > 63 || P * a->ndir * groups > 256) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // counters (and the per-call error word) zeroed per call: a memset node under graph capture; the
-    // caller's status word (a->status) accumulates over calls and is never cleared here
-    if (hipMemsetAsync(a->sync, 0, 4096, s) != hipSuccess) return STZS_EHIP;
+    // the counters start at zero (caller-zeroed once) and every call leaves them zeroed (see the kernel's
+    // tail); the caller's status word (a->status) accumulates over calls and is never cleared here
     const int hp = a->H + 8;
     const size_t lds = ((MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4;
     dim3 grid(P, a->ndir, groups);

@@ -22,6 +22,7 @@ CONV_W_NARROW32 = 32  # include/stzs.h STZS_CONV_W_NARROW32
 CONV_W_FRAG32 = 256  # include/stzs.h STZS_CONV_W_FRAG32
 CONV_W_F32 = 64  # include/stzs.h STZS_CONV_W_F32 (precise mode)
 CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD remap)
+CONV_MRF_PIPE = 512  # include/stzs.h STZS_CONV_MRF_PIPE (k3 residual MRF convs on csrc/mrfp.hip, opt-in)
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -142,6 +143,11 @@ class PoolArgs(C.Structure):
                [(n, i32) for n in ("B", "T", "L", "C", "in_dtype", "out_dtype")]
 
 
+class VqArgs(C.Structure):
+    _fields_ = [("x", vp), ("codebook", vp), ("idx", vp), ("y", vp), ("ldx", i64), ("ldi", i64), ("ldy", i64)] + \
+               [(n, i32) for n in ("R", "G", "K", "dg", "lookup", "pad_i")]
+
+
 class CopyArgs(C.Structure):
     _fields_ = [("x", vp), ("y", vp)] + [(n, i64) for n in ("ldx", "bsx", "ldy", "bsy")] + \
                [(n, i32) for n in ("B", "R", "C", "in_dtype", "out_dtype", "pad_i")]
@@ -152,7 +158,7 @@ EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_ch
            "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
-           "stzs_stft_frames", "stzs_log_mel", "stzs_pool_rows",
+           "stzs_stft_frames", "stzs_log_mel", "stzs_pool_rows", "stzs_code_quantize",
            "stzs_dn_cond", "stzs_dn_cond_steps", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed"]
 
@@ -199,6 +205,7 @@ def load():
         "stzs_stft_frames": ([P(FramesArgs), vp], i32),
         "stzs_log_mel": ([P(LogMelArgs), vp], i32),
         "stzs_pool_rows": ([P(PoolArgs), vp], i32),
+        "stzs_code_quantize": ([P(VqArgs), vp], i32),
         "stzs_dn_cond_steps": ([vp, vp, vp, i32, i32, i32, vp], i32),
         "stzs_dn_cond":([vp, vp, vp, i32, i32, vp], i32),
         "stzs_adaln_expand": ([vp, vp, vp, i32, i32, i32, i32, C.c_uint32, vp], i32),

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -127,9 +128,12 @@ class StyleTTSZS:
         self._ws = None
         self.launches = 0
         self.lstm_spin_limit = 0  # 0 = the library default; tests force tiny values
+        # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
+        self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
         # graph-replayed); check_status() reads it and raises
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.prompt_idx = None  # discrete prompt codes of the last prompt_encode (device int32 [B, L_s, G])
 
     def check_status(self, reset=True):
         """raise RuntimeError if any LSTM exchange since the last check timed out (its h-states are wrong).
@@ -228,7 +232,7 @@ class StyleTTSZS:
             flags |= L.CONV_W_LANE16  # MRF-family kernel (csrc/mrf.hip)
         elif getattr(cw, "narrow32", False):
             flags |= L.CONV_W_NARROW32  # narrow conv (csrc/mrf.hip)
-        a.flags = flags
+        a.flags = flags | self.conv_flags
         st = None
         if stats_key is not None:
             Cc = _rup(cw.Co, 8)
@@ -356,7 +360,9 @@ class StyleTTSZS:
 
     # ------------------------------------------------------------------ front ends
     def text_encode(self, tokens: torch.Tensor) -> Act:
-        """tokens int32 [B, T] (device) -> h_txt bf16 [B, T, d_txt]; HIP (embed + conv + LN)."""
+        """tokens int32 [B, T] (device) -> h_txt bf16 [B, T, d_txt] (StyleTTS2 TextEncoder):
+        embedding gather, te_layers x (k5 conv on MFMA, LayerNorm + LeakyReLU 0.2), then the BiLSTM
+        (input projection on MFMA + the register-resident exchange recurrence of csrc/lstm.hip)."""
         S, W = self.spec, self.W
         B, T = tokens.shape
         e = self.act("te.e", B, T, S.d_txt)
@@ -369,7 +375,8 @@ class StyleTTSZS:
             g, b = W.te_ln[i]
             self.rowln(c, e, G=W.t(g).data_ptr(), gs=0, Bt=W.t(b).data_ptr(), bs=0, gadd=0.0,
                        act=L.ACT_LEAKY, slope=0.2, what=f"te.ln{i}")
-        return e
+        h = self.act("te.h", B, T, S.d_txt)
+        return self.lstm(W.te_lstm, e, h, "te.lstm")
 
     def log_mel(self, wav: torch.Tensor, dtype=torch.bfloat16) -> Act:
         """reference wav fp32 [B, N] (device) -> log-mel [B, N/hop + 1, n_mels]:
@@ -396,9 +403,43 @@ class StyleTTSZS:
         self._call(self.lib.stzs_log_mel, a, "log_mel")
         return mel
 
-    def prompt_encode(self, ref_wav: torch.Tensor) -> torch.Tensor:
-        """reference-prompt front end on HIP: ref wav [B, N] -> codes fp32 [B, L_s, code].
-        log-mel -> 2 x (k5 conv + LeakyReLU 0.2) -> adaptive average pool to L_s rows -> projection."""
+    def prompt_encode(self, ref_wav: torch.Tensor, prompt_idx: torch.Tensor = None) -> torch.Tensor:
+        """reference-prompt front end on HIP: ref wav [B, N] -> DISCRETE style codes
+        (README.md:5): log-mel -> 2 x (k5 conv + LeakyReLU 0.2) -> adaptive average pool to L_s rows ->
+        projection -> product VQ (stzs_code_quantize).  Returns the dequantised codes fp32 [B, L_s, code];
+        the indices stay in self.prompt_idx [B, L_s, G] (int32).  prompt_idx: teacher-forced indices (the
+        front end is skipped, the codebook rows are gathered)."""
+        S, W = self.spec, self.W
+        G = S.code_dim // S.vq_group
+        if prompt_idx is not None:
+            B = prompt_idx.shape[0]
+            idx = self.buf("prompt.idx", (B, S.L_s, G), torch.int32)
+            idx.copy_(prompt_idx.to(torch.int32).reshape(B, S.L_s, G))
+            out = self.buf("prompt", (B, S.L_s, S.code_dim), torch.float32)
+            self.code_quantize(None, idx, out, lookup=True)
+            self.prompt_idx = idx
+            return out
+        z = self.prompt_features(ref_wav)
+        B = z.shape[0]
+        idx = self.buf("prompt.idx", (B, S.L_s, G), torch.int32)
+        out = self.buf("prompt", (B, S.L_s, S.code_dim), torch.float32)
+        self.code_quantize(z, idx, out)
+        self.prompt_idx = idx
+        return out
+
+    def code_quantize(self, z, idx: torch.Tensor, out: torch.Tensor, lookup=False):
+        """product VQ of z fp32 [B, L, code] -> idx int32 [B, L, G] + dequantised rows out (lookup: idx given)."""
+        S, W = self.spec, self.W
+        a = L.VqArgs()
+        a.x = z.data_ptr() if z is not None else None
+        a.codebook, a.idx, a.y = W.t(W.pe_vq).data_ptr(), idx.data_ptr(), out.data_ptr()
+        G = S.code_dim // S.vq_group
+        a.ldx, a.ldi, a.ldy = S.code_dim, G, S.code_dim
+        a.R, a.G, a.K, a.dg, a.lookup = idx.shape[0] * idx.shape[1], G, S.vq_size, S.vq_group, int(lookup)
+        self._call(self.lib.stzs_code_quantize, a, "code_quantize")
+
+    def prompt_features(self, ref_wav: torch.Tensor) -> torch.Tensor:
+        """ref wav [B, N] -> continuous prompt codes fp32 [B, L_s, code] (before the quantiser)."""
         S, W = self.spec, self.W
         wav = ref_wav.to(self.device, torch.float32).contiguous()
         B = wav.shape[0]
@@ -413,20 +454,54 @@ class StyleTTSZS:
         a.x, a.y, a.ldx, a.bsx, a.ldy, a.bsy = c1.ptr, pooled.ptr, c1.ld, c1.bs, pooled.ld, pooled.bs
         a.B, a.T, a.L, a.C, a.in_dtype, a.out_dtype = B, Fr, S.L_s, S.pe_ch, L.BF16, L.BF16
         self._call(self.lib.stzs_pool_rows, a, "pool_rows")
-        out = self.buf("prompt", (B, S.L_s, S.code_dim), torch.float32)
+        out = self.buf("prompt.z", (B, S.L_s, S.code_dim), torch.float32)
         self.conv(W.pe_proj, pooled, Act(out), what="pe.proj")
         return out
 
     # ------------------------------------------------------------------ (a) style diffusion
     def sample_style(self, h_txt: Act, prompt: torch.Tensor, eps: torch.Tensor, steps: int,
                      cfg_scale: float = 1.0) -> torch.Tensor:
+        """a1-a4: Euler sampling over the distilled / Karras sigma schedule with classifier-free guidance.
+        h_txt [B, T, d_txt] bf16, prompt [B, L_s, code] fp32, eps [B, L_s, code] -> codes fp32 [B, L_s, code]."""
+        S = self.spec
+        B = h_txt.B
+        cfg = cfg_scale != 1.0
+        R = 2 * B if cfg else B
+        sig = sigma_schedule(S, steps)
+        st = self.denoiser_prepare(h_txt, prompt, sig[:steps], cfg)
+        x = self.buf("dn.x", (R, S.L_s, S.code_dim), torch.float32)
+        N = S.L_s * S.code_dim
+        self.launches += 1
+        L.check(self.lib.stzs_state_init(x.data_ptr(), eps.data_ptr(), B, N, int(cfg), float(sig[0]), self.stream()),
+                "state_init")
+        D = self.act("dn.D", R, S.L_s, S.code_dim, torch.float32)
+        for i in range(steps):
+            self.denoiser_step(st, i, Act(x), D)
+            self.launches += 1
+            L.check(self.lib.stzs_cfg_euler(x.data_ptr(), D.t.data_ptr(), B, N, int(cfg), float(cfg_scale),
+                                            float(sig[i]), float(sig[i + 1] - sig[i]), self.stream()), "cfg_euler")
+        return x[:B]
+
+    def denoiser_fwd(self, h_txt: Act, prompt: torch.Tensor, x: torch.Tensor, sigma: float, cfg: bool) -> torch.Tensor:
+        """a2 alone: ONE preconditioned denoiser evaluation D(x, sigma) (EDM c_skip / c_out / c_in / c_noise) on the
+        rows x [R, L_s, code] fp32 (R = 2B with CFG: conditional rows, then the null-prompt rows) -> D fp32
+        [R, L_s, code] (a device buffer of the engine)."""
+        S = self.spec
+        st = self.denoiser_prepare(h_txt, prompt, [float(sigma)], cfg)
+        D = self.act("dn.D", x.shape[0], S.L_s, S.code_dim, torch.float32)
+        self.denoiser_step(st, 0, Act(x), D)
+        return D.t
+
+    def denoiser_prepare(self, h_txt: Act, prompt: torch.Tensor, sigmas, cfg: bool) -> dict:
+        """step-invariant part of a sampling run: the cross-attention context [ctx_txt(h) ; ctx_prm(prompt | null)]
+        and its per-layer K/V, the pooled prompt, and the conditioning of EVERY sigma at once (rows s * R + r):
+        adaLN-single input, its two projections and the per-layer expansion -> 5 launches instead of 5 per NFE."""
         S, W = self.spec, self.W
         B, T = h_txt.B, h_txt.T
-        cfg = cfg_scale != 1.0
         R = 2 * B if cfg else B
         Ls, d, cd = S.L_s, S.dn_d, S.code_dim
         Lc = T + Ls
-        # context (once per batch): [ctx_txt(h) ; ctx_prm(prompt | null)]
+        steps = len(sigmas)
         ctx = self.act("dn.ctx", R, Lc, d)
         # ctx_txt rows: the conv writes T rows per utterance into a buffer of Lc rows per utterance
         self._conv_rows(W.dn_ctx_txt, h_txt, ctx.t, 0, 0, "dn.ctx_txt")
@@ -456,24 +531,15 @@ class StyleTTSZS:
             self.conv(lw["kv"], ctx, kvl, what=f"dn.kv{l}")
             kv.append(kvl)
         # sigma embeddings for all steps
-        sig = sigma_schedule(S, steps)
-        fkey = ("dn.four", steps)
+        fkey = ("dn.four", tuple(float(v) for v in sigmas))
         fo = self._consts.get(fkey)
         if fo is None:  # host constant, uploaded once (never inside a graph capture)
-            four = np.stack([fourier_features(S, edm_coeffs(S, s)["c_noise"]) for s in sig[:steps]])
+            four = np.stack([fourier_features(S, edm_coeffs(S, v)["c_noise"]) for v in sigmas])
             fo = self._consts[fkey] = torch.from_numpy(four)[None].to(self.device)
         t0 = self.act("dn.t0", 1, steps, d, torch.float32)
         temb = self.act("dn.temb", 1, steps, d, torch.float32)
         self.conv(W.dn_t0, Act(fo), t0, epi_act=L.ACT_SILU, what="dn.t0")
         self.conv(W.dn_t1, t0, temb, what="dn.t1")
-        # state
-        x = self.buf("dn.x", (R, Ls, cd), torch.float32)
-        N = Ls * cd
-        self.launches += 1
-        L.check(self.lib.stzs_state_init(x.data_ptr(), eps.data_ptr(), B, N, int(cfg), float(sig[0]), self.stream()),
-                "state_init")
-        # step-invariant conditioning of the whole run, all steps at once (rows s * R + r): adaLN-single
-        # input, its two projections and the per-layer expansion -> 5 launches total instead of 5 per NFE
         cb = self.buf("dn.cb", (steps * R, d), torch.bfloat16)
         mod = self.buf("dn.mod", (steps * R, 6 * d), torch.float32)
         fmod = self.buf("dn.fmod", (steps * R, 2 * d), torch.float32)
@@ -489,14 +555,20 @@ class StyleTTSZS:
                                            6, S.dn_layers, 0b010010, self.stream()), "adaln_expand")
         L.check(self.lib.stzs_adaln_expand(fmod.data_ptr(), None, fmodx.data_ptr(), steps * R, d, 2, 1, 0b10,
                                            self.stream()), "adaln_expand.f")
+        return dict(R=R, sig=list(sigmas), kv=kv, modx=modx, fmodx=fmodx)
+
+    def denoiser_step(self, st: dict, i: int, xa: Act, D: Act):
+        """one NFE: D = c_skip x + c_out F(c_in x, sigma_i) for the R rows of xa, with the conditioning prepared
+        by denoiser_prepare (6 layers: adaLN-modulated self-attention, cross-attention, GELU FFN)."""
+        S, W = self.spec, self.W
+        R, kv, modx, fmodx = st["R"], st["kv"], st["modx"], st["fmodx"]
+        Ls, d = S.L_s, S.dn_d
         h = self.act("dn.h", R, Ls, d, torch.float32)
         an = self.act("dn.a", R, Ls, d)
         qkv = self.act("dn.qkv", R, Ls, 3 * d)
         o = self.act("dn.o", R, Ls, d)
         q = self.act("dn.q", R, Ls, d)
         ff = self.act("dn.ff", R, Ls, S.dn_ffn)
-        D = self.act("dn.D", R, Ls, cd, torch.float32)
-        xa = Act(x)
         pos = Act(W.t(W.dn_pos)[None])
         fsz = 4
         f8 = self.fp8_denoiser
@@ -507,54 +579,48 @@ class StyleTTSZS:
             s_an = self.buf("dn.a8s", (R * Ls,), torch.float32)
             s_o = self.buf("dn.o8s", (R * Ls,), torch.float32)
             s_ff = self.buf("dn.ff8s", (R * Ls,), torch.float32)
-        for i in range(steps):
-            s0 = sig[i]
-            co = edm_coeffs(S, s0)
-            self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, what="dn.in")
+        co = edm_coeffs(S, st["sig"][i])
+        self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, what="dn.in")
+        if f8:
+            ain, sin, sfx = an8, s_an, "8"
+        else:
+            ain, sin, sfx = an, None, ""
+        # adaLN / LayerNorm rows of this step: ln1_l, ca_ln_l, ln2_l for every layer, then lnf; each one
+        # after the first is launched right behind the residual linear that produces its input (post_ln).
+        # (Fusing them into that linear's epilogue -- last-arriving tile of a row block, sc1 hand-off --
+        # was tried: bit-identical but 1.6x slower at batch 1, the block's rows then normalise on one CU.)
+        lns = []
+        for l, lw in enumerate(W.dn_layers):
+            mb = modx[l, i * R].data_ptr()  # this step's rows of layer l's modulation
+            lns.append(self._ln_args(h, ain, G=mb + d * fsz, gs=6 * d, Bt=mb, bs=6 * d, gdiv=Ls, y_scale=sin))
+            lns.append(self._ln_args(h, ain, G=W.t(lw["ln_g"]).data_ptr(), Bt=W.t(lw["ln_b"]).data_ptr(),
+                                     y_scale=sin))
+            lns.append(self._ln_args(h, ain, G=mb + 4 * d * fsz, gs=6 * d, Bt=mb + 3 * d * fsz, bs=6 * d, gdiv=Ls,
+                                     y_scale=sin))
+        fb = fmodx[0, i * R].data_ptr()
+        lns.append(self._ln_args(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls))
+        self._call(self.lib.stzs_row_layernorm, lns[0], "ln1")
+        for l, lw in enumerate(W.dn_layers):
+            mb = modx[l, i * R].data_ptr()
+            self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, what="qkv")
+            self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
+            xo, so = (o8, s_o) if f8 else (o, None)
             if f8:
-                ain, sin, sfx = an8, s_an, "8"
-            else:
-                ain, sin, sfx = an, None, ""
-            # adaLN / LayerNorm rows of this step: ln1_l, ca_ln_l, ln2_l for every layer, then lnf; each one
-            # after the first is launched right behind the residual linear that produces its input (post_ln).
-            # (Fusing them into that linear's epilogue -- last-arriving tile of a row block, sc1 hand-off --
-            # was tried: bit-identical but 1.6x slower at batch 1, the block's rows then normalise on one CU.)
-            lns = []
-            for l, lw in enumerate(W.dn_layers):
-                mb = modx[l, i * R].data_ptr()  # this step's rows of layer l's modulation
-                lns.append(self._ln_args(h, ain, G=mb + d * fsz, gs=6 * d, Bt=mb, bs=6 * d, gdiv=Ls, y_scale=sin))
-                lns.append(self._ln_args(h, ain, G=W.t(lw["ln_g"]).data_ptr(), Bt=W.t(lw["ln_b"]).data_ptr(),
-                                         y_scale=sin))
-                lns.append(self._ln_args(h, ain, G=mb + 4 * d * fsz, gs=6 * d, Bt=mb + 3 * d * fsz, bs=6 * d, gdiv=Ls,
-                                         y_scale=sin))
-            fb = fmodx[0, i * R].data_ptr()
-            lns.append(self._ln_args(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls))
-            self._call(self.lib.stzs_row_layernorm, lns[0], "ln1")
-            for l, lw in enumerate(W.dn_layers):
-                mb = modx[l, i * R].data_ptr()
-                self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, what="qkv")
-                self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
-                xo, so = (o8, s_o) if f8 else (o, None)
-                if f8:
-                    self.quant(o, o8, s_o)
-                self.conv(lw["o" + sfx], xo, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=so,
-                          post_ln=lns[3 * l + 1], what="sa_o")
-                self.conv(lw["q" + sfx], ain, q, x_scale=sin, what="ca_q")
-                self.attention(q, kv[l].sl(0, d), kv[l].sl(d, d), o)
-                if f8:
-                    self.quant(o, o8, s_o)
-                self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=lns[3 * l + 2], what="ca_o")
-                self.conv(lw["ff1" + sfx], ain, ff, epi_act=L.ACT_GELU, x_scale=sin, what="ff1")
-                xf, sf = (ff8, s_ff) if f8 else (ff, None)
-                if f8:
-                    self.quant(ff, ff8, s_ff)
-                self.conv(lw["ff2" + sfx], xf, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=sf,
-                          post_ln=lns[3 * l + 3], what="ff2")
-            self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], what="dn.out")
-            self.launches += 1
-            L.check(self.lib.stzs_cfg_euler(x.data_ptr(), D.t.data_ptr(), B, N, int(cfg), float(cfg_scale),
-                                            float(s0), float(sig[i + 1] - s0), self.stream()), "cfg_euler")
-        return x[:B]
+                self.quant(o, o8, s_o)
+            self.conv(lw["o" + sfx], xo, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=so,
+                      post_ln=lns[3 * l + 1], what="sa_o")
+            self.conv(lw["q" + sfx], ain, q, x_scale=sin, what="ca_q")
+            self.attention(q, kv[l].sl(0, d), kv[l].sl(d, d), o)
+            if f8:
+                self.quant(o, o8, s_o)
+            self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=lns[3 * l + 2], what="ca_o")
+            self.conv(lw["ff1" + sfx], ain, ff, epi_act=L.ACT_GELU, x_scale=sin, what="ff1")
+            xf, sf = (ff8, s_ff) if f8 else (ff, None)
+            if f8:
+                self.quant(ff, ff8, s_ff)
+            self.conv(lw["ff2" + sfx], xf, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=sf,
+                      post_ln=lns[3 * l + 3], what="ff2")
+        self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], what="dn.out")
 
     def _ln_args(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=0.0, y_scale=None):
         """stzs_rowln_args of a modulated LayerNorm x -> y (launched by stzs_row_layernorm, or fused into a
@@ -653,6 +719,15 @@ class StyleTTSZS:
             self.copy2d(e16, enc_in, T40, S.d_txt)
         else:
             self.gather(h_txt, idx, enc_in, S.d_txt)
+        F0, Nn = self.f0n_predictor(en, codes)
+        out = dict(extra or {}, dur=dur, idx=idx, T40=T40, en=en, asr_buf=enc_in, d=d, F0=F0, N=Nn)
+        return out
+
+    def f0n_predictor(self, en: Act, codes: torch.Tensor):
+        """a8: shared BiLSTM over the aligned frames, then per branch (F0, N) three AdaIN residual blocks (the
+        middle one x2 upsampling) and a 1x1 projection.  en [B, T40, pr_in] bf16 -> F0, N fp32 [B, 2 T40]."""
+        S, W = self.spec, self.W
+        B, T40 = en.B, en.T
         xs = self.act("pr.xs", B, T40, S.pr_hid)
         self.lstm(W.pr_shared, en, xs, "pr.shared")
         sg = self.mean_rows(codes, S.style_ac, S.style_pr, "pr.sg")
@@ -671,8 +746,7 @@ class StyleTTSZS:
             self.blk(W.pr_blk[f"pr.{br}1"], y0, y1, ng, gbp, f"pr.{br}1")
             self.blk(W.pr_blk[f"pr.{br}2"], y1, y2, ng, gbp, f"pr.{br}2")
             self.conv(W.pr_blk[f"pr.{br}_proj"], y2, Act(out, 0, 1), what=f"pr.{br}_proj")
-        out = dict(extra or {}, dur=dur, idx=idx, T40=T40, en=en, asr_buf=enc_in, d=d, F0=F0[:, :, 0], N=Nn[:, :, 0])
-        return out
+        return F0[:, :, 0], Nn[:, :, 0]
 
     def gather(self, x: Act, idx, y: Act, Cn):
         a = L.GatherArgs()
@@ -715,14 +789,30 @@ class StyleTTSZS:
 
     # ------------------------------------------------------------------ (c) decoder
     def decode(self, pro: dict, codes: torch.Tensor, seeds, istft=True) -> torch.Tensor:
+        """a9-a13: decoder pre-blocks, generator, conv_post + iSTFT.  pro: asr_buf (aligned text features in the
+        decoder input buffer), F0 / N [B, T80], T40 -> wav fp32 [B, 600 T40] (or conv_post rows, istft=False)."""
+        gen_in, gbd = self.decoder_pre(pro, codes)
+        return self.generator(gen_in, pro["F0"], seeds, gbd, istft=istft)
+
+    def dec_style(self, codes: torch.Tensor) -> torch.Tensor:
+        """every AdaIN gamma / beta of the decoder from the pooled acoustic codes: ONE GEMM -> [B, total] fp32."""
         S, W = self.spec, self.W
-        enc_in, F0, Nn, T40 = pro["asr_buf"], pro["F0"], pro["N"], pro["T40"]
-        B = enc_in.B
-        T80 = 2 * T40
+        B = codes.shape[0]
         sa = self.mean_rows(codes, 0, S.style_ac, "dec.sa")
         ng = W.dec_norm
         gbd = self.buf("dec.gbn", (B, ng.total), torch.float32)
         self.conv(ng.lin, Act(sa[:, None]), Act(gbd[:, None]), what="dec.norms")
+        return gbd
+
+    def decoder_pre(self, pro: dict, codes: torch.Tensor):
+        """a9: F0 / N stride-2 convs, asr_res, the encode block and the four decode blocks (1024 channels,
+        the last one x2 upsampling) -> (generator input [B, T80, dec_out], decoder AdaIN gammas/betas)."""
+        S, W = self.spec, self.W
+        enc_in, F0, Nn, T40 = pro["asr_buf"], pro["F0"], pro["N"], pro["T40"]
+        B = enc_in.B
+        T80 = 2 * T40
+        gbd = self.dec_style(codes)
+        ng = W.dec_norm
         dcat = S.dec_enc + 2 + S.dec_asr_res
         dt = self.dec_dt
         cats = [self.act("dec.catA", B, T40, dcat, dt), self.act("dec.catB", B, T40, dcat, dt)]
@@ -746,19 +836,20 @@ class StyleTTSZS:
             src = 1 - src
         gen_in = self.act("dec.gen_in", B, T80, S.dec_out, dt)
         self.blk(W.dec_blk["dec.decode3"], Act(cats[src].t, 0, dcat), gen_in, ng, gbd, "dec.decode3", dt)
-        return self.generator(gen_in, F0, seeds, gbd, istft=istft)
+        return gen_in, gbd
 
-    def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None, istft=True):
+    def sine_gen(self, F0: torch.Tensor, seeds) -> Act:
+        """a10: NSF harmonic source from F0 [B, T80] (SineGen: fp64 frame-rate phase prefix, counter-RNG noise,
+        Linear(9->1) + tanh) and its n_fft-point STFT (real | imag) -> har [B, Tf, har_ch] (csrc/source.hip)."""
         S, W = self.spec, self.W
-        B, T80 = x.B, x.T
-        ng = W.dec_norm
+        B, T80 = F0.shape[0], F0.shape[1]
         N = T80 * S.hop
         Tf = N // S.istft_hop + 1
         nh = S.harmonic_num + 1
         if isinstance(seeds, torch.Tensor) and seeds.device.type != "cpu":
             sd = seeds.to(torch.int32)
         else:
-            skey = ("seeds", tuple(int(s) for s in seeds))
+            skey = ("seeds", tuple(int(v) for v in seeds))
             sd = self._consts.get(skey)
             if sd is None:  # uploaded once per distinct seed list (graph-capture safe afterwards)
                 host = torch.as_tensor(np.asarray(seeds, dtype=np.uint32).view(np.int32).copy())
@@ -775,37 +866,43 @@ class StyleTTSZS:
         a.sr, a.sine_amp, a.noise_std, a.voiced_thr = float(S.sr), S.sine_amp, S.noise_std, S.voiced_threshold
         a.har_dtype = har.dt
         self._call(self.lib.stzs_harmonic_source, a, "harmonic_source")
-        if trace is not None:
-            trace["har"] = har
+        return har
+
+    def upsample(self, x: Act, har: Act, i: int) -> Act:
+        """a11: generator stage i's noise conv of the harmonic features + LeakyReLU(0.1) -> polyphase
+        ConvTranspose1d(k = 2 r, s = r) (+ ReflectionPad(1,0) on the last stage) + the noise conv as residual."""
+        S, W = self.spec, self.W
+        B = x.B
         n_up = len(S.up_rates)
-        Tcur = T80
-        for i, (r, k) in enumerate(zip(S.up_rates, S.up_kernels)):
-            c = S.gen_ch[i]
-            last = i == n_up - 1
-            Tn = Tcur * r + (1 if last else 0)
-            xsrc = self.act(f"gen.xsrc{i}", B, Tn, c, dt)
-            if not last:
-                sf0 = int(np.prod(S.up_rates[i + 1:]))
-                self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, stride=sf0, pad=(sf0 + 1) // 2,
-                          what=f"noise_conv{i}")
-            else:
-                self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, what=f"noise_conv{i}")
-            xu = self.act(f"gen.x{i}", B, Tn, c, dt)
-            self.conv(W.ups[i], x, xu, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=(k - r) // 2, T_final=Tcur * r,
-                      refl=1 if last else 0, res=xsrc, what=f"ups{i}")
-            if trace is not None:
-                trace[f"mrf_in{i}"] = xu
-            x = self.mrf(xu, i, gbd, ng)
-            if trace is not None:
-                trace[f"mrf_out{i}"] = x
-            Tcur = Tn
-        post = self.act("gen.post", B, Tcur, S.har_ch, torch.float32)
+        r, k = S.up_rates[i], S.up_kernels[i]
+        c = S.gen_ch[i]
+        last = i == n_up - 1
+        Tcur = x.T
+        Tn = Tcur * r + (1 if last else 0)
+        dt = self.dec_dt
+        xsrc = self.act(f"gen.xsrc{i}", B, Tn, c, dt)
+        if not last:
+            sf0 = int(np.prod(S.up_rates[i + 1:]))
+            self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, stride=sf0, pad=(sf0 + 1) // 2, what=f"noise_conv{i}")
+        else:
+            self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, what=f"noise_conv{i}")
+        xu = self.act(f"gen.x{i}", B, Tn, c, dt)
+        self.conv(W.ups[i], x, xu, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=(k - r) // 2, T_final=Tcur * r,
+                  refl=1 if last else 0, res=xsrc, what=f"ups{i}")
+        return xu
+
+    def conv_post(self, x: Act) -> Act:
+        """LeakyReLU(0.01) + conv_post (128 -> 22, k7) -> fp32 rows [B, Tf, 22] (log-magnitude | phase argument)."""
+        S, W = self.spec, self.W
+        post = self.act("gen.post", x.B, x.T, S.har_ch, torch.float32)
         self.conv(W.conv_post, x, Act(post.t, 0, S.har_ch), pad=3, pro_act=L.ACT_LEAKY, pro_slope=0.01,
                   what="conv_post")
-        if trace is not None:
-            trace["post"] = post
-        if not istft:
-            return post
+        return post
+
+    def istft(self, post: Act) -> torch.Tensor:
+        """a13: exp / sin spectrum, 20-point irfft, Hann overlap-add (hop 5), window-envelope normalisation."""
+        S = self.spec
+        B, Tcur = post.B, post.T
         Nout = (Tcur - 1) * S.istft_hop
         wav = self.buf("gen.wav", (B, Nout), torch.float32)
         a = L.IstftArgs()
@@ -813,6 +910,28 @@ class StyleTTSZS:
         a.B, a.Tf, a.n_fft, a.hop_s = B, Tcur, S.n_fft, S.istft_hop
         self._call(self.lib.stzs_istft, a, "istft")
         return wav
+
+    def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None, istft=True):
+        """a10-a13: harmonic source, per stage the noise conv + ConvTranspose up-sampling and the MRF, then
+        conv_post and the iSTFT."""
+        S, W = self.spec, self.W
+        ng = W.dec_norm
+        har = self.sine_gen(F0, seeds)
+        if trace is not None:
+            trace["har"] = har
+        for i in range(len(S.up_rates)):
+            xu = self.upsample(x, har, i)
+            if trace is not None:
+                trace[f"mrf_in{i}"] = xu
+            x = self.mrf(xu, i, gbd, ng)
+            if trace is not None:
+                trace[f"mrf_out{i}"] = x
+        post = self.conv_post(x)
+        if trace is not None:
+            trace["post"] = post
+        if not istft:
+            return post
+        return self.istft(post)
 
     def istft_stream(self, post: Act, chunk_frames: int):
         """iSTFT of conv_post frames [B, Tf, 22] in chunks of `chunk_frames` frames,
@@ -905,16 +1024,18 @@ class StyleTTSZS:
         return g, out
 
     def synth(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None, codes=None,
-              n_frames=None):
+              n_frames=None, prompt_idx=None):
         """tokens int [B, T_txt]; ref_wav fp32 [B|1, N]; noise fp32 [B, L_s, code]; durations int [B, T_txt]
         (host tensor, or device tensor + n_frames: no device sync); seeds: per-utterance source-noise
-        seeds.  -> dict(wav=[B, 600*T40], ...)"""
+        seeds; prompt_idx: teacher-forced discrete prompt codes [B|1, L_s, G] (ref_wav then unused).
+        -> dict(wav=[B, 600*T40], prompt_idx=[B|1, L_s, G], ...)"""
         S = self.spec
         dev = self.device
         tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
         B = tokens.shape[0]
         h = self.text_encode(tokens)
-        prompt = self.prompt_encode(ref_wav.to(dev))
+        prompt = self.prompt_encode(None if ref_wav is None else ref_wav.to(dev), prompt_idx)
+        pidx = self.prompt_idx
         if prompt.shape[0] == 1 and B > 1:
             pe = self.buf("prompt.bc", (B, S.L_s, S.code_dim), torch.float32)
             pe.copy_(prompt.expand(B, -1, -1))
@@ -925,11 +1046,11 @@ class StyleTTSZS:
         pro = self.predict_prosody(h, codes, durations, n_frames)
         seeds = list(range(B)) if seeds is None else seeds
         wav = self.decode(pro, codes, seeds)
-        return dict(wav=wav, codes=codes, h_txt=h, prompt=prompt, **pro)
+        return dict(wav=wav, codes=codes, h_txt=h, prompt=prompt, prompt_idx=pidx, **pro)
 
 
     def synth_stream(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None,
-                     codes=None, n_frames=None, chunk_s=1.0):
+                     codes=None, n_frames=None, chunk_s=1.0, prompt_idx=None):
         """configs[4] long-form synthesis with the streaming iSTFT decoder: the text,
         style, prosody and conv stack run over the whole target (AdaIN instance statistics are
         utterance-global), then the waveform is emitted in `chunk_s`-second chunks.  Yields
@@ -939,7 +1060,7 @@ class StyleTTSZS:
         tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
         B = tokens.shape[0]
         h = self.text_encode(tokens)
-        prompt = self.prompt_encode(ref_wav.to(dev))
+        prompt = self.prompt_encode(None if ref_wav is None else ref_wav.to(dev), prompt_idx)
         if prompt.shape[0] == 1 and B > 1:
             pe = self.buf("prompt.bc", (B, S.L_s, S.code_dim), torch.float32)
             pe.copy_(prompt.expand(B, -1, -1))

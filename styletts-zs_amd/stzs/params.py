@@ -101,7 +101,7 @@ def param_shapes(spec: Spec) -> "OrderedDict[str, torch.Size]":
 def _declare(I: _Init, spec: Spec) -> "OrderedDict[str, torch.Tensor]":
     S = spec
     sty = S.style_ac
-    # ---- text encoder (front end; StyleTTS2 TextEncoder CNN part) ----
+    # ---- text encoder (front end; StyleTTS2 TextEncoder CNN part; its BiLSTM is declared last) ----
     I.nrm("te.emb", (S.n_symbols, S.d_txt), 1.0)
     for i in range(S.te_layers):
         I.conv(f"te.conv{i}", S.d_txt, S.d_txt, S.te_kernel)
@@ -184,6 +184,11 @@ def _declare(I: _Init, spec: Spec) -> "OrderedDict[str, torch.Tensor]":
                 I.conv(p + ".c2", c, c, kr)
         cin = c
     I.conv("gen.conv_post", S.har_ch, S.gen_ch[-1], 7)
+    # ---- round-2 additions, declared last so every earlier parameter keeps its seeded value ----
+    # text encoder BiLSTM after the CNN stack (StyleTTS2 TextEncoder: CNN + BiLSTM)
+    I.lstm("te.lstm", S.d_txt, S.d_txt // 2)
+    # discrete style-code codebooks [groups][entries][group width] (README.md:5)
+    I.nrm("pe.vq", (S.code_dim // S.vq_group, S.vq_size, S.vq_group), S.vq_std)
     return I.p
 
 

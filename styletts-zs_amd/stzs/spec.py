@@ -29,7 +29,7 @@ class Spec:
     n_symbols: int = 178
     d_txt: int = 512
     te_layers: int = 3
-    te_kernel: int = 5
+    te_kernel: int = 5             # CNN stack, then one BiLSTM d_txt -> 2 x d_txt/2 (StyleTTS2 TextEncoder)
     # style codes: L_s codes x (style_ac + style_pr)
     L_s: int = 50
     style_ac: int = 128
@@ -39,6 +39,11 @@ class Spec:
     mel_nfft: int = 2048
     mel_win: int = 1200
     pe_ch: int = 256
+    # discrete style codes (README.md:5): product VQ of each prompt code row, code_dim / vq_group groups of
+    # vq_group values, one vq_size-entry codebook per group
+    vq_group: int = 8
+    vq_size: int = 256
+    vq_std: float = 0.2            # codebook init scale (~ the prompt projection's output std)
     # denoiser
     dn_d: int = 512
     dn_heads: int = 8
@@ -110,6 +115,8 @@ class Spec:
             assert k == 2 * r, "ConvTranspose kernels must be 2x stride (polyphase form)"
         assert self.d_txt == self.pr_hid, "predictor hidden width equals the text width (StyleTTS2)"
         assert self.dn_d % self.dn_heads == 0
+        assert self.code_dim % self.vq_group == 0 and self.vq_group in (4, 8, 16)
+        assert self.d_txt % 64 == 0 and self.d_txt // 2 <= 256, "text BiLSTM: H % 32 == 0, H <= 256 (csrc/lstm.hip)"
         return self
 
     def replace(self, **kw) -> "Spec":

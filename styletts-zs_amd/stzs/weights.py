@@ -349,6 +349,7 @@ class PackedModel:
         self.te_emb = A.add("te.emb", P["te.emb"].float())
         self.te_conv = [pack_conv(A, f"te.conv{i}", P[f"te.conv{i}.w"], P[f"te.conv{i}.b"]) for i in range(S.te_layers)]
         self.te_ln = [(A.add(f"te.ln{i}.g", P[f"te.ln{i}.g"]), A.add(f"te.ln{i}.b", P[f"te.ln{i}.b"])) for i in range(S.te_layers)]
+        self.te_lstm = pack_lstm(A, "te.lstm", P)
         # --- reference-prompt front end (csrc/frontend.hip): DFT basis, window, mel filterbank, encoder ---
         self.fe_dft = pack_conv(A, "fe.dft", dft_basis(S.mel_nfft, S.mel_win))
         self.fe_win = A.add("fe.win", torch.hann_window(S.mel_win).float())
@@ -364,6 +365,7 @@ class PackedModel:
         self.pe_conv0 = pack_conv(A, "pe.conv0", P["pe.conv0.w"], P["pe.conv0.b"])
         self.pe_conv1 = pack_conv(A, "pe.conv1", P["pe.conv1.w"], P["pe.conv1.b"])
         self.pe_proj = pack_conv(A, "pe.proj", P["pe.proj.w"], P["pe.proj.b"])
+        self.pe_vq = A.add("pe.vq", P["pe.vq"].float())  # [G][K][dg] codebooks (stzs_code_quantize)
         # --- denoiser ---
         L = lambda n: pack_conv(A, n, P[n + ".w"], P[n + ".b"])
         self.dn_in = L("dn.in_proj")

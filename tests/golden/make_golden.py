@@ -40,7 +40,7 @@ def main():
     o = R.synth(P, S, tok, ref, 2, 5.0, eps, dur, seeds=[0, 1])
     pr = R.predict_prosody(P, S, o["h_txt"], o["codes"], None)
     t = {"tok": tok.to(torch.int32), "ref": ref, "eps": eps, "dur": dur, "h_txt": o["h_txt"], "prompt": o["prompt"],
-         "codes": o["codes"], "F0": o["F0"], "N": o["N"], "wav": o["wav"], "dur_pred": pr["dur_pred"],
+         "prompt_idx": o["prompt_idx"], "prompt_margin": o["prompt_margin"], "codes": o["codes"], "F0": o["F0"], "N": o["N"], "wav": o["wav"], "dur_pred": pr["dur_pred"],
          "dur_sum": pr["dur_sum"]}
     save_file({k: v.contiguous() for k, v in t.items()}, os.path.join(HERE, "tiny_synth.safetensors"),
               metadata={"spec": S.name, "seed": "0", "param_checksum": param_checksum(P), "steps": "2", "cfg": "5.0",
@@ -50,8 +50,8 @@ def main():
     P = init_params(S, 0)
     tok, ref, eps, dur = inputs(S, 1, 16, seed=99)
     o = R.synth(P, S, tok, ref, 1, 1.0, eps, dur, seeds=[5])
-    t = {"tok": tok.to(torch.int32), "ref": ref, "eps": eps, "dur": dur, "codes": o["codes"], "F0": o["F0"],
-         "N": o["N"], "wav": o["wav"]}
+    t = {"tok": tok.to(torch.int32), "ref": ref, "eps": eps, "dur": dur, "prompt_idx": o["prompt_idx"],
+         "prompt_margin": o["prompt_margin"], "codes": o["codes"], "F0": o["F0"], "N": o["N"], "wav": o["wav"]}
     save_file({k: v.contiguous() for k, v in t.items()}, os.path.join(HERE, "v0_synth_1s.safetensors"),
               metadata={"spec": S.name, "seed": "0", "param_checksum": param_checksum(P), "steps": "1", "cfg": "1.0",
                         "seeds": "5"})

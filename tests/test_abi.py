@@ -51,6 +51,7 @@ STRUCTS = {
     "stzs_dwup_args": "DwupArgs", "stzs_f0n_args": "F0nArgs", "stzs_source_args": "SourceArgs",
     "stzs_istft_args": "IstftArgs", "stzs_istft_stream_args": "IstftStreamArgs", "stzs_quant_args": "QuantArgs", "stzs_frames_args": "FramesArgs",
     "stzs_logmel_args": "LogMelArgs", "stzs_pool_args": "PoolArgs", "stzs_copy_args": "CopyArgs",
+    "stzs_vq_args": "VqArgs",
 }
 
 
@@ -129,6 +130,7 @@ _STRUCT_CALLS = [  # entry point, ctypes struct, extra int arguments between the
     ("stzs_harmonic_source", "SourceArgs", ()), ("stzs_istft", "IstftArgs", ()),
     ("stzs_istft_stream", "IstftStreamArgs", ()), ("stzs_stft_frames", "FramesArgs", ()),
     ("stzs_log_mel", "LogMelArgs", ()), ("stzs_pool_rows", "PoolArgs", ()), ("stzs_copy2d", "CopyArgs", ()),
+    ("stzs_code_quantize", "VqArgs", ()),
 ]
 
 

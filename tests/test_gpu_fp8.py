@@ -148,7 +148,7 @@ def test_sample_style_fp8_vs_oracle(gpu_device, spec):
     e8 = StyleTTSZS(S, P, device=gpu_device, fp8_denoiser=True)
     tok, ref, eps = _style_inputs(S, 2, 12 if spec == "tiny" else 80)
     h = R.text_encoder(P, S, tok).to(torch.bfloat16).float()
-    prompt = R.prompt_encoder(P, S, ref)
+    prompt = R.prompt_encoder(P, S, ref)[0]
     for steps, cfg, tol in ((1, 1.0, 6e-2), (2, 5.0, 1.5e-1)):
         want = R.sample_style(P, S, h, prompt, eps, steps, cfg)
         ht = torch.zeros(*h.shape, dtype=torch.bfloat16, device=gpu_device)

@@ -194,10 +194,18 @@ MRF_CASES = [
     (3, 400, 1090, 256, 3, 1, "leaky", True, False, True, 2),    # decoder block conv2: Ci 1090 (9 chunks), x2 shortcut
     (4, 200, 200, 96, 3, 1, "leaky", False, False, True, 1),     # predictor block conv1 (2 chunks, 1 column tile)
     (2, 300, 130, 64, 3, 1, "none", False, False, True, 1),      # up-block conv1 after the dw-ConvT: no prologue
+    # k3, one 128-channel chunk: the persistent LDS-DMA-pipelined kernel (csrc/mrfp.hip) under FRAG32
+    (16, 24001, 128, 128, 3, 1, "snake", False, False, True, 1),  # stage-1 c1 shape: 3008 tiles, ~12 per CU
+    (5, 24001, 128, 128, 3, 5, "snake", True, True, False, 1),    # stage-1 last c2 (residual + accumulate)
+    (7, 3001, 128, 128, 3, 3, "snake", True, False, True, 1),     # c2 + stats, ragged last tile (3001 % 128)
+    (300, 130, 128, 128, 3, 1, "snake", True, False, True, 1),    # 600 tiles of which every 2nd has 2 valid rows
+    (3, 500, 128, 64, 3, 1, "leaky", True, False, True, 1),       # Co 64 (half the column tile), LeakyReLU
+    (2, 333, 128, 128, 3, 2, "none", False, False, True, 1),      # no prologue
 ]
+PIPE_CASES = [c for c in MRF_CASES if c[2] == 128 and c[4] == 3 and c[7]]  # residual forms (csrc/mrfp.hip)
 
 
-def _run_mrf(eng, case, form):
+def _run_mrf(eng, case, form, flags=0):
     B, T, Ci, Co, k, dil, act, hr, ha, st, tdiv = case
     g = torch.Generator().manual_seed(B * T + Ci + k)
     pad = dil * (k - 1) // 2
@@ -232,7 +240,7 @@ def _run_mrf(eng, case, form):
     pa = {"snake": L.ACT_SNAKE, "leaky": L.ACT_LEAKY, "none": L.ACT_NONE}[act]
     out = eng.conv(cw, xd, yd, pad=pad, dil=dil, pro=pro, pro_act=pa, pro_slope=0.2,
                    pro_alpha=keep[3] if act == "snake" else None, res=rd, res_tdiv=tdiv, alpha=osc, acc_in=ad,
-                   beta=1.0, stats_key=f"t.mrfst.{form}" if st else None)
+                   beta=1.0, stats_key=f"t.mrfst.{form}" if st else None, flags=flags)
     stats = (out[1][0].clone().cpu(), out[1][1].clone().cpu()) if st else None
     return yd.t.float().cpu(), stats, ref
 
@@ -262,6 +270,19 @@ def test_mrf_frag32_bit_identical(eng, case):
     """the register-direct kernel accumulates every output in the same K order from the same staged bf16
     operands as the LDS-ring kernel: outputs and fused statistics are bit-identical (tolerance 0)."""
     a, sa, _ = _run_mrf(eng, case, "lane16")
+    b, sb, _ = _run_mrf(eng, case, "frag32")
+    assert torch.equal(a, b)
+    if sa is not None:
+        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
+
+
+@pytest.mark.parametrize("case", PIPE_CASES)
+def test_mrf_pipelined_bit_identical(eng, case):
+    """the persistent LDS-DMA-pipelined k3 kernel (csrc/mrfp.hip, STZS_CONV_MRF_PIPE) vs the one-tile-per-
+    workgroup register-direct kernel (csrc/mrfv.hip, the FRAG32 default): same staged operands, same K order,
+    same statistics grouping -> outputs and statistics bit-identical."""
+    from stzs import _lib as L
+    a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRF_PIPE)
     b, sb, _ = _run_mrf(eng, case, "frag32")
     assert torch.equal(a, b)
     if sa is not None:

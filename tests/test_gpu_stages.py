@@ -3,9 +3,11 @@ per stage: each GPU stage gets the oracle's inputs (rounded to b
 stores bf16) so kernel error is not masked by upstream drift.  Whole-pipeline error is reported
 separately with its own stated tolerance.
 
-Stated tolerances (bf16 storage, fp32 accumulate; relative L2 error unless noted):
-  text encoder 2e-2 | denoiser 1 NFE 3e-2 | 10-step CFG-5 sampler 1e-1 | predictor F0/N 5e-2 |
-  decoder waveform 1e-1 (rel-L2) + log-mel L1 stated in the test | durations bit-exact outside ties
+Stated tolerances (bf16 storage, fp32 accumulate; relative L2 error unless noted; ~2x the MI355X measurements of
+r02_j given in brackets): text encoder 1.2e-2 [5.5e-3] | denoiser 1 NFE 8e-3 [3.2e-3] | 2-step CFG-5 sampler 2e-2
+[8.7e-3] | 10-step CFG-5 sampler 1e-2 [4.1e-3] | predictor F0 1e-4 [2.3e-5], N 3e-2 [1.2e-2] | decoder waveform
+tiny 3e-2 [1.5e-2], v0 8e-2 [4.1e-2] | end to end tiny 5e-2 [2.1e-2], v0 1.5e-1 [7.6e-2] | durations bit-exact
+outside the measured tie window
 """
 import math
 
@@ -48,7 +50,7 @@ def test_text_encoder(eng, tiny, tiny_params):
     out = eng.text_encode(tok.to(eng.device, torch.int32)).t.float().cpu()
     e = rel_err(out, ref)
     print("text", e)
-    assert e < 2e-2
+    assert e < 1.2e-2
 
 
 @pytest.mark.parametrize("steps,cfg", [(1, 1.0), (2, 5.0), (10, 5.0)])
@@ -56,12 +58,12 @@ def test_sample_style(eng, tiny, tiny_params, steps, cfg):
     from oracle import stzs_ref as R
     tok, ref, eps, _ = _inputs(tiny, 2, 12)
     h = bf(R.text_encoder(tiny_params, tiny, tok))
-    prompt = R.prompt_encoder(tiny_params, tiny, ref)
+    prompt = R.prompt_encoder(tiny_params, tiny, ref)[0]
     codes_ref = R.sample_style(tiny_params, tiny, h, prompt, eps, steps, cfg)
     codes = eng.sample_style(_h_act(eng, h), prompt.to(eng.device), eps.to(eng.device), steps, cfg).cpu()
     e = rel_err(codes, codes_ref)
     print("sample_style", steps, cfg, e)
-    assert e < (3e-2 if steps == 1 else 1e-1)
+    assert e < {1: 8e-3, 2: 2e-2, 10: 1e-2}[steps]
 
 
 def test_predictor(eng, tiny, tiny_params):
@@ -71,18 +73,19 @@ def test_predictor(eng, tiny, tiny_params):
     codes = torch.randn(2, tiny.L_s, tiny.code_dim, generator=torch.Generator().manual_seed(3)) * 0.3
     pr = R.predict_prosody(tiny_params, tiny, h, codes, dur)
     out = eng.predict_prosody(_h_act(eng, h), codes.to(eng.device), dur)
-    # integer path: predicted durations bit-exact except at ties (oracle sum within 1e-2 of .5)
+    # integer path: the predicted durations (no override) equal the oracle's wherever the oracle's sum is
+    # farther from a rounding tie than the GPU sum's measured error (+ the 1e-4 teacher-forced guard)
     dsum = pr["dur_sum"]
-    tie = (dsum - dsum.floor() - 0.5).abs() < 2e-2
-    dp = out["dur"]  # forced -> equals override; check the predicted path separately below
-    assert torch.equal(dp.cpu(), dur)
-    e_dsum = (out["dsum"].cpu() - dsum).abs().max().item()
-    print("dsum max abs", e_dsum, "ties", int(tie.sum()))
+    du = eng.predict_durations(_h_act(eng, h), codes.to(eng.device), None)
+    e_dsum = (du["dsum"].cpu() - dsum).abs().max().item()
+    tie = (dsum - dsum.floor() - 0.5).abs() <= e_dsum + 1e-4
+    print("dsum max abs", e_dsum, "guarded ties", int(tie.sum()), "of", tie.numel())
     assert e_dsum < 0.15
+    assert bool(((du["dur"].cpu() == pr["dur_pred"]) | tie).all())
     assert torch.equal(out["idx"].cpu(), pr["idx"])
     eF, eN = rel_err(out["F0"].cpu(), pr["F0"]), rel_err(out["N"].cpu(), pr["N"])
     print("F0", eF, "N", eN)
-    assert eF < 5e-2 and eN < 5e-2
+    assert eF < 1e-4 and eN < 3e-2
 
 
 def test_predicted_durations_exact_teacher_forced(eng, tiny, tiny_params):
@@ -136,20 +139,20 @@ def test_decoder_tiny(eng, tiny, tiny_params):
     e = rel_err(wav, ref)
     ml = _logmel_l1(wav, ref, tiny)
     print("decoder tiny rel", e, "logmel L1", ml)
-    assert e < 1e-1
+    assert e < 3e-2
 
 
 def test_synth_end_to_end_tiny(eng, tiny, tiny_params):
     from oracle import stzs_ref as R
     tok, ref, eps, dur = _inputs(tiny, 2, 12)
-    o = R.synth(tiny_params, tiny, tok, ref, 2, 5.0, eps, dur, seeds=[0, 1])
     out = eng.synth(tok, ref, steps=2, cfg_scale=5.0, noise=eps, durations=dur, seeds=[0, 1])
+    o = R.synth(tiny_params, tiny, tok, ref, 2, 5.0, eps, dur, seeds=[0, 1], prompt_idx=out["prompt_idx"].cpu())
     w = out["wav"].cpu()
     assert w.shape == o["wav"].shape
     assert torch.isfinite(w).all()
     e = rel_err(w, o["wav"])
     print("e2e tiny rel", e, "codes", rel_err(out["codes"].cpu(), o["codes"]))
-    assert e < 3e-1
+    assert e < 5e-2
 
 
 @pytest.fixture(scope="module")
@@ -172,17 +175,17 @@ def test_decoder_v0_full_dims(eng_v0, v0):
     e = rel_err(wav, ref)
     ml = _logmel_l1(wav, ref, S)
     print("decoder v0 rel", e, "logmel L1", ml)
-    assert e < 1e-1
+    assert e < 8e-2
 
 
 def test_synth_v0_full_dims(eng_v0, v0):
     from oracle import stzs_ref as R
     S, P = v0
     tok, ref, eps, dur = _inputs(S, 1, 32)
-    o = R.synth(P, S, tok, ref, 2, 5.0, eps, dur, seeds=[0])
     out = eng_v0.synth(tok, ref, steps=2, cfg_scale=5.0, noise=eps, durations=dur, seeds=[0])
+    o = R.synth(P, S, tok, ref, 2, 5.0, eps, dur, seeds=[0], prompt_idx=out["prompt_idx"].cpu())
     e = rel_err(out["wav"].cpu(), o["wav"])
     print("e2e v0 rel", e, "codes", rel_err(out["codes"].cpu(), o["codes"]),
           "F0", rel_err(out["F0"].cpu(), o["F0"]))
     assert torch.isfinite(out["wav"]).all()
-    assert e < 3e-1
+    assert e < 1.5e-1

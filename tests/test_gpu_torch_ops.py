@@ -93,7 +93,7 @@ def test_stage_ops_match_engine(handle, tiny, tiny_params):
     w = torch.ops.stzs.synth(h, tok.to(dev), ref.to(dev), eps.to(dev), dur.to(dev), 2, 5.0, [0, 1])
     assert torch.equal(w, wav_e)
     hf = R.text_encoder(tiny_params, S, tok).to(dev)
-    pr = R.prompt_encoder(tiny_params, S, ref).to(dev)
+    pr = R.prompt_encoder(tiny_params, S, ref)[0].to(dev)
     c = torch.ops.stzs.sample_style(h, hf, pr, eps.to(dev), 2, 5.0)
     assert torch.isfinite(c).all() and c.shape == codes_e.shape
     d, idx, F0, N = torch.ops.stzs.predict_prosody(h, hf, codes_e, dur.to(dev))

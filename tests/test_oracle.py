@@ -89,9 +89,58 @@ def test_harmonic_source_phase_and_noise(tiny, tiny_params):
 
 
 def test_counter_normal_statistics():
-    from stzs.frontend import counter_normal, stream_key
-    z = counter_normal(stream_key(1, 2), np.arange(200000))
+    z = R.counter_normal(R.stream_key(1, 2), np.arange(200000))
     assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1) < 0.01
+
+
+def test_oracle_front_end_restatement_matches_product_front_end(tiny):
+    """the oracle restates the front-end arithmetic instead of importing it: its counter RNG equals the
+    product's (stzs.frontend, mirrored in csrc/source.hip) bit for bit, its filterbank / log-mel to fp32."""
+    from stzs import frontend as FE
+    for seed, stream in ((0, 0), (7, 3), (2 ** 31 + 5, 8), (0xFFFFFFFF, 1)):
+        k_o, k_p = R.stream_key(seed, stream), FE.stream_key(seed, stream)
+        assert int(k_o) == int(k_p)
+        idx = np.arange(0, 5000, 7)
+        assert np.array_equal(R.counter_normal(k_o, idx), FE.counter_normal(k_p, idx))
+        assert R.initial_phase(k_o) == FE.initial_phase(k_p)
+    fb_o = R.htk_mel_filterbank(80, 2048, 24000)
+    fb_p = FE.mel_filterbank(80, 2048, 24000)
+    torch.testing.assert_close(fb_o, fb_p, atol=1e-6, rtol=0)
+    wav = torch.randn(2, 24000, generator=torch.Generator().manual_seed(5)) * 0.1
+    from stzs.spec import SPEC_V0
+    torch.testing.assert_close(R.log_mel(wav, SPEC_V0), FE.log_mel(wav, SPEC_V0), atol=2e-4, rtol=0)
+
+
+def test_vq_matches_bruteforce_and_roundtrips(tiny, tiny_params):
+    """discrete style codes: indices = argmin of the fp64 distances wherever the fp32 margin is clear, the
+    dequantised rows are codebook rows, lookup(idx) == quantised codes, codebook rows are fixed points."""
+    S, P = tiny, tiny_params
+    z = torch.randn(3, S.L_s, S.code_dim, generator=torch.Generator().manual_seed(21)) * 0.2
+    idx, q, margin = R.quantize_codes(P, S, z)
+    G = S.code_dim // S.vq_group
+    assert idx.shape == (3, S.L_s, G) and idx.dtype == torch.int32 and (margin >= 0).all()
+    cb = P["pe.vq"].double()
+    d = ((z.double().reshape(-1, G, 1, S.vq_group) - cb[None]) ** 2).sum(-1)
+    clear = margin.reshape(-1, G) > 1e-5
+    assert clear.float().mean() > 0.95
+    assert torch.equal(d.argmin(-1)[clear], idx.reshape(-1, G).long()[clear])
+    torch.testing.assert_close(R.lookup_codes(P, S, idx), q, atol=0, rtol=0)
+    i2, q2, _ = R.quantize_codes(P, S, q)
+    assert torch.equal(i2, idx) and torch.equal(q2, q)
+
+
+def test_text_encoder_ends_in_bilstm(tiny, tiny_params):
+    """StyleTTS2 TextEncoder: the CNN stack's output goes through the text BiLSTM (row f2)."""
+    S, P = tiny, tiny_params
+    tok = torch.randint(1, S.n_symbols, (2, 9), generator=torch.Generator().manual_seed(4))
+    h = R.text_encoder(P, S, tok)
+    x = P["te.emb"][tok.long()].transpose(1, 2)
+    for i in range(S.te_layers):
+        x = F.conv1d(x, P[f"te.conv{i}.w"], P[f"te.conv{i}.b"], padding=S.te_kernel // 2)
+        x = F.leaky_relu(F.layer_norm(x.transpose(1, 2), (S.d_txt,), P[f"te.ln{i}.g"], P[f"te.ln{i}.b"]), 0.2)
+        x = x.transpose(1, 2)
+    torch.testing.assert_close(h, R.bilstm(x.transpose(1, 2), P, "te.lstm"), atol=0, rtol=0)
+    assert h.shape == (2, 9, S.d_txt)
 
 
 def test_convtranspose_polyphase_equivalence():
@@ -185,6 +234,7 @@ def test_golden_tiny_reproduces(tiny, tiny_params):
     t, meta = _load("tiny_synth.safetensors")
     assert meta["param_checksum"] == param_checksum(tiny_params)
     o = R.synth(tiny_params, tiny, t["tok"], t["ref"], 2, 5.0, t["eps"], t["dur"], seeds=[0, 1])
+    assert torch.equal(o["prompt_idx"], t["prompt_idx"])
     for k in ("h_txt", "prompt", "codes", "F0", "N", "wav"):
         torch.testing.assert_close(o[k], t[k], atol=2e-5, rtol=1e-4, msg=k)
     pr = R.predict_prosody(tiny_params, tiny, o["h_txt"], o["codes"], None)
@@ -199,5 +249,6 @@ def test_golden_v0_reproduces():
     P = init_params(SPEC_V0, 0)
     assert meta["param_checksum"] == param_checksum(P)
     o = R.synth(P, SPEC_V0, t["tok"], t["ref"], 1, 1.0, t["eps"], t["dur"], seeds=[5])
+    assert torch.equal(o["prompt_idx"], t["prompt_idx"])
     for k in ("codes", "F0", "N", "wav"):
         torch.testing.assert_close(o[k], t[k], atol=1e-4, rtol=1e-3, msg=k)

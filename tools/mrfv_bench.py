@@ -1,5 +1,5 @@
-"""Register-direct MRF conv (csrc/mrfv.hip, STZS_CONV_W_FRAG32) vs the LDS-ring MRF conv (csrc/mrf.hip,
-STZS_CONV_W_LANE16) on the generator shapes: bit-identity of outputs and fused statistics, then time per launch.
+"""Register-direct MRF conv (csrc/mrfv.hip, STZS_CONV_W_FRAG32), the persistent LDS-DMA-pipelined k3 residual
+form (csrc/mrfp.hip, + STZS_CONV_MRF_PIPE) and the LDS-ring MRF conv (csrc/mrf.hip, STZS_CONV_W_LANE16) on the generator shapes: bit-identity of outputs and fused statistics, then time per launch.
 
     python tools/mrfv_bench.py            (env: B=64, CASES=0,1,2,..., FLAGS=0, REPS=5)
 """
@@ -46,10 +46,10 @@ for (T, C, k, dil) in cases:
     byt = 2.0 * B * T * C * 2
     for variant in ("c1", "c2", "c2acc"):
         outs = {}
-        for name, cw in (("lane16", c16), ("frag32", cfr)):
+        for name, cw, fl in (("lane16", c16, 0), ("mrfv", cfr, 0), ("mrfp", cfr, L.CONV_MRF_PIPE)):
             y = Act(torch.zeros(B, T, C, device=dev, dtype=torch.bfloat16))
             kw = dict(pad=dil * (k - 1) // 2, dil=dil, pro=(mean, rstd, C, gb.data_ptr(), 2 * C, C),
-                      pro_act=L.ACT_SNAKE, pro_alpha=al, flags=flags)
+                      pro_act=L.ACT_SNAKE, pro_alpha=al, flags=flags | fl)
             if variant != "c1":
                 kw["res"] = res
             if variant == "c2acc":
@@ -73,11 +73,13 @@ for (T, C, k, dil) in cases:
             nb = byt * (1 + (variant != "c1") + (variant == "c2acc") * 0.5)
             print(f"T={T} C={C} k={k:2d} d={dil} {variant:6s} {name:7s}: {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s  "
                   f"{nb / us / 1e3:7.1f} GB/s", flush=True)
-        a, bb = outs["lane16"], outs["frag32"]
-        same = torch.equal(a[0], bb[0]) and (a[1] is None or (torch.equal(a[1][0], bb[1][0]) and
-                                                               torch.equal(a[1][1], bb[1][1])))
-        if not same:
-            d = (a[0].float() - bb[0].float()).abs().max().item()
-            print(f"   MISMATCH lane16 vs frag32: max |diff| {d:.3e}", flush=True)
-        else:
-            print("   bit-identical", flush=True)
+        a = outs["lane16"]
+        for other in ("mrfv", "mrfp"):
+            bb = outs[other]
+            same = torch.equal(a[0], bb[0]) and (a[1] is None or (torch.equal(a[1][0], bb[1][0]) and
+                                                                   torch.equal(a[1][1], bb[1][1])))
+            if not same:
+                d = (a[0].float() - bb[0].float()).abs().max().item()
+                print(f"   MISMATCH lane16 vs {other}: max |diff| {d:.3e}", flush=True)
+            else:
+                print(f"   lane16 == {other}: bit-identical", flush=True)
