@@ -12,6 +12,15 @@ operators pin the L1 surface SURVEY §8(b) lists, one per hot-path row of §8(a)
   stzs::cfg_euler_step   a3      fused CFG combine + Euler update
   stzs::istft            a13     conv_post rows [B, Tf, n_fft + 2] -> waveform
   stzs::istft_stream     a14     one chunk of the streaming iSTFT with its carried frame tail
+  stzs::bilstm           a5, a8  one named BiLSTM of the model (text encoder, DurationEncoder, duration, shared)
+  stzs::denoiser_fwd     a2      one preconditioned denoiser evaluation D(x, sigma) (CFG rows)
+  stzs::f0n_predictor    a8      shared BiLSTM + F0 / N AdaIN-block branches
+  stzs::decoder_pre      a9      F0/N convs, asr_res, encode + 4 decode AdaIN blocks -> generator input
+  stzs::sine_gen         a10     harmonic source + its STFT features
+  stzs::conv_transpose_up a11    noise conv + LeakyReLU + polyphase ConvTranspose1d (+ ReflectionPad)
+  stzs::mrf_resblock     a12     the MRF of one generator stage (AdaIN + Snake + dilated convs)
+  stzs::conv_post_istft  a13     conv_post + exp/sin spectrum + iSTFT
+  stzs::code_quantize    (f)1    the discrete style-code quantiser (README.md:5)
 
 Model-bound operators take an integer engine handle from `register(engine)` (the packed weights live in
 the engine's device arena).  Every operator is registered for the HIP device ONLY
@@ -239,5 +248,185 @@ def _(post, tail, f0, final, n_fft, hop):
     return post.new_empty((B, n1 - n0), dtype=torch.float32), post.new_empty(tail.shape, dtype=torch.float32)
 
 
+# ------------------------------------------------------------------ per-row operators (SURVEY §8(b) list)
+# Activations cross this boundary channels-last, [B, T, C] (the kernels' layout; a torch Conv1d NCT tensor is
+# x.transpose(1, 2)); outputs are fp32 copies.
+
+def _act_in(eng, key, x: torch.Tensor, dtype=torch.bfloat16):
+    """x [B, T, C] -> an engine Act (row pitch padded to 8) holding x in `dtype`."""
+    from .engine import Act
+    B, T, Cn = x.shape
+    t = eng.buf("op." + key, (B, T, (Cn + 7) // 8 * 8), dtype, zero=True)
+    t[:, :, :Cn].copy_(x)
+    return Act(t, 0, Cn)
+
+
+_LSTMS = {"te.lstm": lambda W: W.te_lstm, "pr.dur_lstm": lambda W: W.pr_dur_lstm, "pr.shared": lambda W: W.pr_shared}
+
+
+@custom_op("stzs::bilstm", mutates_args=(), device_types="cuda")
+def bilstm(handle: int, name: str, x: torch.Tensor) -> torch.Tensor:
+    """a5 / a8 / text encoder: the named single-layer BiLSTM ("te.lstm", "pr.de{i}", "pr.dur_lstm", "pr.shared") of
+    the packed model: x [B, T, in] -> h [B, T, 2H] fp32 (bf16 state in the exchange, fp32 gates)."""
+    eng = _eng(handle, x)
+    W = eng.W
+    if name.startswith("pr.de"):
+        lw = W.pr_de[int(name[5:])]
+    elif name in _LSTMS:
+        lw = _LSTMS[name](W)
+    else:
+        raise RuntimeError(f"stzs::bilstm: unknown LSTM {name!r}")
+    xa = _act_in(eng, "lstm.x", x)
+    y = eng.act("op.lstm.y", x.shape[0], x.shape[1], 2 * lw.H)
+    eng.lstm(lw, xa, y, "op." + name)
+    return y.t[:, :, :2 * lw.H].float()
+
+
+def _spec(handle):
+    """the registered engine's spec (host metadata: usable by the fake implementations)."""
+    eng = _ENGINES.get(int(handle))
+    if eng is None:
+        raise RuntimeError(f"stzs: unknown engine handle {handle}")
+    return eng.spec
+
+
+@register_fake("stzs::bilstm")
+def _(handle, name, x):
+    return x.new_empty((x.shape[0], x.shape[1], _spec(handle).pr_hid), dtype=torch.float32)  # 2H = pr_hid = d_txt
+
+
+@custom_op("stzs::denoiser_fwd", mutates_args=(), device_types="cuda")
+def denoiser_fwd(handle: int, h_txt: torch.Tensor, prompt: torch.Tensor, x: torch.Tensor, sigma: float,
+                 cfg: bool) -> torch.Tensor:
+    """a2: one EDM-preconditioned denoiser evaluation D(x, sigma).  h_txt [B, T_txt, d_txt], prompt [B, L_s, code],
+    x [R, L_s, code] (R = 2B with cfg: conditional rows, then null-prompt rows) -> D fp32 [R, L_s, code]."""
+    eng = _eng(handle, h_txt, prompt, x)
+    ha = _act_in(eng, "h_txt", h_txt)
+    xs = x.float().contiguous()
+    return eng.denoiser_fwd(ha, prompt.float().contiguous(), xs, float(sigma), bool(cfg)).clone()
+
+
+@register_fake("stzs::denoiser_fwd")
+def _(handle, h_txt, prompt, x, sigma, cfg):
+    return x.new_empty(x.shape, dtype=torch.float32)
+
+
+@custom_op("stzs::f0n_predictor", mutates_args=(), device_types="cuda")
+def f0n_predictor(handle: int, en: torch.Tensor, codes: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """a8: aligned predictor features en [B, T40, pr_in], codes [B, L_s, code] -> (F0, N) fp32 [B, 2 T40]."""
+    eng = _eng(handle, en, codes)
+    F0, Nn = eng.f0n_predictor(_act_in(eng, "en", en), codes.float().contiguous())
+    return F0.contiguous().clone(), Nn.contiguous().clone()
+
+
+@register_fake("stzs::f0n_predictor")
+def _(handle, en, codes):
+    B, T40 = en.shape[0], en.shape[1]
+    return en.new_empty((B, 2 * T40), dtype=torch.float32), en.new_empty((B, 2 * T40), dtype=torch.float32)
+
+
+@custom_op("stzs::decoder_pre", mutates_args=(), device_types="cuda")
+def decoder_pre(handle: int, asr: torch.Tensor, F0: torch.Tensor, N: torch.Tensor, codes: torch.Tensor) -> torch.Tensor:
+    """a9: asr [B, T40, d_txt], F0 / N [B, 2 T40], codes [B, L_s, code] -> generator input fp32 [B, 2 T40, dec_out]."""
+    eng = _eng(handle, asr, F0, N, codes)
+    S = eng.spec
+    B, T40, D = asr.shape
+    enc_in = eng.act("dec.enc_in", B, T40, S.d_txt + 2, eng.dec_dt)
+    enc_in.t[:, :, :D].copy_(asr)
+    pro = dict(asr_buf=enc_in, F0=F0.float().contiguous(), N=N.float().contiguous(), T40=T40)
+    gen_in, _ = eng.decoder_pre(pro, codes.float().contiguous())
+    return gen_in.t[:, :, :S.dec_out].float()
+
+
+@register_fake("stzs::decoder_pre")
+def _(handle, asr, F0, N, codes):
+    return asr.new_empty((asr.shape[0], 2 * asr.shape[1], _spec(handle).dec_out), dtype=torch.float32)
+
+
+@custom_op("stzs::sine_gen", mutates_args=(), device_types="cuda")
+def sine_gen(handle: int, F0: torch.Tensor, seeds: List[int]) -> torch.Tensor:
+    """a10: harmonic source of F0 [B, T80] and its n_fft STFT -> (real | imag) fp32 [B, T80 hop / hop_s + 1, n_fft + 2]."""
+    eng = _eng(handle, F0)
+    S = eng.spec
+    har = eng.sine_gen(F0.float().contiguous(), list(seeds))
+    return har.t[:, :, :S.har_ch].float()
+
+
+@register_fake("stzs::sine_gen")
+def _(handle, F0, seeds):
+    S = _spec(handle)
+    return F0.new_empty((F0.shape[0], F0.shape[1] * S.hop // S.istft_hop + 1, S.har_ch), dtype=torch.float32)
+
+
+@custom_op("stzs::conv_transpose_up", mutates_args=(), device_types="cuda")
+def conv_transpose_up(handle: int, x: torch.Tensor, har: torch.Tensor, stage: int) -> torch.Tensor:
+    """a11: generator stage `stage`'s LeakyReLU(0.1) + polyphase ConvTranspose1d (+ ReflectionPad(1,0) on the last
+    stage) + noise conv of the harmonic features har [B, Tf, n_fft + 2] -> fp32 [B, T_up, gen_ch[stage]]."""
+    eng = _eng(handle, x, har)
+    S = eng.spec
+    from .engine import Act
+    B, Tf, hc = har.shape
+    hb = eng.buf("op.har", (B, Tf, (hc + 31) // 32 * 32), eng.dec_dt, zero=True)
+    hb[:, :, :hc].copy_(har)
+    xu = eng.upsample(_act_in(eng, "ups.x", x, eng.dec_dt), Act(hb, 0, hc), int(stage))
+    return xu.t[:, :, :S.gen_ch[stage]].float()
+
+
+@register_fake("stzs::conv_transpose_up")
+def _(handle, x, har, stage):
+    S = _spec(handle)
+    T_up = x.shape[1] * S.up_rates[stage] + (1 if stage == len(S.up_rates) - 1 else 0)
+    return x.new_empty((x.shape[0], T_up, S.gen_ch[stage]), dtype=torch.float32)
+
+
+@custom_op("stzs::mrf_resblock", mutates_args=(), device_types="cuda")
+def mrf_resblock(handle: int, x: torch.Tensor, codes: torch.Tensor, stage: int) -> torch.Tensor:
+    """a12: the multi-receptive-field fusion of generator stage `stage` (its rb_kernels AdaIN + Snake + dilated-conv
+    resblocks, averaged), AdaIN style from the pooled acoustic codes: x [B, T, C] -> fp32 [B, T, C]."""
+    eng = _eng(handle, x, codes)
+    gbd = eng.dec_style(codes.float().contiguous())
+    y = eng.mrf(_act_in(eng, "mrf.x", x, eng.dec_dt), int(stage), gbd, eng.W.dec_norm)
+    return y.t[:, :, :x.shape[2]].float()
+
+
+@register_fake("stzs::mrf_resblock")
+def _(handle, x, codes, stage):
+    return x.new_empty(x.shape, dtype=torch.float32)
+
+
+@custom_op("stzs::conv_post_istft", mutates_args=(), device_types="cuda")
+def conv_post_istft(handle: int, x: torch.Tensor) -> torch.Tensor:
+    """a13: LeakyReLU(0.01) + conv_post + exp / sin spectrum + iSTFT: x [B, Tf, gen_ch[-1]] -> wav fp32 [B, (Tf-1) hop_s]."""
+    eng = _eng(handle, x)
+    wav = eng.istft(eng.conv_post(_act_in(eng, "post.x", x, eng.dec_dt)))
+    return wav.clone()
+
+
+@register_fake("stzs::conv_post_istft")
+def _(handle, x):
+    return x.new_empty((x.shape[0], (x.shape[1] - 1) * _spec(handle).istft_hop), dtype=torch.float32)
+
+
+@custom_op("stzs::code_quantize", mutates_args=(), device_types="cuda")
+def code_quantize(handle: int, z: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """discrete style codes (README.md:5): z [B, L_s, code] fp32 -> (indices int32 [B, L_s, G], dequantised
+    codes fp32 [B, L_s, code]); bit-exact against oracle quantize_codes."""
+    eng = _eng(handle, z)
+    S = eng.spec
+    B, Lr, D = z.shape
+    G = S.code_dim // S.vq_group
+    idx = torch.empty(B, Lr, G, dtype=torch.int32, device=z.device)
+    out = torch.empty(B, Lr, D, dtype=torch.float32, device=z.device)
+    eng.code_quantize(z.float().contiguous(), idx, out)
+    return idx, out
+
+
+@register_fake("stzs::code_quantize")
+def _(handle, z):
+    G = z.shape[2] // _spec(handle).vq_group
+    return z.new_empty((z.shape[0], z.shape[1], G), dtype=torch.int32), z.new_empty(z.shape, dtype=torch.float32)
+
+
 OPS = ["synth", "sample_style", "predict_prosody", "decode", "duration_head", "length_regulate",
-       "cfg_euler_step", "istft", "istft_stream"]
+       "cfg_euler_step", "istft", "istft_stream", "bilstm", "denoiser_fwd", "f0n_predictor", "decoder_pre",
+       "sine_gen", "conv_transpose_up", "mrf_resblock", "conv_post_istft", "code_quantize"]

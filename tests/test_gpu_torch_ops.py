@@ -104,3 +104,143 @@ def test_stage_ops_match_engine(handle, tiny, tiny_params):
     e = rel_err(wd.cpu(), wr)
     print("decode op vs oracle", e)
     assert e < 1e-1
+
+
+# ---------------------------------------------------------------- per-row operators vs the oracle (tiny spec)
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def test_op_bilstm(handle, tiny, tiny_params):
+    """stzs::bilstm vs oracle bilstm (nn.LSTM); bf16 input / output rows: rel-L2 <= 1e-2."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    g = torch.Generator().manual_seed(41)
+    for name, cin in (("te.lstm", tiny.d_txt), ("pr.de1", tiny.pr_in), ("pr.shared", tiny.pr_in)):
+        x = _bf(torch.randn(3, 17, cin, generator=g))
+        y = torch.ops.stzs.bilstm(h, name, x.to(eng.device)).cpu()
+        e = rel_err(y, R.bilstm(x, tiny_params, name))
+        print("bilstm", name, e)
+        assert e < 1e-2
+
+
+def test_op_denoiser_fwd(handle, tiny, tiny_params):
+    """stzs::denoiser_fwd (one NFE, CFG rows) vs oracle denoiser: rel-L2 <= 8e-3 (the 1-NFE stage bound)."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    S, P = tiny, tiny_params
+    g = torch.Generator().manual_seed(42)
+    ht = _bf(torch.randn(2, 11, S.d_txt, generator=g))
+    prompt = torch.randn(2, S.L_s, S.code_dim, generator=g) * 0.2
+    x = torch.randn(4, S.L_s, S.code_dim, generator=g) * 2.0
+    for sigma in (3.0, 0.5):
+        kv, pool = R.denoiser_context(P, S, ht, prompt, True)
+        want = R.denoiser(P, S, x, sigma, kv, pool)
+        got = torch.ops.stzs.denoiser_fwd(h, ht.to(eng.device), prompt.to(eng.device), x.to(eng.device), sigma,
+                                          True).cpu()
+        e = rel_err(got, want)
+        print("denoiser_fwd sigma", sigma, e)
+        assert e < 8e-3
+
+
+def test_op_f0n_predictor(handle, tiny, tiny_params):
+    """stzs::f0n_predictor vs oracle f0n_predictor: F0 rel-L2 <= 1e-4, N <= 3e-2 (the stage bounds)."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    S, P = tiny, tiny_params
+    g = torch.Generator().manual_seed(43)
+    en = _bf(torch.randn(2, 30, S.pr_in, generator=g))
+    codes = torch.randn(2, S.L_s, S.code_dim, generator=g) * 0.3
+    F0r, Nr = R.f0n_predictor(P, S, en, codes)
+    F0, N = torch.ops.stzs.f0n_predictor(h, en.to(eng.device), codes.to(eng.device))
+    eF, eN = rel_err(F0.cpu(), F0r), rel_err(N.cpu(), Nr)
+    print("f0n_predictor", eF, eN)
+    assert eF < 1e-4 and eN < 3e-2
+
+
+@pytest.fixture(scope="module")
+def dec_inputs(tiny):
+    S = tiny
+    g = torch.Generator().manual_seed(44)
+    T40 = 20
+    asr = _bf(torch.randn(2, T40, S.d_txt, generator=g))
+    F0 = 100 + 150 * torch.rand(2, 2 * T40, generator=g)
+    F0[:, :3] = 0.0
+    N = torch.randn(2, 2 * T40, generator=g)
+    codes = torch.randn(2, S.L_s, S.code_dim, generator=g) * 0.3
+    return asr, F0, N, codes
+
+
+def test_op_decoder_pre(handle, tiny, tiny_params, dec_inputs):
+    """stzs::decoder_pre vs oracle decoder_pre (5 AdaIN blocks, bf16 activations): rel-L2 <= 3e-2."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    asr, F0, N, codes = dec_inputs
+    want = R.decoder_pre(tiny_params, tiny, asr, F0, N, codes).transpose(1, 2)
+    d = eng.device
+    got = torch.ops.stzs.decoder_pre(h, asr.to(d), F0.to(d), N.to(d), codes.to(d)).cpu()
+    e = rel_err(got, want)
+    print("decoder_pre", e)
+    assert e < 3e-2
+
+
+def test_op_sine_gen(handle, tiny, tiny_params, dec_inputs):
+    """stzs::sine_gen vs oracle source_features (STFT of the harmonic source; bf16 storage): rel-L2 <= 1e-2."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    _, F0, _, _ = dec_inputs
+    want, _ = R.source_features(tiny_params, tiny, F0, [3, 4])
+    got = torch.ops.stzs.sine_gen(h, F0.to(eng.device), [3, 4]).cpu()
+    e = rel_err(got, want.transpose(1, 2))
+    print("sine_gen", e)
+    assert e < 1e-2
+
+
+@pytest.mark.parametrize("stage", [0, 1])
+def test_op_conv_transpose_up_and_mrf(handle, tiny, tiny_params, dec_inputs, stage):
+    """stzs::conv_transpose_up vs oracle upsample_stage (rel-L2 <= 2e-2) and stzs::mrf_resblock vs oracle
+    mrf_stage (rel-L2 <= 3e-2), on bf16-rounded inputs."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    S, P = tiny, tiny_params
+    _, F0, _, codes = dec_inputs
+    d = eng.device
+    g = torch.Generator().manual_seed(45 + stage)
+    cin = S.dec_out if stage == 0 else S.gen_ch[0]
+    T = F0.shape[1] * (1 if stage == 0 else S.up_rates[0])
+    x = _bf(torch.randn(2, T, cin, generator=g))
+    har, _ = R.source_features(P, S, F0, [3, 4])
+    har = _bf(har)
+    want = R.upsample_stage(P, S, x.transpose(1, 2), har, stage).transpose(1, 2)
+    got = torch.ops.stzs.conv_transpose_up(h, x.to(d), har.transpose(1, 2).contiguous().to(d), stage).cpu()
+    e = rel_err(got, want)
+    xm = _bf(want)
+    s = R.decoder_style(S, codes)
+    want_m = R.mrf_stage(P, S, xm.transpose(1, 2), s, stage).transpose(1, 2)
+    got_m = torch.ops.stzs.mrf_resblock(h, xm.to(d), codes.to(d), stage).cpu()
+    em = rel_err(got_m, want_m)
+    print("conv_transpose_up", stage, e, "mrf_resblock", em)
+    assert e < 2e-2 and em < 3e-2
+
+
+def test_op_conv_post_istft(handle, tiny, tiny_params):
+    """stzs::conv_post_istft vs oracle conv_post_istft: rel-L2 <= 2e-2 (bf16 input rows, fp32 conv output)."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    g = torch.Generator().manual_seed(47)
+    x = _bf(torch.randn(2, 481, tiny.gen_ch[-1], generator=g) * 0.5)
+    want, _ = R.conv_post_istft(tiny_params, tiny, x.transpose(1, 2))
+    got = torch.ops.stzs.conv_post_istft(h, x.to(eng.device)).cpu()
+    e = rel_err(got, want)
+    print("conv_post_istft", e)
+    assert e < 2e-2
+
+
+def test_op_code_quantize(handle, tiny, tiny_params):
+    """stzs::code_quantize vs oracle quantize_codes: indices and dequantised codes bit-exact."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    z = torch.randn(3, tiny.L_s, tiny.code_dim, generator=torch.Generator().manual_seed(48)) * 0.2
+    idx_w, q_w, _ = R.quantize_codes(tiny_params, tiny, z)
+    idx, q = torch.ops.stzs.code_quantize(h, z.to(eng.device))
+    assert torch.equal(idx.cpu(), idx_w) and torch.equal(q.cpu(), q_w)

@@ -29,6 +29,35 @@ def test_fake_shapes():
                                            torch.empty(2, 50, 256), 2, 5.0).shape == (2, 50, 256)
 
 
+def test_fake_shapes_model_bound(tiny, tiny_params):
+    """the model-bound per-row operators' fakes read the registered engine's spec (host metadata, no GPU)."""
+    from stzs import ops
+    from stzs.engine import StyleTTSZS
+    S = tiny
+    eng = object.__new__(StyleTTSZS)  # metadata-only stand-in: the fakes only read .spec
+    eng.spec = S
+    h = ops.register(eng)
+    with FakeTensorMode():
+        assert torch.ops.stzs.bilstm(h, "pr.de0", torch.empty(2, 9, S.pr_in)).shape == (2, 9, S.pr_hid)
+        assert torch.ops.stzs.denoiser_fwd(h, torch.empty(2, 9, S.d_txt), torch.empty(2, S.L_s, S.code_dim),
+                                           torch.empty(4, S.L_s, S.code_dim), 3.0, True).shape == (4, S.L_s, S.code_dim)
+        F0, N = torch.ops.stzs.f0n_predictor(h, torch.empty(2, 20, S.pr_in), torch.empty(2, S.L_s, S.code_dim))
+        assert F0.shape == N.shape == (2, 40)
+        assert torch.ops.stzs.decoder_pre(h, torch.empty(2, 20, S.d_txt), torch.empty(2, 40), torch.empty(2, 40),
+                                          torch.empty(2, S.L_s, S.code_dim)).shape == (2, 40, S.dec_out)
+        har = torch.ops.stzs.sine_gen(h, torch.empty(2, 40), [0, 1])
+        assert har.shape == (2, 40 * S.hop // S.istft_hop + 1, S.har_ch)
+        assert torch.ops.stzs.conv_transpose_up(h, torch.empty(2, 40, S.dec_out), har, 0).shape == \
+            (2, 40 * S.up_rates[0], S.gen_ch[0])
+        assert torch.ops.stzs.conv_transpose_up(h, torch.empty(2, 400, S.gen_ch[0]), har, 1).shape == \
+            (2, 400 * S.up_rates[1] + 1, S.gen_ch[1])
+        assert torch.ops.stzs.mrf_resblock(h, torch.empty(2, 400, S.gen_ch[0]), torch.empty(2, S.L_s, S.code_dim),
+                                           0).shape == (2, 400, S.gen_ch[0])
+        assert torch.ops.stzs.conv_post_istft(h, torch.empty(2, 2401, S.gen_ch[1])).shape == (2, 2400 * S.istft_hop)
+        i, q = torch.ops.stzs.code_quantize(h, torch.empty(2, S.L_s, S.code_dim))
+        assert i.shape == (2, S.L_s, S.code_dim // S.vq_group) and i.dtype == torch.int32 and q.shape == (2, S.L_s, S.code_dim)
+
+
 def test_cpu_tensor_raises():
     from stzs import ops  # noqa: F401
     with pytest.raises(NotImplementedError):
