@@ -413,6 +413,92 @@ int stzs_copy2d(const stzs_copy_args* a, void* stream);
 int stzs_embed(const int32_t* tok, const float* emb, void* y, int B, int T, int D, int64_t ldy,
                void* stream);
 
+/* ======================================================================================================
+ * Generic tensor-descriptor entry points (SURVEY.md §8(b) "C-ABI"): one per hot-path operator of §8(a),
+ *   int    stzs_<op>(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out,
+ *                    const stzs_params_t* p, void* workspace, size_t ws_bytes, void* stream);
+ *   size_t stzs_<op>_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+ * composed in native host code (csrc/abi.hip) over the per-kernel entry points above.  Tensors are caller-owned
+ * device memory described by (data, dtype, ndim, shape, stride in ELEMENTS); activations are channels-last
+ * [B, T, C] with stride[2] == 1 (the row pitch stride[1] may exceed C).  The workspace is caller-owned device
+ * memory of at least the queried size (ws_bytes is checked); ops that hold LSTM exchange counters in it require
+ * it zero-initialised before the FIRST call and leave those counters zeroed.  Weights are the packed layouts
+ * produced by stzs_pack_conv / stzs_pack_lstm below (host memory; the caller copies them to the device).
+ * The denoiser, decoder pre-blocks and F0/N predictor (a2, a9, a8) compose dozens of weight tensors: they are
+ * provided as torch operators over the per-kernel entries (stzs/ops.py), not in this generic form.
+ * ====================================================================================================== */
+typedef struct stzs_tensor_t {
+    void* data;
+    int32_t dtype; /* STZS_F32 | STZS_BF16 | STZS_I32 | STZS_F8 */
+    int32_t ndim;  /* <= 4 */
+    int64_t shape[4];
+    int64_t stride[4]; /* elements */
+} stzs_tensor_t;
+typedef struct stzs_params_t {
+    int32_t i[16];
+    float f[8];
+} stzs_params_t;
+
+/* packed weight forms (host-side packers; stzs/weights.py pack_conv restated in C++) */
+enum { STZS_PACK_KSTEP = 0, STZS_PACK_LANE16 = 1, STZS_PACK_FRAG32 = 2, STZS_PACK_NARROW32 = 3 };
+/* bytes of the packed bf16 form of a Conv1d weight [Co][Ci][ks] (ups = 0) or ConvTranspose1d weight [Ci][Co][2 ups]
+ * (ups > 0, polyphase); 0 if the form does not apply to the shape */
+size_t stzs_pack_conv_size(int Co, int Ci, int ks, int ups, int form);
+/* w fp32 (host), packed bf16 (host, stzs_pack_conv_size bytes); returns STZS_OK / STZS_ESHAPE / STZS_EINVAL */
+int stzs_pack_conv(const float* w, int Co, int Ci, int ks, int ups, int form, void* packed);
+/* LSTM of input width In, hidden H: W_ih (fwd | rev) as ONE KSTEP linear [8H][In] (bytes stzs_pack_conv_size(8H, In,
+ * 1, 0, KSTEP)) + its bias b_ih + b_hh [8H] fp32, and W_hh^T MFMA fragments (2 * 4H * H bf16).  Torch gate order
+ * i, f, g, o; w_* fp32 host arrays in torch.nn.LSTM layout. */
+int stzs_pack_lstm(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, const float* w_ih_rev,
+                   const float* w_hh_rev, const float* b_ih_rev, const float* b_hh_rev, int In, int H, void* ih_packed,
+                   float* ih_bias, void* whh_frags);
+
+/* a3  cfg_euler_step: in {x f32 [R, N], D f32 [R, N]} -> out {x' f32 [R, N]};
+ *     i[0] = cfg (R = 2B, conditional rows first), f[0] = scale, f[1] = sigma, f[2] = sigma_next */
+int stzs_cfg_euler_step(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out,
+                        const stzs_params_t* p, void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_cfg_euler_step_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+/* a6  duration_head: in {logits f32 [B, T, nbins]} -> out {dur i32 [B, T] (, dsum f32 [B, T])} */
+int stzs_duration_head(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out,
+                       const stzs_params_t* p, void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_duration_head_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+/* a7  length_regulate: in {dur i32 [B, T]} -> out {idx i32 [B, T40]} (T40 = outputs[0].shape[1]) */
+int stzs_length_regulate(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out,
+                         const stzs_params_t* p, void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_length_regulate_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+/* a10 sine_gen: in {F0 f32 [B, T80], merge f32 [nh + 1], seeds i32 [B]} -> out {har bf16|f32 [B, Tf, >= n_fft + 2]};
+ *     i[0] = hop, i[1] = n_fft, i[2] = hop_s, i[3] = nh; f[0] = sr, f[1] = sine_amp, f[2] = noise_std,
+ *     f[3] = voiced_threshold.  Tf = T80 hop / hop_s + 1 */
+int stzs_sine_gen(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out, const stzs_params_t* p,
+                  void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_sine_gen_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+/* a13 conv_post_istft: in {x bf16 [B, Tf, Ci], w (packed NARROW32 if Ci % 128 == 0 else KSTEP, Co = n_fft + 2,
+ *     ks = 7), bias f32 [Co]} -> out {wav f32 [B, (Tf - 1) hop_s]}; i[0] = n_fft, i[1] = hop_s; f[0] = LeakyReLU slope */
+int stzs_conv_post_istft(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out,
+                         const stzs_params_t* p, void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_conv_post_istft_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+/* a5/a8 bilstm: in {x bf16 [B, T, In], ih packed (stzs_pack_lstm), ih_bias f32 [8H], whh frags} -> out {y bf16
+ *     [B, T, >= 2H] (, status i32 [1]: OR-ed STZS_STATUS_LSTM_TIMEOUT)}; i[0] = H */
+int stzs_bilstm(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out, const stzs_params_t* p,
+                void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_bilstm_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+/* a11 conv_transpose_up: in {x bf16 [B, T, Cin], har bf16 [B, Tf, >= har_ch], ups w (packed LANE16 if Cin % 128 == 0
+ *     and Co % 16 == 0 else KSTEP; ConvTranspose1d [Cin][Co][2r]), ups bias f32 [Co], noise w (KSTEP,
+ *     [Co][har_ch][nk]), noise bias f32 [Co]} -> out {y bf16 [B, T r + last, >= Co]};
+ *     i[0] = r, i[1] = last stage (ReflectionPad(1,0) + 1 row), i[2] = noise kernel nk, i[3] = noise stride,
+ *     i[4] = noise pad, i[5] = har_ch, i[6] = Co; f[0] = LeakyReLU slope (0.1) */
+int stzs_conv_transpose_up(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out,
+                           const stzs_params_t* p, void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_conv_transpose_up_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+/* a12 mrf_resblock: the MRF of one generator stage, nk resblocks (kernels i[1..nk]) x nd dilations (i[4..3+nd]),
+ *     averaged: in {x bf16 [B, T, C], gb f32 [B, nk * nd * 4C] (per resblock layer (j, m): gamma1 | beta1 | gamma2 |
+ *     beta2, C each), then per layer (j, m) in order: c1 w, c1 bias, alpha1 f32 [C], c2 w, c2 bias, alpha2} ->
+ *     out {y bf16 [B, T, C]}; i[0] = C, i[1..3] = resblock kernels, i[4..6] = dilations, i[7] = nk, i[8] = nd,
+ *     i[9] = weight form (STZS_PACK_FRAG32 | LANE16 | KSTEP) */
+int stzs_mrf_resblock(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out,
+                      const stzs_params_t* p, void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_mrf_resblock_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -153,6 +153,43 @@ class CopyArgs(C.Structure):
                [(n, i32) for n in ("B", "R", "C", "in_dtype", "out_dtype", "pad_i")]
 
 
+class Tensor(C.Structure):
+    """stzs_tensor_t: (data, dtype, ndim, shape[4], stride[4] in elements)"""
+    _fields_ = [("data", vp), ("dtype", i32), ("ndim", i32), ("shape", i64 * 4), ("stride", i64 * 4)]
+
+
+class Params(C.Structure):
+    _fields_ = [("i", i32 * 16), ("f", f32 * 8)]
+
+
+PACK_KSTEP, PACK_LANE16, PACK_FRAG32, PACK_NARROW32 = 0, 1, 2, 3
+GENERIC_OPS = ["cfg_euler_step", "duration_head", "length_regulate", "sine_gen", "conv_post_istft", "bilstm",
+               "conv_transpose_up", "mrf_resblock"]
+
+
+def tensor(t, dtype=None) -> Tensor:
+    """stzs_tensor_t of a torch tensor (device memory; dtype inferred unless given)."""
+    import torch
+    d = Tensor()
+    d.data = t.data_ptr()
+    d.dtype = dtype if dtype is not None else {torch.float32: F32, torch.bfloat16: BF16, torch.int32: I32,
+                                                torch.float8_e4m3fn: F8}[t.dtype]
+    d.ndim = t.dim()
+    for k in range(t.dim()):
+        d.shape[k] = t.shape[k]
+        d.stride[k] = t.stride(k)
+    return d
+
+
+def params(ints=(), floats=()) -> Params:
+    p = Params()
+    for k, v in enumerate(ints):
+        p.i[k] = int(v)
+    for k, v in enumerate(floats):
+        p.f[k] = float(v)
+    return p
+
+
 # every exported symbol of include/stzs.h (tests check the .so exports exactly these)
 EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_chan_stats_workspace",
            "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
@@ -160,7 +197,8 @@ EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_ch
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
            "stzs_stft_frames", "stzs_log_mel", "stzs_pool_rows", "stzs_code_quantize",
            "stzs_dn_cond", "stzs_dn_cond_steps", "stzs_adaln_expand", "stzs_cfg_euler",
-           "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed"]
+           "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed", "stzs_pack_conv_size", "stzs_pack_conv",
+           "stzs_pack_lstm"] + [f"stzs_{o}{sfx}" for o in GENERIC_OPS for sfx in ("", "_workspace")]
 
 _lib = None
 
@@ -214,7 +252,13 @@ def load():
         "stzs_mean_rows": ([vp, vp, i32, i32, i64, i64, i32, i32, i64, vp], i32),
         "stzs_copy2d": ([P(CopyArgs), vp], i32),
         "stzs_embed": ([vp, vp, vp, i32, i32, i32, i64, vp], i32),
+        "stzs_pack_conv_size": ([i32, i32, i32, i32, i32], C.c_size_t),
+        "stzs_pack_conv": ([vp, i32, i32, i32, i32, i32, vp], i32),
+        "stzs_pack_lstm": ([vp] * 8 + [i32, i32, vp, vp, vp], i32),
     }
+    for o in GENERIC_OPS:
+        sig[f"stzs_{o}"] = ([P(Tensor), i32, P(Tensor), i32, P(Params), vp, C.c_size_t, vp], i32)
+        sig[f"stzs_{o}_workspace"] = ([P(Tensor), i32, P(Params)], C.c_size_t)
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)
         fn.argtypes = argt

@@ -51,7 +51,7 @@ STRUCTS = {
     "stzs_dwup_args": "DwupArgs", "stzs_f0n_args": "F0nArgs", "stzs_source_args": "SourceArgs",
     "stzs_istft_args": "IstftArgs", "stzs_istft_stream_args": "IstftStreamArgs", "stzs_quant_args": "QuantArgs", "stzs_frames_args": "FramesArgs",
     "stzs_logmel_args": "LogMelArgs", "stzs_pool_args": "PoolArgs", "stzs_copy_args": "CopyArgs",
-    "stzs_vq_args": "VqArgs",
+    "stzs_vq_args": "VqArgs", "stzs_tensor_t": "Tensor", "stzs_params_t": "Params",
 }
 
 

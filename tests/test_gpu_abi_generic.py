@@ -1,0 +1,202 @@
+"""The generic tensor-descriptor C-ABI on the GPU (include/stzs.h, csrc/abi.hip): each operator, fed the C++
+packers' weights, against the engine path it restates natively (bit-identical: same kernels, same arguments,
+bit-identical packed bytes) or against the oracle formula."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from stzs import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _call(op, ins, outs, p, ws_bytes=None):
+    lib = L.load()
+    ti = (L.Tensor * len(ins))(*[L.tensor(t) for t in ins])
+    to = (L.Tensor * len(outs))(*[L.tensor(t) for t in outs])
+    n = getattr(lib, f"stzs_{op}_workspace")(ti, len(ins), C.byref(p))
+    ws = torch.zeros(max(n, 256), dtype=torch.uint8, device=ins[0].device)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = getattr(lib, f"stzs_{op}")(ti, len(ins), to, len(outs), C.byref(p), ws.data_ptr(), n if ws_bytes is None else
+                                    ws_bytes, s)
+    return rc, ws
+
+
+def _pack(w, Co, Ci, ks, ups, form, dev):
+    lib = L.load()
+    n = lib.stzs_pack_conv_size(Co, Ci, ks, ups, form)
+    assert n > 0
+    out = np.zeros(n, np.uint8)
+    wc = np.ascontiguousarray(w.float().numpy())
+    assert lib.stzs_pack_conv(wc.ctypes.data, Co, Ci, ks, ups, form, out.ctypes.data) == L.OK
+    return torch.from_numpy(out).to(dev)
+
+
+@pytest.fixture(scope="module")
+def eng(gpu_device, tiny, tiny_params):
+    from stzs.engine import StyleTTSZS
+    return StyleTTSZS(tiny, tiny_params, device=gpu_device)
+
+
+def test_generic_cfg_euler_duration_length(gpu_device):
+    from oracle import stzs_ref as R
+    g = torch.Generator().manual_seed(61)
+    x = torch.randn(4, 50, 16, generator=g)
+    D = torch.randn(4, 50, 16, generator=g)
+    y = torch.empty_like(x).to(gpu_device)
+    rc, _ = _call("cfg_euler_step", [x.to(gpu_device), D.to(gpu_device)], [y], L.params([1], [5.0, 3.0, 0.5]))
+    assert rc == L.OK
+    Dg = D[2:] + 5.0 * (D[:2] - D[2:])
+    want = torch.cat([x[:2] + (0.5 - 3.0) * (x[:2] - Dg) / 3.0, x[2:] + (0.5 - 3.0) * (x[2:] - Dg) / 3.0])
+    assert (y.cpu() - want).abs().max().item() < 1e-5
+    logits = torch.randn(3, 40, 50, generator=g) * 2
+    dref, sref = R.durations_from_logits(logits)
+    dur = torch.empty(3, 40, dtype=torch.int32, device=gpu_device)
+    dsum = torch.empty(3, 40, device=gpu_device)
+    assert _call("duration_head", [logits.to(gpu_device)], [dur, dsum], L.params())[0] == L.OK
+    tie = (sref - sref.floor() - 0.5).abs() < 1e-4
+    assert bool(((dur.cpu() == dref) | tie).all())
+    d = torch.randint(1, 4, (3, 30), generator=g, dtype=torch.int32)
+    d[:, -1] = 100 - d[:, :-1].sum(1)
+    d = d.clamp_min(1)
+    d[:, -1] += 100 - d.sum(1)
+    idx = torch.empty(3, 100, dtype=torch.int32, device=gpu_device)
+    assert _call("length_regulate", [d.to(gpu_device)], [idx], L.params())[0] == L.OK
+    assert torch.equal(idx.cpu(), R.alignment_index(d))
+
+
+def test_generic_sine_gen_and_conv_post_istft(eng, tiny, tiny_params):
+    S, P, dev = tiny, tiny_params, eng.device
+    g = torch.Generator().manual_seed(62)
+    F0 = (100 + 150 * torch.rand(2, 40, generator=g)).to(dev)
+    har_e = eng.sine_gen(F0, [3, 4]).t[:, :, :S.har_ch].clone()
+    Tf = har_e.shape[1]
+    har = torch.zeros(2, Tf, 32, dtype=torch.bfloat16, device=dev)
+    merge = torch.cat([P["gen.src_merge.w"].reshape(-1), P["gen.src_merge.b"]]).float().to(dev)
+    seeds = torch.tensor([3, 4], dtype=torch.int32, device=dev)
+    p = L.params([S.hop, S.n_fft, S.istft_hop, S.harmonic_num + 1], [S.sr, S.sine_amp, S.noise_std, S.voiced_threshold])
+    assert _call("sine_gen", [F0, merge, seeds], [har], p)[0] == L.OK
+    assert torch.equal(har[:, :, :S.har_ch], har_e)
+    # conv_post + iSTFT on some generator-width rows, vs the engine's conv_post / istft launches
+    Ci = S.gen_ch[-1]
+    x = (torch.randn(2, 241, Ci, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    from stzs.engine import Act
+    want = eng.istft(eng.conv_post(Act(x))).clone()
+    w = _pack(P["gen.conv_post.w"], S.har_ch, Ci, 7, 0, L.PACK_KSTEP, dev)
+    wav = torch.empty(2, 240 * S.istft_hop, device=dev)
+    rc, _ = _call("conv_post_istft", [x, w, P["gen.conv_post.b"].float().to(dev)], [wav],
+                  L.params([S.n_fft, S.istft_hop], [0.01]))
+    assert rc == L.OK
+    assert torch.equal(wav, want)
+
+
+def test_generic_bilstm(eng, tiny, tiny_params):
+    S, P, dev = tiny, tiny_params, eng.device
+    lib = L.load()
+    g = torch.Generator().manual_seed(63)
+    In, H = S.pr_in, S.lstm_h
+    x = torch.randn(3, 13, In, generator=g).to(torch.bfloat16).to(dev)
+    from stzs.engine import Act
+    y_e = eng.act("t.gen.lstm", 3, 13, 2 * H)
+    eng.lstm(eng.W.pr_de[0], Act(x), y_e, "t.gen")
+    ih = np.zeros(lib.stzs_pack_conv_size(8 * H, In, 1, 0, L.PACK_KSTEP), np.uint8)
+    bias = np.zeros(8 * H, np.float32)
+    fr = np.zeros(2 * 4 * H * H * 2, np.uint8)
+    arrs = [np.ascontiguousarray(P["pr.de0." + n].numpy(), dtype=np.float32)
+            for n in ("w_ih", "w_hh", "b_ih", "b_hh", "w_ih_rev", "w_hh_rev", "b_ih_rev", "b_hh_rev")]
+    assert lib.stzs_pack_lstm(*[a.ctypes.data for a in arrs], In, H, ih.ctypes.data, bias.ctypes.data,
+                              fr.ctypes.data) == L.OK
+    y = torch.zeros(3, 13, 2 * H, dtype=torch.bfloat16, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ins = [x, torch.from_numpy(ih).to(dev), torch.from_numpy(bias).to(dev), torch.from_numpy(fr).to(dev)]
+    rc, ws = _call("bilstm", ins, [y, status], L.params([H]))
+    assert rc == L.OK
+    assert torch.equal(y, y_e.t[:, :, :2 * H]) and int(status.item()) == 0
+    # the workspace's counters are left zeroed: a second call on the same workspace agrees
+    lib_ = L.load()
+    ti = (L.Tensor * 4)(*[L.tensor(t) for t in ins])
+    to = (L.Tensor * 2)(L.tensor(y), L.tensor(status))
+    y.zero_()
+    rc = lib_.stzs_bilstm(ti, 4, to, 2, C.byref(L.params([H])), ws.data_ptr(), ws.numel(),
+                          C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == L.OK and torch.equal(y, y_e.t[:, :, :2 * H])
+
+
+@pytest.mark.parametrize("stage", [0, 1])
+def test_generic_conv_transpose_up(eng, tiny, tiny_params, stage):
+    S, P, dev = tiny, tiny_params, eng.device
+    g = torch.Generator().manual_seed(64 + stage)
+    from stzs.engine import Act
+    cin = S.dec_out if stage == 0 else S.gen_ch[0]
+    T80 = 20
+    T = T80 * (1 if stage == 0 else S.up_rates[0])
+    x = torch.randn(2, T, cin, generator=g).to(torch.bfloat16).to(dev)
+    F0 = (100 + 150 * torch.rand(2, T80, generator=g)).to(dev)
+    har = eng.sine_gen(F0, [1, 2])
+    want = eng.upsample(Act(x), har, stage).t.clone()
+    r, k, Co = S.up_rates[stage], S.up_kernels[stage], S.gen_ch[stage]
+    last = stage == len(S.up_rates) - 1
+    nk = 1 if last else 2 * int(np.prod(S.up_rates[stage + 1:]))
+    nstride = 1 if last else nk // 2
+    npad = 0 if last else (nstride + 1) // 2
+    form = L.PACK_LANE16 if (cin % 128 == 0 and Co % 16 == 0) else L.PACK_KSTEP
+    wu = _pack(P[f"gen.ups{stage}.w"], Co, cin, k, r, form, dev)
+    wn = _pack(P[f"gen.noise_conv{stage}.w"], Co, S.har_ch, nk, 0, L.PACK_KSTEP, dev)
+    y = torch.zeros_like(want)
+    ins = [x, har.t, wu, P[f"gen.ups{stage}.b"].float().to(dev), wn, P[f"gen.noise_conv{stage}.b"].float().to(dev)]
+    # har descriptor: the engine's buffer (row pitch 32, channels har_ch)
+    hv = har.t[:, :, :S.har_ch]
+    ins[1] = hv
+    rc, _ = _call("conv_transpose_up", ins, [y[:, :, :Co]], L.params([r, int(last), nk, nstride, npad, S.har_ch, Co],
+                                                                       [0.1]))
+    assert rc == L.OK
+    assert torch.equal(y[:, :, :Co], want[:, :, :Co])
+
+
+@pytest.mark.parametrize("spec", ["tiny", "v0"])
+def test_generic_mrf_resblock(gpu_device, tiny, tiny_params, spec):
+    """the MRF of generator stage 1 through the generic entry (C++ orchestration of 18 convs + statistics) vs the
+    engine's mrf(): bit-identical (tiny: KSTEP weights; v0: FRAG32 weights, 128 channels)."""
+    from stzs.engine import Act, StyleTTSZS
+    if spec == "tiny":
+        S, P = tiny, tiny_params
+    else:
+        from stzs.params import init_params
+        from stzs.spec import SPEC_V0
+        S, P = SPEC_V0, init_params(SPEC_V0, seed=0)
+    eng = StyleTTSZS(S, P, device=gpu_device)
+    dev = eng.device
+    stage, C_ = 1, S.gen_ch[1]
+    g = torch.Generator().manual_seed(66)
+    B, T = 2, 3001
+    x = torch.randn(B, T, C_, generator=g).to(torch.bfloat16).to(dev)
+    codes = (torch.randn(B, S.L_s, S.code_dim, generator=g) * 0.3).to(dev)
+    gbd = eng.dec_style(codes)
+    want = eng.mrf(Act(x), stage, gbd, eng.W.dec_norm).t.clone()
+    ng = eng.W.dec_norm
+    form = L.PACK_FRAG32 if (C_ == 128) else (L.PACK_LANE16 if C_ % 128 == 0 else L.PACK_KSTEP)
+    gb_cols, ins = [], []
+    nk, nd = len(S.rb_kernels), len(S.rb_dils)
+    for j, kr in enumerate(S.rb_kernels):
+        for m in range(nd):
+            pfx = f"gen.rb{stage}.{j}.{m}"
+            for nn in (".n1", ".n2"):
+                off, c = ng.offsets[pfx + nn]
+                gb_cols.append(gbd[:, off:off + 2 * c])
+            for cc, al in ((".c1", ".alpha1"), (".c2", ".alpha2")):
+                ins += [_pack(P[pfx + cc + ".w"], C_, C_, kr, 0, form, dev), P[pfx + cc + ".b"].float().to(dev),
+                        P[pfx + al].float().to(dev)]
+    gb = torch.cat(gb_cols, 1).contiguous()
+    y = torch.zeros(B, T, C_, dtype=torch.bfloat16, device=dev)
+    p = L.params([C_] + list(S.rb_kernels) + list(S.rb_dils) + [nk, nd, form])
+    rc, _ = _call("mrf_resblock", [x, gb] + ins, [y], p)
+    assert rc == L.OK
+    assert torch.equal(y, want[:, :, :C_])
+
+
+def test_generic_rejects_short_workspace(eng):
+    x = torch.zeros(2, 30, dtype=torch.int32, device=eng.device)
+    idx = torch.zeros(2, 60, dtype=torch.int32, device=eng.device)
+    assert _call("length_regulate", [x], [idx], L.params(), ws_bytes=4)[0] == L.ESHAPE
