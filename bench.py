@@ -14,7 +14,10 @@ roofline: the dominant kernel (the generator MRF convs -- mrfv_conv at stage 1, 
           per launch with HIP events on its own stream in an instrumented eager pass right after
           the timed region; achieved = algorithmic FLOP / average launch time (bound: MFMA).
 cpu     : the CPU oracle (oracle/stzs_ref.py, torch fp32) on a bounded sample of the same
-          workload (rank 0, N=1 only), threads = min(16, affinity).
+          workload (rank 0, N=1 only), threads = the process's affinity cores (capped by OMP_NUM_THREADS, the
+          job's CPU share, when set); core counts and the host ISA are reported.
+h2h     : the same steps timed host to host as well (tokens / reference / noise / durations copied in from
+          pinned host memory, the waveform copied back) -- reported beside `value`, which is device-resident.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
@@ -78,9 +81,31 @@ def rank_inputs(S, B, rank):
     return tok, ref, eps, dur, seeds
 
 
+def host_isa():
+    """the host CPU's model and the vector ISA torch's CPU kernels dispatch to."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        cap = torch.backends.cpu.get_cpu_capability()
+    except Exception:  # older torch
+        cap = "unknown"
+    return f"{model} ({cap})" if model else cap
+
+
 def cpu_baseline(S, P, budget_s=15.0):
     from oracle import stzs_ref as R
-    nthr = min(16, len(os.sched_getaffinity(0)))
+    # every core of this process's affinity, unless the job's CPU share is pinned (OMP_NUM_THREADS: the GPU box
+    # sets it to the share one GPU may use; both numbers are reported)
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    nthr = min(aff, share) if share > 0 else aff
     torch.set_num_threads(nthr)
     tok, ref, eps, dur = make_inputs(S, 1, 0)
     n, t0 = 0, time.perf_counter()
@@ -90,7 +115,7 @@ def cpu_baseline(S, P, budget_s=15.0):
         el = time.perf_counter() - t0
         if el > budget_s or n >= 64:
             break
-    return dict(value=n * TARGET_S / el, unit="audio-s/s", cores=nthr, kind="port",
+    return dict(value=n * TARGET_S / el, unit="audio-s/s", cores=nthr, affinity_cores=aff, isa=host_isa(), kind="port",
                 sample=f"{n} x 1 utterance of the bench workload (5-s target, {STEPS_THROUGHPUT}-step CFG-{CFG:g}), "
                        f"CPU oracle torch fp32, {el:.1f} s")
 
@@ -237,30 +262,40 @@ def main():
             front()
             back()
             ga = tw.capture(front)[0]
-            gb = tw.capture(back)[0]
-            pairs.append((ga, gb))
+            gb, wv = tw.capture(back)
+            pairs.append((ga, gb, sl, wv))
         streams = [torch.cuda.Stream(dev) for _ in range(nstream)]
 
-        def run_steps(k):
+        def run_steps(k, h2h=False):
             cur = torch.cuda.current_stream(dev)
             for st in streams:
                 st.wait_stream(cur)
             ev = torch.cuda.Event()
             for i in range(k):
-                for j, (st, (ga, gb)) in enumerate(zip(streams, pairs)):
+                for j, (st, (ga, gb, sl, wv)) in enumerate(zip(streams, pairs)):
                     with torch.cuda.stream(st):
                         if i == 0 and j > 0 and args.stagger:
                             st.wait_event(ev)
+                        if h2h:  # this shard's inputs in from pinned host memory
+                            for d_, h_ in ((tok_d, tok_h), (ref_d, ref_h), (eps_d, eps_h), (dur_d, dur_h)):
+                                d_[sl].copy_(h_[sl], non_blocking=True)
                         ga.replay()
                         if i == 0 and j == 0:
                             ev.record(st)
                         gb.replay()
+                        if h2h:  # and its waveform back
+                            wav_h[sl].copy_(wv, non_blocking=True)
             for st in streams:
                 cur.wait_stream(st)
     else:
-        def run_steps(k):
+        def run_steps(k, h2h=False):
             for _ in range(k):
+                if h2h:
+                    for d_, h_ in ((tok_d, tok_h), (ref_d, ref_h), (eps_d, eps_h), (dur_d, dur_h)):
+                        d_.copy_(h_, non_blocking=True)
                 run()
+                if h2h:
+                    wav_h.copy_(out["wav"], non_blocking=True)
     run_steps(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
@@ -272,10 +307,20 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # the same steps host to host (inputs from pinned host memory, waveform back): reported beside `value`
+    tok_h, ref_h, eps_h, dur_h = (t.pin_memory() for t in (tok, ref, eps, dur))
+    wav_h = torch.empty(B, out["wav"].shape[1], dtype=torch.float32).pin_memory()
+    run_steps(1, h2h=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    run_steps(args.steps, h2h=True)
+    torch.cuda.synchronize()
+    el_h2h = time.perf_counter() - t1
+    h2d_bytes = sum(t.numel() * t.element_size() for t in (tok, ref, eps, dur))
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el, el_h2h], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el, el_h2h = float(t[0].item()), float(t[1].item())
     total_audio = world * B * audio_s * args.steps
     value = total_audio / el
     # the LSTM exchange's spin-timeout words of every engine that ran (a timeout = wrong prosody, reported)
@@ -373,6 +418,11 @@ def main():
             "cpu_baseline": cpu,
             "weight_broadcast_ms": round(bcast_ms, 3),
             "lstm_timeouts": lstm_timeouts,
+            "host_to_host": {"value": round(world * B * audio_s * args.steps / el_h2h, 2), "unit": "audio-s/s",
+                             "ms_per_step": round(el_h2h / args.steps * 1e3, 3), "h2d_bytes_per_step": h2d_bytes,
+                             "d2h_bytes_per_step": int(wav_h.numel() * 4),
+                             "note": "inputs copied in from pinned host memory and the waveform copied back inside "
+                                     "every step, on the shard streams"},
             "longform": lf,
             "precise_decoder": pr,
         }

@@ -172,8 +172,9 @@ def tensor(t, dtype=None) -> Tensor:
     import torch
     d = Tensor()
     d.data = t.data_ptr()
+    # (packed weights travel as raw bytes: uint8 descriptors are tagged BF16, the packed element type)
     d.dtype = dtype if dtype is not None else {torch.float32: F32, torch.bfloat16: BF16, torch.int32: I32,
-                                                torch.float8_e4m3fn: F8}[t.dtype]
+                                                torch.float8_e4m3fn: F8, torch.uint8: BF16}[t.dtype]
     d.ndim = t.dim()
     for k in range(t.dim()):
         d.shape[k] = t.shape[k]

@@ -43,13 +43,15 @@ def eng(gpu_device, tiny, tiny_params):
 def test_generic_cfg_euler_duration_length(gpu_device):
     from oracle import stzs_ref as R
     g = torch.Generator().manual_seed(61)
-    x = torch.randn(4, 50, 16, generator=g)
+    x0 = torch.randn(2, 50, 16, generator=g)
+    x = torch.cat([x0, x0])  # the CFG state is duplicated: both halves hold the same x
     D = torch.randn(4, 50, 16, generator=g)
     y = torch.empty_like(x).to(gpu_device)
     rc, _ = _call("cfg_euler_step", [x.to(gpu_device), D.to(gpu_device)], [y], L.params([1], [5.0, 3.0, 0.5]))
     assert rc == L.OK
     Dg = D[2:] + 5.0 * (D[:2] - D[2:])
-    want = torch.cat([x[:2] + (0.5 - 3.0) * (x[:2] - Dg) / 3.0, x[2:] + (0.5 - 3.0) * (x[2:] - Dg) / 3.0])
+    xn = x0 + (0.5 - 3.0) * (x0 - Dg) / 3.0
+    want = torch.cat([xn, xn])
     assert (y.cpu() - want).abs().max().item() < 1e-5
     logits = torch.randn(3, 40, 50, generator=g) * 2
     dref, sref = R.durations_from_logits(logits)
