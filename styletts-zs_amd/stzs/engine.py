@@ -103,13 +103,16 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
-                 packed: PackedModel = None):
+                 packed: PackedModel = None, branch_streams=False):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
         precise_decoder: PARITY mode -- the decoder (pre-blocks, generator, conv_post) keeps fp32 activations
         and runs every conv on fp32 MFMA operands (STZS_CONV_W_F32) to meet the north-star mel-L1 <= 1e-3 vs
-        the fp32 oracle; slower, not the benchmark path (bf16 weights alone cost ~1.3e-2)."""
+        the fp32 oracle; slower, not the benchmark path (bf16 weights alone cost ~1.3e-2).
+        branch_streams: run the independent branches (text encoder || prompt encoder, F0 || N predictor branches)
+        on forked side streams (graph-capturable: the fork/join is stream-ordered); each branch has its own
+        scratch (statistics slab / workspace), results bit-identical to the single-stream order."""
         self.spec = spec
         self.fp8_denoiser = fp8_denoiser
         self.precise = precise_decoder
@@ -124,8 +127,11 @@ class StyleTTSZS:
         else:
             self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder)
         self._bufs = {}
+        self._retired = []
         self._consts = {}
-        self._ws = None
+        self.branch_streams = branch_streams
+        self._branch = ""  # scratch-key suffix of the branch being enqueued (see fork())
+        self._side = []
         self.launches = 0
         self.lstm_spin_limit = 0  # 0 = the library default; tests force tiny values
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
@@ -158,14 +164,38 @@ class StyleTTSZS:
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def buf(self, key, shape, dtype=torch.bfloat16, zero=False):
-        """cached device buffer (stable address across calls -> graph-capturable)."""
-        k = (key, tuple(shape), dtype)
-        t = self._bufs.get(k)
-        if t is None:
-            t = torch.zeros(shape, dtype=dtype, device=self.device) if zero else \
-                torch.empty(shape, dtype=dtype, device=self.device)
-            self._bufs[k] = t
-        return t
+        """cached device buffer: ONE storage per (key, dtype), reused by capacity for every shape that fits, so a
+        stream of distinct request lengths (stzs/scheduler.py) does not allocate a buffer set per length.  The
+        address is stable while the shape fits (graph-capturable); a shape change re-zeroes zero=True buffers
+        (their padding rows / channels are read by the kernels); growth allocates 1.25x the request and keeps
+        the old storage alive in self._retired, so graphs captured on it stay valid."""
+        k = (key, dtype)
+        shape = tuple(int(v) for v in shape)
+        n = 1
+        for v in shape:
+            n *= v
+        ent = self._bufs.get(k)
+        # a storage a captured graph reads (ent[3], set by capture()) is never re-viewed at another shape:
+        # the graph would replay over the other shape's data and padding
+        if ent is None or ent[0].numel() < n or (ent[3] and ent[1] != shape):
+            if ent is not None:
+                self._retired.append(ent[0])
+            cap = n if ent is None else max(n, int(ent[0].numel() * 1.25))
+            store = torch.zeros(max(cap, 1), dtype=dtype, device=self.device) if zero else \
+                torch.empty(max(cap, 1), dtype=dtype, device=self.device)
+            ent = self._bufs[k] = [store, shape, store[:n].view(shape), False]
+            return ent[2]
+        if ent[1] != shape:
+            ent[1] = shape
+            ent[2] = ent[0][:n].view(shape)
+            if zero:
+                ent[2].zero_()
+        return ent[2]
+
+    def buffer_bytes(self) -> int:
+        """device bytes held by the buffer cache (live storages + retired ones kept for captured graphs)."""
+        live = sum(e[0].numel() * e[0].element_size() for k, e in self._bufs.items() if isinstance(k, tuple))
+        return live + sum(t.numel() * t.element_size() for t in self._retired)
 
     def act(self, key, B, T, C, dtype=torch.bfloat16):
         return Act(self.buf(key, (B, T, _rup(C, 8)), dtype, zero=True), 0, C)
@@ -267,12 +297,46 @@ class StyleTTSZS:
         L.check(self.lib.stzs_chan_stats_final(C.byref(s), L.CONV_STAT_ROWS, self.stream()), "chan_stats_final")
         return y, (mean, rstd, Cc)
 
-    def _slab(self, n):
-        """shared fp32 partial-statistics slab (consumed by the finalize launch right behind its conv)."""
-        t = self._bufs.get("stat_slab")
+    def _scratch(self, name, n):
+        """fp32 scratch shared by consecutive launches of ONE branch (a conv's statistics partials, consumed by
+        the finalize launch right behind it; the standalone statistics workspace).  Each forked branch has its
+        own (key suffix self._branch): concurrent branches sharing one slab would race on the partials.  A
+        grown slab's old storage is retired, not freed: launches already enqueued (or captured) on it --
+        possibly on another stream -- still read it, and a freed block could be handed to another stream's
+        allocation while they run."""
+        key = name + self._branch
+        t = self._bufs.get(key)
         if t is None or t.numel() < n:
-            t = self._bufs["stat_slab"] = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=self.device)
+            if t is not None:
+                self._retired.append(t)
+            t = self._bufs[key] = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=self.device)
         return t
+
+    def _slab(self, n):
+        return self._scratch("stat_slab", n)
+
+    def fork(self, *fns):
+        """run fns[0] on the current stream and fns[1:] on side streams forked from it (waits on the current
+        stream, joined back into it before returning); sequential when branch_streams is off.  -> outputs"""
+        if not self.branch_streams or len(fns) < 2:
+            return [f() for f in fns]
+        cur = torch.cuda.current_stream(self.device)
+        while len(self._side) < len(fns) - 1:
+            self._side.append(torch.cuda.Stream(self.device))
+        side = self._side[:len(fns) - 1]
+        for st in side:
+            st.wait_stream(cur)
+        outs = []
+        try:
+            for i, f in enumerate(fns):
+                self._branch = "" if i == 0 else f"@b{i}"
+                with torch.cuda.stream(cur if i == 0 else side[i - 1]):
+                    outs.append(f())
+        finally:
+            self._branch = ""
+        for st in side:
+            cur.wait_stream(st)
+        return outs
 
     timer = None
 
@@ -291,10 +355,7 @@ class StyleTTSZS:
         Cc = _rup(x.C, 8)
         mean = self.buf(key + ".m", (x.B, Cc), torch.float32)
         rstd = self.buf(key + ".r", (x.B, Cc), torch.float32)
-        need = self.lib.stzs_chan_stats_workspace(x.B, x.T, Cc) // 4 + 1
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=self.device)
-        ws = self._ws
+        ws = self._scratch("stat_ws", self.lib.stzs_chan_stats_workspace(x.B, x.T, Cc) // 4 + 1)
         a = L.StatsArgs()
         a.x, a.mean, a.rstd, a.partial = x.ptr, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr()
         a.ld, a.bs, a.stat_bs, a.B, a.T, a.C, a.dtype, a.eps = x.ld, x.bs, Cc, x.B, x.T, Cc, x.dt, 1e-5
@@ -738,7 +799,8 @@ class StyleTTSZS:
         F0 = self.buf("pr.F0", (B, T80, 1), torch.float32)
         Nn = self.buf("pr.N", (B, T80, 1), torch.float32)
         c0, c1, c2 = S.f0n_ch
-        for br, out in (("f0", F0), ("n", Nn)):
+
+        def branch(br, out):
             y0 = self.act(f"pr.{br}.y0", B, T40, c0)
             y1 = self.act(f"pr.{br}.y1", B, T80, c1)
             y2 = self.act(f"pr.{br}.y2", B, T80, c2)
@@ -746,6 +808,7 @@ class StyleTTSZS:
             self.blk(W.pr_blk[f"pr.{br}1"], y0, y1, ng, gbp, f"pr.{br}1")
             self.blk(W.pr_blk[f"pr.{br}2"], y1, y2, ng, gbp, f"pr.{br}2")
             self.conv(W.pr_blk[f"pr.{br}_proj"], y2, Act(out, 0, 1), what=f"pr.{br}_proj")
+        self.fork(lambda: branch("f0", F0), lambda: branch("n", Nn))
         return F0[:, :, 0], Nn[:, :, 0]
 
     def gather(self, x: Act, idx, y: Act, Cn):
@@ -1004,9 +1067,14 @@ class StyleTTSZS:
         latency-bound phases -- LSTM recurrences, statistics, small GEMMs -- overlap the other's convs)."""
         t = object.__new__(StyleTTSZS)
         t.__dict__.update(self.__dict__)
-        t._bufs, t._consts, t._ws, t.launches, t.timer = {}, {}, None, 0, None
+        t._bufs, t._retired, t._consts, t._side, t._branch, t.launches, t.timer = {}, [], {}, [], "", 0, None
         t.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         return t
+
+    def encode_inputs(self, tokens, ref_wav, prompt_idx=None):
+        """text encoder || prompt encoder (independent; forked when branch_streams) -> (h_txt, prompt codes)."""
+        ref = None if ref_wav is None else ref_wav.to(self.device)
+        return self.fork(lambda: self.text_encode(tokens), lambda: self.prompt_encode(ref, prompt_idx))
 
     def capture(self, fn):
         """Capture `fn()` into one HIP graph.  fn must be replay-safe: device-resident inputs, cached
@@ -1021,6 +1089,9 @@ class StyleTTSZS:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             out = fn()
+        for k, ent in self._bufs.items():
+            if isinstance(k, tuple):
+                ent[3] = True
         return g, out
 
     def synth(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None, codes=None,
@@ -1033,8 +1104,7 @@ class StyleTTSZS:
         dev = self.device
         tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
         B = tokens.shape[0]
-        h = self.text_encode(tokens)
-        prompt = self.prompt_encode(None if ref_wav is None else ref_wav.to(dev), prompt_idx)
+        h, prompt = self.encode_inputs(tokens, ref_wav, prompt_idx)
         pidx = self.prompt_idx
         if prompt.shape[0] == 1 and B > 1:
             pe = self.buf("prompt.bc", (B, S.L_s, S.code_dim), torch.float32)
@@ -1059,8 +1129,7 @@ class StyleTTSZS:
         dev = self.device
         tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
         B = tokens.shape[0]
-        h = self.text_encode(tokens)
-        prompt = self.prompt_encode(None if ref_wav is None else ref_wav.to(dev), prompt_idx)
+        h, prompt = self.encode_inputs(tokens, ref_wav, prompt_idx)
         if prompt.shape[0] == 1 and B > 1:
             pe = self.buf("prompt.bc", (B, S.L_s, S.code_dim), torch.float32)
             pe.copy_(prompt.expand(B, -1, -1))
