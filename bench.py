@@ -195,6 +195,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="split the per-GPU batch over this many concurrently replayed graphs (engine twins)")
     ap.add_argument("--stagger", type=int, default=1, help="start shard j > 0 one front phase late")
+    ap.add_argument("--branch-streams", type=int, default=0,
+                    help="fork the independent branches (text || prompt encoder, F0 || N) onto side streams")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,7 +213,7 @@ def main():
     S = SPEC_V0
     # rank 0 owns the weights; every other rank receives them with ONE RCCL broadcast of the arena
     W, bcast_ms = rank_weights(S, rank, world, dev)
-    eng = StyleTTSZS(S, None, device=dev, packed=W)
+    eng = StyleTTSZS(S, None, device=dev, packed=W, branch_streams=bool(args.branch_streams))
     P = init_params(S, seed=0) if rank == 0 and world == 1 else None  # host params: CPU baseline / extra modes
 
     B = args.batch
@@ -252,8 +254,7 @@ def main():
             st_ = {}
 
             def front(tw=tw, sl=sl, st_=st_):
-                h = tw.text_encode(tok_d[sl])
-                pr = tw.prompt_encode(ref_d[sl])
+                h, pr = tw.encode_inputs(tok_d[sl], ref_d[sl])
                 codes = tw.sample_style(h, pr, eps_d[sl], STEPS_THROUGHPUT, CFG)
                 st_["codes"], st_["pro"] = codes, tw.predict_prosody(h, codes, dur_d[sl], n_frames)
 
@@ -409,7 +410,7 @@ def main():
             "data": "synthetic (seeded tokens 16/s, 3-s noise reference, forced [3,2] durations); random-init weights",
             "config": {"workload": "configs[2]: batch 64/GPU, 5-s targets, 2-step distilled style diffusion, CFG 5",
                        "global_batch": world * B, "seq_len": n_frames, "parallelism": f"dp{world} (utterance shards)",
-                       "spec": S.name, "graph": graph is not None, "streams": nstream,
+                       "spec": S.name, "graph": graph is not None, "branch_streams": bool(args.branch_streams), "streams": nstream,
                        "stagger": bool(args.stagger and nstream > 1)},
             "audio_s_per_s_per_gpu": round(value / world, 2),
             "p50_latency_ms": lat["p50_ms"] if lat else None,
