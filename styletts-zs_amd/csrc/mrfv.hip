@@ -17,6 +17,8 @@
 // accumulate loads and stores; fused InstanceNorm statistics per 64-row chunk as in mrf.hip.
 #include "common.hpp"
 
+#include <type_traits>
+
 #ifndef STZS_MRFV_OCC
 #define STZS_MRFV_OCC 2
 #endif
@@ -29,24 +31,35 @@ namespace {
 constexpr int NTH = 256;
 constexpr int BT = 128, BCO = 128;
 constexpr int P = 272;  // staged input row pitch, bytes (conflict-free ds_read_b128)
-constexpr int SB = 12;  // staged 16-B vectors per thread: 16 rows x 12 = 192 >= rows_in
-#ifndef STZS_MRFV_SBB
-#define STZS_MRFV_SBB 12
-#endif
-constexpr int SBB = STZS_MRFV_SBB;  // loads per staging batch (SB / SBB batches)
+// staged 16-B vectors per thread (16 rows each): rows_in = 128 + (KS - 1) dil <= 16 SB.  Sized per kernel width
+// (k3: dil <= 8; k7 / k11: dil <= 5), not for the widest: every staged vector costs its transform (the cosines
+// of the Snake) whether or not its row is used, and a k3 tile with SB = 12 transformed 192 rows for 130-138
+constexpr int sb_rows(int ks) { return ks == 3 ? 9 : (ks == 7 ? 10 : 12); }
+constexpr int SB_MAX = 12;
 constexpr int CS_BYTES = 5 * 128 * 4;  // per-channel prologue constants
 
-STZS_DEV float row_sum16(float x) {  // sum over the 16 lanes of a DPP row (VALU only)
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, true));
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, true));
-    return x;
+// x[0..N) summed over the 16 lanes of each DPP row, in place, VALU only.  Each step is ONE v_add_f32 with the DPP
+// permutation on its first source (hipcc emitted a v_mov_b32_dpp + v_add_f32 pair per step); the N values go
+// step-major, so a value's next step issues N instructions after the write it reads (DPP read-after-VALU-write
+// needs 2 wait states; N >= 8 here).  Same additions in the same order as x += dpp(x): bit-identical.
+template <int N>
+STZS_DEV void row_sum16_n(float* x) {
+    static_assert(N >= 4, "dependent DPP steps need >= 2 independent instructions between them");
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(x[i]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "+v"(x[i]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("v_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf" : "+v"(x[i]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("v_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf" : "+v"(x[i]));
 }
 
 // NCH = 1: exactly one 128-channel input chunk (the stage-1 generator convs): the accumulators are not live
 // during the staging, so the kernel fits 3 workgroups per CU; NCH = 0: any number of chunks, 2 per CU.
-template <int PACT, bool HR, bool HA, int KS, int NCH>
+// AL: the epilogue scales by a.alpha (alpha != 1; a uniform runtime test was if-converted into a multiply + select
+// per element)
+template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL>
 __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NKC = KS * 4;  // 32-wide K-steps per 128-channel chunk
@@ -62,6 +75,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     const int bq = bx / tpb;
     const int t0 = (bx - bq * tpb) * BT;
     const int nchunk = NCH ? NCH : a.ci_pad >> 7;
+    constexpr int SB = sb_rows(KS);
     // weights: [co tile][chunk][tap][kq][wave][nt][lane][8] bf16 -> 512 bf16x8 per K-step
     const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + ((long)by * nchunk * NKC) * 512 + wave * 128 + lane;
     auto wload = [&](bf16x8 (&w)[2], int kk) {
@@ -121,18 +135,20 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                     cs[384 + tid] = sh;
                 }
             }
-            // the tile's rows (+ dilation halo) in SB / SBB batches of SBB 16-B loads per thread
+            // the tile's rows (+ dilation halo): SB 16-B loads per thread, then the transform in registers, then the
+            // LDS stores.  Interior tiles (every staged row inside [0, T_in), every channel < Ci: all but the first
+            // and last tile of an utterance) take a path without the clamps and the zero-padding masks.
+            auto stage = [&](auto full_tag) {
+                constexpr bool FULL = decltype(full_tag)::value;
+                uint4 raw[SB];
 #pragma unroll
-            for (int bt = 0; bt < SB / SBB; ++bt) {
-                uint4 raw[SBB];
-#pragma unroll
-                for (int i = 0; i < SBB; ++i) {  // 32-bit offsets from the utterance base (SGPR): saddr loads
-                    int tin = t0 - a.pad + rsub + 16 * (bt * SBB + i);
-                    tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+                for (int i = 0; i < SB; ++i) {  // 32-bit offsets from the utterance base (SGPR): saddr loads
+                    int tin = t0 - a.pad + rsub + 16 * i;
+                    if constexpr (!FULL) tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
                     const unsigned off = (unsigned)(tin * (int)a.ldx + cl) * 2u;
                     raw[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(X) + off);
                 }
-                if (bt == 0) __syncthreads();  // constants visible
+                __syncthreads();  // constants visible
                 // pair-major: the constants of one channel pair (10 registers) at a time, each vector's
                 // pair transformed in place (the staging holds only the raw vectors + one pair's constants)
                 const float slope = a.pro_slope;
@@ -150,7 +166,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                         km = *reinterpret_cast<const f32x2*>(cs + 512 + c0);
                     }
 #pragma unroll
-                    for (int i = 0; i < SBB; ++i) {
+                    for (int i = 0; i < SB; ++i) {
                         const uint32_t w = rw[4 * i + p];
                         const f32x2 x = f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)};
                         f32x2 y = x * ksc + ksh;  // v_pk_fma_f32
@@ -162,48 +178,69 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                             y.x = y.x >= 0.f ? y.x : y.x * slope;
                             y.y = y.y >= 0.f ? y.y : y.y * slope;
                         }
-                        const int tin = t0 - a.pad + rsub + 16 * (bt * SBB + i);  // zero padding / channels past Ci
-                        const bool ok = c_ok && tin >= 0 && tin < a.T_in;
-                        rw[4 * i + p] = ok ? pack2bf(y.x, y.y) : 0u;
+                        if constexpr (FULL) {
+                            rw[4 * i + p] = pack2bf(y.x, y.y);
+                        } else {
+                            const int tin = t0 - a.pad + rsub + 16 * i;  // zero padding / channels past Ci
+                            const bool ok = c_ok && tin >= 0 && tin < a.T_in;
+                            rw[4 * i + p] = ok ? pack2bf(y.x, y.y) : 0u;
+                        }
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < SBB; ++i) {
-                    const int r = rsub + 16 * (bt * SBB + i);
+                for (int i = 0; i < SB; ++i) {
+                    const int r = rsub + 16 * i;
                     if (r < rows_in) *reinterpret_cast<uint4*>(smem + r * P + cv * 16) = raw[i];
                 }
-            }
+            };
+            const bool interior = t0 - a.pad >= 0 && t0 - a.pad + 16 * SB <= a.T_in && cc * 128 + 128 <= a.Ci;
+            if (interior)
+                stage(std::integral_constant<bool, true>{});
+            else
+                stage(std::integral_constant<bool, false>{});
         }
         __syncthreads();
-        if (cc == 0) {  // (after the first staging: the accumulators are not live across it)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
         // K loop: no barrier.  K-step s = tap*4 + kq reads input rows t + tap*dil, channels kq*32 ..
+        // FIRST (the first chunk): K-step 0 takes the MFMA's inline-constant 0 as its C operand instead of 64
+        // v_mov zeroings of the accumulators (the same sums: 0 + products either way)
+        auto kloop = [&](auto first_tag) {
+            constexpr bool FIRST = decltype(first_tag)::value;
+            const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
+            for (int mt = 0; mt < 8; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
 #pragma unroll
-        for (int s = 0; s < NKC; ++s) {
-            if (s + 2 < NKC) wload(wf[(s + 2) % 3], kb + s + 2);
-            const int sn = s + 1;
-            const int offn = (sn >> 2) * dP + (sn & 3) * 64;
+            for (int s = 0; s < NKC; ++s) {
+                if (s + 2 < NKC) wload(wf[(s + 2) % 3], kb + s + 2);
+                const int sn = s + 1;
+                const int offn = (sn >> 2) * dP + (sn & 3) * 64;
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
-                acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % 3][0], xf[mt], acc[0][mt], 0, 0, 0);
-                acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % 3][1], xf[mt], acc[1][mt], 0, 0, 0);
-                if (sn < NKC) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + offn + mt * 16 * P);
+                for (int mt = 0; mt < 8; ++mt) {
+                    const bool z = FIRST && s == 0;
+                    acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % 3][0], xf[mt], z ? zero : acc[0][mt], 0, 0, 0);
+                    acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % 3][1], xf[mt], z ? zero : acc[1][mt], 0, 0, 0);
+                    if (sn < NKC) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + offn + mt * 16 * P);
+                }
+                if (s + 2 < NKC) {
+                    __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // the two weight loads first
+                }
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    if (sn < NKC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
-            if (s + 2 < NKC) {
-                __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // the two weight loads first
-            }
+        };
+        if constexpr (NCH == 1) {
+            kloop(std::integral_constant<bool, true>{});
+        } else {  // (two K-loop bodies spill the multi-chunk forms: zero the accumulators once instead)
+            if (cc == 0) {
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                if (sn < NKC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            __builtin_amdgcn_sched_barrier(0);
+            kloop(std::integral_constant<bool, false>{});
         }
     }
     if (a.flags & 4) return;
@@ -217,25 +254,30 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 #pragma unroll
     for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
     const bool stat = a.stat_part != nullptr;
+    // residual rows at t / res_tdiv; the Snake (MRF) forms always have res_tdiv 1 (checked by the launcher)
+    constexpr bool TD1 = PACT == STZS_ACT_SNAKE;
+    const char* Rq = reinterpret_cast<const char*>(a.res) + (long)bq * a.bsr * 2;
+    const char* Aq = reinterpret_cast<const char*>(a.acc_in) + (long)bq * a.bsa * 2;
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
     const int nch = (a.T_out + 63) / 64;
+    // the residual / accumulate rows of BOTH halves in flight at once (the second half's HBM latency hides
+    // behind the first half's epilogue); uniform utterance bases + 32-bit per-lane offsets
+    uint4 rr[8], aa[8];
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+        const int t = t0 + mt * 16 + n;
+        const int tc = t < a.T_out ? t : a.T_out - 1;
+        if constexpr (HR) {
+            const int tr = TD1 ? tc : tc / a.res_tdiv;
+            rr[mt] = *reinterpret_cast<const uint4*>(Rq + (unsigned)(tr * (int)a.ldr + coc) * 2u);
+        }
+        if constexpr (HA) aa[mt] = *reinterpret_cast<const uint4*>(Aq + (unsigned)(tc * (int)a.lda + coc) * 2u);
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // two 64-row halves: one statistics partial each
         float ss[8], sq[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
-        uint4 rr[4], aa[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int t = t0 + (h * 4 + m) * 16 + n;
-            const int tc = t < a.T_out ? t : a.T_out - 1;
-            if constexpr (HR)
-                rr[m] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr +
-                                                        (long)(tc / a.res_tdiv) * a.ldr + coc);
-            if constexpr (HA)
-                aa[m] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(a.acc_in) + (long)bq * a.bsa +
-                                                        (long)tc * a.lda + coc);
-        }
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const int mt = h * 4 + m;
@@ -248,15 +290,17 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[nt][mt][r] + bias[nt * 4 + r];
             if constexpr (HR) {
                 float f[8];
-                unpack8(rr[m], f);
+                unpack8(rr[mt], f);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] += f[i];
             }
+            if constexpr (AL) {  // (x * 1 == x: the alpha == 1 forms skip it without changing a bit)
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] *= a.alpha;
+                for (int i = 0; i < 8; ++i) v[i] *= a.alpha;
+            }
             if constexpr (HA) {
                 float f[8];
-                unpack8(aa[m], f);
+                unpack8(aa[mt], f);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = fmaf(a.beta, f[i], v[i]);
             }
@@ -273,11 +317,8 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
             }
         }
         if (stat) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                ss[i] = row_sum16(ss[i]);
-                sq[i] = row_sum16(sq[i]);
-            }
+            row_sum16_n<8>(ss);
+            row_sum16_n<8>(sq);
             const int r0 = t0 + h * 64;
             if (n == 0 && col_ok && r0 < a.T_out) {
                 float* Pp = reinterpret_cast<float*>(a.stat_part) + (((long)bq * nch + r0 / 64) * a.stat_ld + co0) * 2;
@@ -291,18 +332,19 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     }
 }
 
-template <int PACT, bool HR, bool HA, int NCH>
+template <int PACT, bool HR, bool HA, int NCH, bool AL>
 void (*pick_ks(int ks))(stzs_conv_args) {
     switch (ks) {
-        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH>;
-        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH>;
-        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH>;
+        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL>;
+        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL>;
+        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH, AL>;
         default: return nullptr;
     }
 }
 template <int PACT, bool HR, bool HA>
-void (*pick(int ks, bool one))(stzs_conv_args) {
-    return one ? pick_ks<PACT, HR, HA, 1>(ks) : pick_ks<PACT, HR, HA, 0>(ks);
+void (*pick(int ks, bool one, bool al))(stzs_conv_args) {
+    if (al) return one ? pick_ks<PACT, HR, HA, 1, true>(ks) : pick_ks<PACT, HR, HA, 0, true>(ks);
+    return one ? pick_ks<PACT, HR, HA, 1, false>(ks) : pick_ks<PACT, HR, HA, 0, false>(ks);
 }
 
 }  // namespace
@@ -312,12 +354,13 @@ int stzs_mrfp_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrfp
 // internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32 weights
 __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s) {
     const int rows_in = BT + (a.ks - 1) * a.dil;
-    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || rows_in > 16 * SB ||
+    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || rows_in > 16 * (a.ks == 3 ? sb_rows(3) : a.ks == 7 ? sb_rows(7) : SB_MAX) ||
         a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.gate || a.epi_act != STZS_ACT_NONE || a.ups ||
         a.refl || a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv <= 0)) ||
         (a.acc_in && (a.lda % 8 || a.bsa % 8)) || (a.stat_part && a.stat_ld < a.Co))
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
+    if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
     {  // STZS_CONV_MRF_PIPE: the k3 single-chunk residual convs on the persistent LDS-DMA-pipelined form (mrfp.hip)
         const int r = stzs_mrfp_conv_launch(a, s);
         if (r != 1) return r;
@@ -327,13 +370,14 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
     if (a.pro_act == STZS_ACT_SNAKE) {
         const bool one = a.ci_pad == 128;
-        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one))
-              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one));
+        const bool al = a.alpha != 1.f;
+        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al))
+              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al));
     } else if (!A && a.ks == 3) {  // the AdaIN residual blocks of the decoder / prosody predictor
         if (a.pro_act == STZS_ACT_LEAKY)
-            k = R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0>;
+            k = R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true>;
         else if (a.pro_act == STZS_ACT_NONE)
-            k = R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0>;
+            k = R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0, true>;
     }
     if (!k) return STZS_ESHAPE;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
