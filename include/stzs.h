@@ -120,6 +120,12 @@ typedef struct stzs_conv_args {
  * the two-stream bench the step time is unchanged and its resident persistent workgroups can hold back the
  * co-resident LSTM launch of the concurrent stream. */
 #define STZS_CONV_MRF_PIPE 512
+/* flags: PRECISE split-operand form (csrc/conv.hip conv_x3).  w = two bf16 K-step streams (hi = bf16(w),
+ * then lo = bf16(w - hi)), each [co_pad/128][ci_pad/32 * ks][128][32] in the STZS_PACK_KSTEP swizzle with
+ * cic = 32 (stzs/weights.py kstep_stream_x3); activations are split the same way when staged, and every
+ * product is ah*bh + ah*bl + al*bh on bf16 MFMA with fp32 accumulation (~fp32 accuracy at ~3x bf16 work).
+ * Requires cic = 32; any in/out dtype; the accurate (libm) prologue activations. */
+#define STZS_CONV_W_X3 1024
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------
@@ -171,7 +177,8 @@ typedef struct stzs_quant_args {
 int stzs_quant_rows(const stzs_quant_args* a, void* stream);
 
 /* ---- multi-head attention, softmax(q k^T / sqrt(dh)) v, rows independent ----------------
- * q [R, Lq, ldq], k/v [R, Lk, ldk/ldv], o [R, Lq, ldo]; bf16; heads x dh = D.
+ * q [R, Lq, ldq], k/v [R, Lk, ldk/ldv], o [R, Lq, ldo]; bf16 (precise = 0, MFMA flash kernel) or fp32
+ * (precise = 1: fp32 dot products, libm expf -- the split-operand precise mode); heads x dh = D.
  * (denoiser self-attention over L_s codes, cross-attention to context) */
 typedef struct stzs_attn_args {
     const void* q;
@@ -179,7 +186,7 @@ typedef struct stzs_attn_args {
     const void* v;
     void* o;
     int64_t ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso;
-    int32_t R, Lq, Lk, heads, dh, pad_i;
+    int32_t R, Lq, Lk, heads, dh, precise;
 } stzs_attn_args;
 int stzs_attention(const stzs_attn_args* a, void* stream);
 
@@ -206,7 +213,10 @@ typedef struct stzs_lstm_args {
      * status of every launch of a captured graph; the caller reads it after the work (StyleTTSZS raises). */
     uint32_t* status;
     uint32_t spin_limit; /* polls before a spin times out; 0 = default (1 << 22). Tests force small values. */
-    uint32_t pad_u;
+    /* 1 = PRECISE split-operand mode: whhT holds the hi fragments of both directions followed by the lo ones
+     * (stzs/weights.py pack_lstm(x3=True)), h is exchanged as hi | lo bf16, the gates use libm expf / tanhf
+     * and y is fp32 [b, t, dir*H + j].  0 = bf16 h / bf16 y. */
+    uint32_t precise;
 } stzs_lstm_args;
 #define STZS_STATUS_LSTM_TIMEOUT 1u
 size_t stzs_lstm_workspace(int B, int H, int ndir);
@@ -220,7 +230,7 @@ typedef struct stzs_prprep_args {
     const void* h;
     void* y;
     int64_t ldc, bsc, ldh, bsh, ldy, bsy;
-    int32_t B, L, T, c0, Cs, Ch, yc0, pad_i;
+    int32_t B, L, T, c0, Cs, Ch, yc0, f32; /* f32 = 1: h and y fp32 (precise mode), 0: bf16 */
 } stzs_prprep_args;
 int stzs_predictor_prep(const stzs_prprep_args* a, void* stream);
 
@@ -388,6 +398,8 @@ int stzs_dn_cond(const float* pool, const float* temb, void* c, int R, int D, vo
 /* the same for every sampler step at once: c[s][r][j] = silu(pool[r][j] + temb[s][j]), s < steps (the
  * step-invariant conditioning of a whole sampling run in one launch instead of one per NFE) */
 int stzs_dn_cond_steps(const float* pool, const float* temb, void* c, int R, int D, int steps, void* stream);
+/* precise mode: the same with fp32 c */
+int stzs_dn_cond_steps_f32(const float* pool, const float* temb, float* c, int R, int D, int steps, void* stream);
 /* out[l][r][j] = mod[r][j] + (table ? table[l][j] : 0) + ((j / D) in scale_mask ? 1 : 0) */
 int stzs_adaln_expand(const float* mod, const float* table, float* out, int R, int D, int nchunk,
                       int nlayers, unsigned scale_mask, void* stream);
@@ -412,6 +424,8 @@ int stzs_copy2d(const stzs_copy_args* a, void* stream);
 /* token embedding gather: y[b, t, :] = emb[tok[b, t], :] (f32 table -> bf16 rows) */
 int stzs_embed(const int32_t* tok, const float* emb, void* y, int B, int T, int D, int64_t ldy,
                void* stream);
+/* precise mode: fp32 embedding rows */
+int stzs_embed_f32(const int32_t* tok, const float* emb, float* y, int B, int T, int D, int64_t ldy, void* stream);
 
 /* ======================================================================================================
  * Generic tensor-descriptor entry points (SURVEY.md §8(b) "C-ABI"): one per hot-path operator of §8(a),

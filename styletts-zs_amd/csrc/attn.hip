@@ -138,6 +138,73 @@ __global__ __launch_bounds__(256) void attn_mfma(const stzs_attn_args a) {
     }
 }
 
+// PRECISE mode (stzs_attn_args.precise = 1): fp32 q / k / v / o, fp32 dot products and libm expf on the VALU,
+// online softmax per 64-key chunk.  One thread per query, one workgroup per (row, head, 256 queries): the
+// denoiser's 50 x (<= a few hundred) x 64 per head is small, this path exists for fp32-level parity.
+constexpr int KC32 = 64;
+template <int DH>
+__global__ __launch_bounds__(256) void attn_f32(const stzs_attn_args a) {
+    __shared__ float Ks[KC32][DH + 1];
+    __shared__ float Vs[KC32][DH + 1];
+    const int tid = threadIdx.x;
+    const long r = blockIdx.x;
+    const int h = blockIdx.y;
+    const int qi = blockIdx.z * 256 + tid;
+    const bool qok = qi < a.Lq;
+    const float* Q = reinterpret_cast<const float*>(a.q) + r * a.bsq + h * DH;
+    const float* K = reinterpret_cast<const float*>(a.k) + r * a.bsk + h * DH;
+    const float* V = reinterpret_cast<const float*>(a.v) + r * a.bsv + h * DH;
+    const float scale = 1.f / sqrtf((float)DH);
+    float q[DH], o[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) {
+        q[d] = qok ? Q[(long)qi * a.ldq + d] : 0.f;
+        o[d] = 0.f;
+    }
+    float m = -INFINITY, l = 0.f;
+    for (int c0 = 0; c0 < a.Lk; c0 += KC32) {
+        const int nk = min(KC32, a.Lk - c0);
+        __syncthreads();
+        for (int i = tid; i < KC32 * DH; i += 256) {  // rows past nk zeroed (read, masked)
+            const int kr = i / DH, d = i - kr * DH;
+            const bool ok = kr < nk;
+            Ks[kr][d] = ok ? K[(long)(c0 + kr) * a.ldk + d] : 0.f;
+            Vs[kr][d] = ok ? V[(long)(c0 + kr) * a.ldv + d] : 0.f;
+        }
+        __syncthreads();
+        if (!qok) continue;
+        // (static key indices keep sv in registers; keys past nk are masked, not branched around)
+        float sv[KC32];
+        float mx = m;
+#pragma unroll
+        for (int j = 0; j < KC32; ++j) {
+            float acc = 0.f;
+#pragma unroll
+            for (int d = 0; d < DH; ++d) acc = fmaf(q[d], Ks[j][d], acc);
+            sv[j] = j < nk ? acc * scale : -INFINITY;
+            mx = fmaxf(mx, sv[j]);
+        }
+        const float corr = expf(m - mx);
+        l *= corr;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) o[d] *= corr;
+#pragma unroll
+        for (int j = 0; j < KC32; ++j) {
+            const float pj = j < nk ? expf(sv[j] - mx) : 0.f;
+            l += pj;
+#pragma unroll
+            for (int d = 0; d < DH; ++d) o[d] = fmaf(pj, Vs[j][d], o[d]);
+        }
+        m = mx;
+    }
+    if (qok) {
+        float* O = reinterpret_cast<float*>(a.o) + r * a.bso + h * DH + (long)qi * a.ldo;
+        const float inv = 1.f / l;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) O[d] = o[d] * inv;
+    }
+}
+
 }  // namespace
 
 extern "C" int stzs_attention(const stzs_attn_args* a, void* stream) {
@@ -145,6 +212,18 @@ extern "C" int stzs_attention(const stzs_attn_args* a, void* stream) {
     if (a->R <= 0 || a->Lq <= 0 || a->Lk <= 0 || a->heads <= 0) return STZS_ESHAPE;
     if (a->ldq % 8 || a->ldk % 8 || a->ldv % 8 || a->bsq % 8 || a->bsk % 8 || a->bsv % 8) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (a->precise == 1) {
+        dim3 g((unsigned)a->R, a->heads, (a->Lq + 255) / 256);
+        if (a->dh == 64)
+            hipLaunchKernelGGL(attn_f32<64>, g, dim3(256), 0, s, *a);
+        else if (a->dh == 32)
+            hipLaunchKernelGGL(attn_f32<32>, g, dim3(256), 0, s, *a);
+        else
+            return STZS_ESHAPE;
+        STZS_LAUNCH_CHECK();
+        return STZS_OK;
+    }
+    if (a->precise != 0) return STZS_EINVAL;
     dim3 g((unsigned)a->R, a->heads, (a->Lq + 63) / 64);
     if (a->dh == 64)
         hipLaunchKernelGGL(attn_mfma<64>, g, dim3(256), 0, s, *a);

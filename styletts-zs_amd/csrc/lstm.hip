@@ -17,6 +17,10 @@
 //     consumers poll that counter with sc1 loads, then all loads of the slab are sc1 (no fences).
 //     Spins are bounded: on timeout the kernel records an error word and finishes (never hangs).
 // Residency: grid = P x ndir x groups <= 64 workgroups, one per CU: always co-resident on MI355X.
+// PRECISE (stzs_lstm_args.precise, the split-operand mode): h travels as hi = bf16(h) and lo = bf16(h - hi)
+// (one slab row = hi[H] | lo[H]), W_hh^T as hi and lo fragments, the recurrent product is
+// h_lo W_hi + h_hi W_lo + h_hi W_hi on the same MFMAs (~fp32 accuracy), the gates use libm expf / tanhf,
+// and y is written in fp32.
 #include "common.hpp"
 
 namespace {
@@ -48,13 +52,16 @@ STZS_DEV float fast_tanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
-template <int NKS>
+STZS_DEV float acc_sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
+
+template <int NKS, bool PR>
 __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.H, G4 = 4 * H;
     const int hp = H + 8;
-    bf16_t* As = reinterpret_cast<bf16_t*>(smem);                                   // [64][hp]
-    float* gs = reinterpret_cast<float*>(smem + ((MROWS * hp * 2 + 15) & ~15));     // [64][4*UNITS + 4]
+    constexpr int NH = PR ? 2 : 1;  // slab row = hi[H] (| lo[H])
+    bf16_t* As = reinterpret_cast<bf16_t*>(smem);                                   // [NH][64][hp]
+    float* gs = reinterpret_cast<float*>(smem + ((NH * MROWS * hp * 2 + 15) & ~15)); // [64][4*UNITS + 4]
     __shared__ int s_ok;
     const int gp = 4 * UNITS + 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -64,23 +71,27 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     const int b0 = grp * MROWS;
     const int nrows = min(MROWS, a.B - b0);
     const int nmt = (nrows + 15) >> 4;
-    // exchange slab [group][dir][2][64][H] bf16, counters [group][dir] (16 words apart)
-    bf16_t* X = reinterpret_cast<bf16_t*>(a.xchg) + ((long)(grp * a.ndir + dir) * 2) * MROWS * H;
+    // exchange slab [group][dir][2][64][NH H] bf16, counters [group][dir] (16 words apart)
+    bf16_t* X = reinterpret_cast<bf16_t*>(a.xchg) + ((long)(grp * a.ndir + dir) * 2) * MROWS * NH * H;
     gu32* ctr = (gu32*)(a.sync) + (grp * a.ndir + dir) * 16;
     // the slab through a buffer descriptor: 16-B write-through (sc1, aux 16) stores and loads
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(X, 0, 2 * MROWS * H * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(X, 0, 2 * MROWS * NH * H * 2, 0x00020000);
     gu32* err = (gu32*)(a.sync) + 1023;
     gu32* status = (gu32*)a.status;
     const unsigned limit = a.spin_limit ? a.spin_limit : SPIN_LIMIT;
 
     // W_hh^T fragments of this wave's gate (g = wave) for the workgroup's 32 units, in registers
     const bf16_t* Wd = reinterpret_cast<const bf16_t*>(a.whhT) + (long)dir * (G4 / 16) * NKS * 512;
-    bf16x8 bw[2][NKS];
+    bf16x8 bw[2][NKS], bwl[PR ? 2 : 1][PR ? NKS : 1];
+    const long lo_off = (long)2 * (G4 / 16) * NKS * 512;  // PR: the lo fragments follow both directions' hi ones
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int ct = (gate * H + p * UNITS) / 16 + c;
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) bw[c][ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)ct * NKS + ks) * 512 + lane * 8);
+        for (int ks = 0; ks < NKS; ++ks) {
+            bw[c][ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)ct * NKS + ks) * 512 + lane * 8);
+            if constexpr (PR) bwl[c][ks] = *reinterpret_cast<const bf16x8*>(Wd + lo_off + ((long)ct * NKS + ks) * 512 + lane * 8);
+        }
     }
     // cells of this thread: row = tid / 8, units (tid % 8) * 4 .. +4
     constexpr int CPT = 4;
@@ -91,6 +102,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
 #pragma unroll
     for (int j = 0; j < CPT; ++j) c[j] = 0.f;
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
+    float* Yf = reinterpret_cast<float*>(a.y);
     if (tid == 0) s_ok = 1;
 
 #ifdef STZS_LSTM_PROF
@@ -109,26 +121,27 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         for (int g = 0; g < 4; ++g) gx[g] = *reinterpret_cast<const float4*>(G + g * H);
         // ---- wait for h_{s-1} from all P workgroups, stage it into the A tile ----
         if (s == 0) {
-            for (int e = tid; e < MROWS * hp / 8; e += 512) reinterpret_cast<uint4*>(As)[e] = make_uint4(0, 0, 0, 0);
+            for (int e = tid; e < NH * MROWS * hp / 8; e += 512) reinterpret_cast<uint4*>(As)[e] = make_uint4(0, 0, 0, 0);
         } else {
             if (tid == 0 && s_ok) s_ok = poll_ge(ctr, (unsigned)(P * s), err, status, limit);  // after a timeout: no more spins
             PROF(1)
             __syncthreads();
             // h_{s-1}: MROWS x H bf16 = H/8 16-B words per row, all of this thread's sc1 loads in flight
-            const int base = ((s - 1) & 1) * MROWS * H * 2;
-            constexpr int NWT = MROWS * NKS * 32 / 8;          // 16-B words of h (H = 32 NKS)
+            const int base = ((s - 1) & 1) * MROWS * NH * H * 2;
+            constexpr int NWT = MROWS * NH * NKS * 32 / 8;     // 16-B words of h (H = 32 NKS)
             constexpr int NW = (NWT + 511) / 512;              // per thread
             // only the group's valid rows (a batch-1 group moves 1/64 of the slab); rows >= nrows of the A
             // tile stay as zeroed at s = 0 and only feed gate rows no cell reads
-            const int nwt = nrows * (NKS * 32 / 8);
+            const int nwt = nrows * (NH * NKS * 32 / 8);
             u32x4 v[NW];
 #pragma unroll
             for (int i = 0; i < NW; ++i)  // uniform guard; the modulo keeps every address inside the rows
                 if (i * 512 < nwt) v[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, base + ((tid + i * 512) % nwt) * 16, 0, 16);
 #pragma unroll
             for (int i = 0; i < NW; ++i) {
-                const int e = tid + i * 512, r = (e * 8) / H, k = (e * 8) - r * H;
-                if (e < nwt) *reinterpret_cast<u32x4*>(As + r * hp + k) = v[i];
+                const int e = tid + i * 512, r = (e * 8) / (NH * H), k = (e * 8) - r * (NH * H);
+                const int hl = PR ? (k >= H) : 0;  // PR: lo half of the slab row -> the lo tile
+                if (e < nwt) *reinterpret_cast<u32x4*>(As + hl * MROWS * hp + r * hp + k - hl * H) = v[i];
             }
         }
         __syncthreads();
@@ -141,7 +154,15 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (mt * 16 + (lane & 15)) * hp + ks * 32 + 8 * (lane >> 4));
+                const int ao = (mt * 16 + (lane & 15)) * hp + ks * 32 + 8 * (lane >> 4);
+                const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + ao);
+                if constexpr (PR) {  // h_lo W_hi + h_hi W_lo + h_hi W_hi (small terms first)
+                    const bf16x8 afl = *reinterpret_cast<const bf16x8*>(As + MROWS * hp + ao);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl, bw[0][ks], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl, bw[1][ks], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bwl[0][ks], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bwl[1][ks], acc1, 0, 0, 0);
+                }
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[0][ks], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[1][ks], acc1, 0, 0, 0);
             }
@@ -161,21 +182,42 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
             const float* gr = gs + crow * gp + cu0 + j;
             const float gi = gr[0] + gx[0][j], gf = gr[UNITS] + gx[1][j], gg = gr[2 * UNITS] + gx[2][j],
                         go = gr[3 * UNITS] + gx[3][j];
-            const float ig = fast_sigmoid(gi), fg = fast_sigmoid(gf), og = fast_sigmoid(go);
-            c[j] = fg * c[j] + ig * fast_tanh(gg);
-            hv[j] = og * fast_tanh(c[j]);
+            if constexpr (PR) {
+                const float ig = acc_sigmoid(gi), fg = acc_sigmoid(gf), og = acc_sigmoid(go);
+                c[j] = fg * c[j] + ig * tanhf(gg);
+                hv[j] = og * tanhf(c[j]);
+            } else {
+                const float ig = fast_sigmoid(gi), fg = fast_sigmoid(gf), og = fast_sigmoid(go);
+                c[j] = fg * c[j] + ig * fast_tanh(gg);
+                hv[j] = og * fast_tanh(c[j]);
+            }
         }
         const uint2 hb = make_uint2(pack2bf(hv[0], hv[1]), pack2bf(hv[2], hv[3]));
         if (cvalid) {
             const __attribute__((ext_vector_type(2))) unsigned int hw = {hb.x, hb.y};
-            __builtin_amdgcn_raw_buffer_store_b64(hw, xr, ((s & 1) * MROWS * H + crow * H + p * UNITS + cu0) * 2, 0, 16);
+            const int so = ((s & 1) * MROWS * NH * H + crow * NH * H + p * UNITS + cu0) * 2;
+            __builtin_amdgcn_raw_buffer_store_b64(hw, xr, so, 0, 16);
+            if constexpr (PR) {  // lo = bf16(h - hi) (exact difference)
+                float hf[4];
+#pragma unroll
+                for (int j = 0; j < CPT; ++j) hf[j] = hv[j] - __uint_as_float((j & 1) ? ((j < 2 ? hb.x : hb.y) & 0xFFFF0000u)
+                                                                                      : ((j < 2 ? hb.x : hb.y) << 16));
+                const __attribute__((ext_vector_type(2))) unsigned int lw = {pack2bf(hf[0], hf[1]), pack2bf(hf[2], hf[3])};
+                __builtin_amdgcn_raw_buffer_store_b64(lw, xr, so + H * 2, 0, 16);
+            }
         }
         PROF(4)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the layer output (read by later launches only) leaves after the signal, outside the drain
-        if (cvalid) *reinterpret_cast<uint2*>(Y + (long)cb * a.bsy + (long)t * a.ldy + dir * H + p * UNITS + cu0) = hb;
+        if (cvalid) {
+            const long yo = (long)cb * a.bsy + (long)t * a.ldy + dir * H + p * UNITS + cu0;
+            if constexpr (PR)
+                *reinterpret_cast<float4*>(Yf + yo) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+            else
+                *reinterpret_cast<uint2*>(Y + yo) = hb;
+        }
         PROF(5)
     }
 #ifdef STZS_LSTM_PROF
@@ -205,7 +247,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
 
 extern "C" size_t stzs_lstm_workspace(int B, int H, int ndir) {
     const int groups = (B + MROWS - 1) / MROWS;
-    return (size_t)groups * ndir * 2 * MROWS * H * sizeof(bf16_t);
+    return (size_t)groups * ndir * 2 * MROWS * 2 * H * sizeof(bf16_t);  // (sized for the precise hi | lo rows)
 }
 
 extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
@@ -219,13 +261,16 @@ extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // the counters start at zero (caller-zeroed once) and every call leaves them zeroed (see the kernel's
     // tail); the caller's status word (a->status) accumulates over calls and is never cleared here
+    if (a->precise > 1) return STZS_EINVAL;
+    if (a->precise && (a->ldy % 4 || a->bsy % 4)) return STZS_ESHAPE;
     const int hp = a->H + 8;
-    const size_t lds = ((MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4;
+    const int nh = a->precise ? 2 : 1;
+    const size_t lds = ((nh * MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4;
     dim3 grid(P, a->ndir, groups);
     switch (a->H / 32) {
 #define STZS_LSTM_CASE(n)                                                                                   \
     case n: {                                                                                               \
-        auto k = lstm_xchg<n>;                                                                              \
+        auto k = a->precise ? lstm_xchg<n, true> : lstm_xchg<n, false>;                                     \
         if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
         hipLaunchKernelGGL(k, grid, dim3(512), lds, s, *a);                                                 \
         break;                                                                                              \

@@ -11,7 +11,8 @@
 namespace {
 
 // c[s][r][j] = silu(pool[r][j] + temb[s][j]) for all sampler steps s at once
-__global__ void dn_cond_kernel(const float* pool, const float* temb, bf16_t* c, int R, int D, int steps) {
+template <typename TO>
+__global__ void dn_cond_kernel(const float* pool, const float* temb, TO* c, int R, int D, int steps) {
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     const long rd = (long)R * D;
     if (i >= rd * steps) return;
@@ -19,7 +20,7 @@ __global__ void dn_cond_kernel(const float* pool, const float* temb, bf16_t* c, 
     const long rj = i - s * rd;
     const int j = (int)(rj % D);
     const float x = pool[rj] + temb[(long)s * D + j];
-    c[i] = f2bf(x / (1.f + expf(-x)));
+    DT<TO>::st(c + i, x / (1.f + expf(-x)));
 }
 
 __global__ void adaln_expand_kernel(const float* mod, const float* table, float* out, int R, int D, int nchunk,
@@ -81,12 +82,13 @@ __global__ void copy_kernel(const stzs_copy_args a) {
     DT<TO>::st(reinterpret_cast<TO*>(a.y) + b * a.bsy + rr * a.ldy + c, v);
 }
 
-__global__ void embed_kernel(const int32_t* tok, const float* emb, bf16_t* y, int B, int T, int D, long ldy) {
+template <typename TO>
+__global__ void embed_kernel(const int32_t* tok, const float* emb, TO* y, int B, int T, int D, long ldy) {
     const int t = blockIdx.x, b = blockIdx.y;
     const int id = tok[(long)b * T + t];
     const float* e = emb + (long)id * D;
-    bf16_t* o = y + ((long)b * T + t) * ldy;
-    for (int c = threadIdx.x; c < D; c += 256) o[c] = f2bf(e[c]);
+    TO* o = y + ((long)b * T + t) * ldy;
+    for (int c = threadIdx.x; c < D; c += 256) DT<TO>::st(o + c, e[c]);
 }
 
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
@@ -96,7 +98,7 @@ inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 extern "C" int stzs_dn_cond(const float* pool, const float* temb, void* c, int R, int D, void* stream) {
     if (!pool || !temb || !c) return STZS_EINVAL;
     if (R <= 0 || D <= 0) return STZS_ESHAPE;
-    hipLaunchKernelGGL(dn_cond_kernel, dim3(nblk((long)R * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(dn_cond_kernel<bf16_t>, dim3(nblk((long)R * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        pool, temb, reinterpret_cast<bf16_t*>(c), R, D, 1);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
@@ -106,8 +108,18 @@ extern "C" int stzs_dn_cond_steps(const float* pool, const float* temb, void* c,
                                   void* stream) {
     if (!pool || !temb || !c) return STZS_EINVAL;
     if (R <= 0 || D <= 0 || steps <= 0) return STZS_ESHAPE;
-    hipLaunchKernelGGL(dn_cond_kernel, dim3(nblk((long)R * D * steps)), dim3(256), 0,
+    hipLaunchKernelGGL(dn_cond_kernel<bf16_t>, dim3(nblk((long)R * D * steps)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), pool, temb, reinterpret_cast<bf16_t*>(c), R, D, steps);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_dn_cond_steps_f32(const float* pool, const float* temb, float* c, int R, int D, int steps,
+                                      void* stream) {
+    if (!pool || !temb || !c) return STZS_EINVAL;
+    if (R <= 0 || D <= 0 || steps <= 0) return STZS_ESHAPE;
+    hipLaunchKernelGGL(dn_cond_kernel<float>, dim3(nblk((long)R * D * steps)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), pool, temb, c, R, D, steps);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }
@@ -174,8 +186,18 @@ extern "C" int stzs_embed(const int32_t* tok, const float* emb, void* y, int B, 
                           void* stream) {
     if (!tok || !emb || !y) return STZS_EINVAL;
     if (B <= 0 || T <= 0 || D <= 0) return STZS_ESHAPE;
-    hipLaunchKernelGGL(embed_kernel, dim3(T, B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), tok, emb,
+    hipLaunchKernelGGL(embed_kernel<bf16_t>, dim3(T, B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), tok, emb,
                        reinterpret_cast<bf16_t*>(y), B, T, D, (long)ldy);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_embed_f32(const int32_t* tok, const float* emb, float* y, int B, int T, int D, int64_t ldy,
+                              void* stream) {
+    if (!tok || !emb || !y) return STZS_EINVAL;
+    if (B <= 0 || T <= 0 || D <= 0) return STZS_ESHAPE;
+    hipLaunchKernelGGL(embed_kernel<float>, dim3(T, B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), tok, emb,
+                       y, B, T, D, (long)ldy);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

@@ -6,12 +6,16 @@
 
 namespace {
 
+template <typename TT>
 __global__ __launch_bounds__(256) void pr_prep(const stzs_prprep_args a) {
     const int t = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-    bf16_t* Y = reinterpret_cast<bf16_t*>(a.y) + (long)b * a.bsy + (long)t * a.ldy;
-    const bf16_t* Hs = reinterpret_cast<const bf16_t*>(a.h) + (long)b * a.bsh + (long)t * a.ldh;
-    for (int v = tid; v < a.Ch / 8; v += 256)
-        *reinterpret_cast<uint4*>(Y + v * 8) = *reinterpret_cast<const uint4*>(Hs + v * 8);
+    TT* Y = reinterpret_cast<TT*>(a.y) + (long)b * a.bsy + (long)t * a.ldy;
+    const TT* Hs = reinterpret_cast<const TT*>(a.h) + (long)b * a.bsh + (long)t * a.ldh;
+    for (int v = tid; v < a.Ch / 8; v += 256) {
+        float f[8];
+        load8(Hs + v * 8, f);
+        store8(Y + v * 8, f);
+    }
     // torch upsample_linear1d, align_corners=False (area_pixel_compute_source_index)
     const float ratio = (float)a.L / (float)a.T;
     float src = ratio * ((float)t + 0.5f) - 0.5f;
@@ -23,7 +27,7 @@ __global__ __launch_bounds__(256) void pr_prep(const stzs_prprep_args a) {
     const float l0 = 1.f - l1;
     const float* C0 = a.codes + (long)b * a.bsc + (long)i0 * a.ldc + a.c0;
     const float* C1 = a.codes + (long)b * a.bsc + (long)i1 * a.ldc + a.c0;
-    for (int c = tid; c < a.Cs; c += 256) Y[a.yc0 + c] = f2bf(l0 * C0[c] + l1 * C1[c]);
+    for (int c = tid; c < a.Cs; c += 256) DT<TT>::st(Y + a.yc0 + c, l0 * C0[c] + l1 * C1[c]);
 }
 
 __global__ __launch_bounds__(256) void dur_kernel(const stzs_dur_args a) {
@@ -142,7 +146,11 @@ __global__ __launch_bounds__(256) void f0n_kernel(const stzs_f0n_args a) {
 extern "C" int stzs_predictor_prep(const stzs_prprep_args* a, void* stream) {
     if (!a || !a->codes || !a->h || !a->y) return STZS_EINVAL;
     if (a->B <= 0 || a->T <= 0 || a->L <= 0 || a->Ch % 8 || a->ldh % 8 || a->ldy % 8) return STZS_ESHAPE;
-    hipLaunchKernelGGL(pr_prep, dim3(a->T, a->B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), *a);
+    if (a->f32 > 1) return STZS_EINVAL;
+    if (a->f32)
+        hipLaunchKernelGGL(pr_prep<float>, dim3(a->T, a->B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), *a);
+    else
+        hipLaunchKernelGGL(pr_prep<bf16_t>, dim3(a->T, a->B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), *a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

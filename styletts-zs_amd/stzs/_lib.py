@@ -20,7 +20,8 @@ CONV_STAT_ROWS = 64  # include/stzs.h STZS_CONV_STAT_ROWS
 CONV_W_LANE16 = 16  # include/stzs.h STZS_CONV_W_LANE16
 CONV_W_NARROW32 = 32  # include/stzs.h STZS_CONV_W_NARROW32
 CONV_W_FRAG32 = 256  # include/stzs.h STZS_CONV_W_FRAG32
-CONV_W_F32 = 64  # include/stzs.h STZS_CONV_W_F32 (precise mode)
+CONV_W_F32 = 64  # include/stzs.h STZS_CONV_W_F32 (fp32-MFMA conv_f32)
+CONV_W_X3 = 1024  # include/stzs.h STZS_CONV_W_X3 (precise mode: split-operand bf16x3 conv_x3)
 CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD remap)
 CONV_MRF_PIPE = 512  # include/stzs.h STZS_CONV_MRF_PIPE (k3 residual MRF convs on csrc/mrfp.hip, opt-in)
 
@@ -62,14 +63,14 @@ class QuantArgs(C.Structure):
 class AttnArgs(C.Structure):
     _fields_ = [("q", vp), ("k", vp), ("v", vp), ("o", vp)] + \
                [(n, i64) for n in ("ldq", "ldk", "ldv", "ldo", "bsq", "bsk", "bsv", "bso")] + \
-               [(n, i32) for n in ("R", "Lq", "Lk", "heads", "dh", "pad_i")]
+               [(n, i32) for n in ("R", "Lq", "Lk", "heads", "dh", "precise")]
 
 
 class LstmArgs(C.Structure):
     _fields_ = [("gx", vp), ("whhT", vp), ("y", vp), ("xchg", vp), ("sync", vp),
                 ("ldg", i64), ("bsg", i64), ("ldy", i64), ("bsy", i64),
                 ("B", i32), ("T", i32), ("H", i32), ("ndir", i32),
-                ("status", vp), ("spin_limit", C.c_uint32), ("pad_u", C.c_uint32)]
+                ("status", vp), ("spin_limit", C.c_uint32), ("precise", C.c_uint32)]
 
 
 STATUS_LSTM_TIMEOUT = 1  # include/stzs.h STZS_STATUS_LSTM_TIMEOUT
@@ -78,7 +79,7 @@ STATUS_LSTM_TIMEOUT = 1  # include/stzs.h STZS_STATUS_LSTM_TIMEOUT
 class PrPrepArgs(C.Structure):
     _fields_ = [("codes", vp), ("h", vp), ("y", vp)] + \
                [(n, i64) for n in ("ldc", "bsc", "ldh", "bsh", "ldy", "bsy")] + \
-               [(n, i32) for n in ("B", "L", "T", "c0", "Cs", "Ch", "yc0", "pad_i")]
+               [(n, i32) for n in ("B", "L", "T", "c0", "Cs", "Ch", "yc0", "f32")]
 
 
 class DurArgs(C.Structure):
@@ -198,7 +199,7 @@ EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_ch
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
            "stzs_stft_frames", "stzs_log_mel", "stzs_pool_rows", "stzs_code_quantize",
            "stzs_dn_cond", "stzs_dn_cond_steps", "stzs_adaln_expand", "stzs_cfg_euler",
-           "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed", "stzs_pack_conv_size", "stzs_pack_conv",
+           "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed", "stzs_embed_f32", "stzs_dn_cond_steps_f32", "stzs_pack_conv_size", "stzs_pack_conv",
            "stzs_pack_lstm"] + [f"stzs_{o}{sfx}" for o in GENERIC_OPS for sfx in ("", "_workspace")]
 
 _lib = None
@@ -246,6 +247,7 @@ def load():
         "stzs_pool_rows": ([P(PoolArgs), vp], i32),
         "stzs_code_quantize": ([P(VqArgs), vp], i32),
         "stzs_dn_cond_steps": ([vp, vp, vp, i32, i32, i32, vp], i32),
+        "stzs_dn_cond_steps_f32": ([vp, vp, vp, i32, i32, i32, vp], i32),
         "stzs_dn_cond":([vp, vp, vp, i32, i32, vp], i32),
         "stzs_adaln_expand": ([vp, vp, vp, i32, i32, i32, i32, C.c_uint32, vp], i32),
         "stzs_cfg_euler": ([vp, vp, i32, i32, i32, f32, f32, f32, vp], i32),
@@ -253,6 +255,7 @@ def load():
         "stzs_mean_rows": ([vp, vp, i32, i32, i64, i64, i32, i32, i64, vp], i32),
         "stzs_copy2d": ([P(CopyArgs), vp], i32),
         "stzs_embed": ([vp, vp, vp, i32, i32, i32, i64, vp], i32),
+        "stzs_embed_f32": ([vp, vp, vp, i32, i32, i32, i64, vp], i32),
         "stzs_pack_conv_size": ([i32, i32, i32, i32, i32], C.c_size_t),
         "stzs_pack_conv": ([vp, i32, i32, i32, i32, i32, vp], i32),
         "stzs_pack_lstm": ([vp] * 8 + [i32, i32, vp, vp, vp], i32),

@@ -103,29 +103,38 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
-                 packed: PackedModel = None, branch_streams=False):
+                 packed: PackedModel = None, branch_streams=False, precise=False):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
-        precise_decoder: PARITY mode -- the decoder (pre-blocks, generator, conv_post) keeps fp32 activations
-        and runs every conv on fp32 MFMA operands (STZS_CONV_W_F32) to meet the north-star mel-L1 <= 1e-3 vs
-        the fp32 oracle; slower, not the benchmark path (bf16 weights alone cost ~1.3e-2).
+        precise_decoder: PARITY mode for the decoder -- pre-blocks, generator and conv_post keep fp32 activations
+        and run every conv on split bf16 operands (hi*hi + hi*lo + lo*hi, STZS_CONV_W_X3, csrc/conv.hip conv_x3).
+        precise: the whole pipeline in that mode -- text encoder, style diffusion and prosody predictor too (fp32
+        activations, split-operand convs / linears / LSTM recurrences, fp32 attention, libm activations) -- the
+        mode that meets the north-star log-mel L1 <= 1e-3 END TO END vs the fp32 oracle (tools/precision_probe.py:
+        2.2e-4 in emulation); bf16 weights/activations alone cost ~5e-2.  The reference-prompt
+        front end stays bf16: its output is quantised to discrete codes.
         branch_streams: run the independent branches (text encoder || prompt encoder, F0 || N predictor branches)
         on forked side streams (graph-capturable: the fork/join is stream-ordered); each branch has its own
         scratch (statistics slab / workspace), results bit-identical to the single-stream order."""
         self.spec = spec
         self.fp8_denoiser = fp8_denoiser
+        precise_decoder = precise_decoder or precise
+        assert not (precise and fp8_denoiser), "precise mode keeps every linear at ~fp32 accuracy"
         self.precise = precise_decoder
+        self.precise_all = precise
         self.dec_dt = torch.float32 if precise_decoder else torch.bfloat16
+        self.adt = torch.float32 if precise else torch.bfloat16  # text / sampler / predictor activations
         self.device = torch.device(device)
         self.lib = L.load()
         L.check(self.lib.stzs_init(self.device.index or 0), "stzs_init")
         if packed is not None:
-            assert packed.spec == spec and packed.arena.buf.device == self.device and packed.precise == precise_decoder, \
+            assert packed.spec == spec and packed.arena.buf.device == self.device and \
+                packed.precise == precise_decoder and packed.precise_all == precise, \
                 "packed model: spec / device / precise mode differ"
             self.W = packed
         else:
-            self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder)
+            self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder, precise_all=precise)
         self._bufs = {}
         self._retired = []
         self._consts = {}
@@ -253,7 +262,10 @@ class StyleTTSZS:
                 and cscale == 1.0 and x.t.dtype in (torch.bfloat16, torch.float8_e4m3fn)
                 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
-        if cw.w32 is not None:  # precise mode: fp32 operands on fp32 MFMA (csrc/conv.hip conv_f32)
+        if cw.wx3 is not None:  # precise mode: split bf16 operands (csrc/conv.hip conv_x3)
+            a.w, a.cic = self._t(cw.wx3).data_ptr(), 32
+            flags = (flags & ~8) | L.CONV_W_X3
+        elif cw.w32 is not None:  # fp32 operands on fp32 MFMA (csrc/conv.hip conv_f32)
             a.w, a.cic = self._t(cw.w32).data_ptr(), 32
             flags = (flags & ~8) | L.CONV_W_F32
         elif getattr(cw, "frag32", False):
@@ -389,6 +401,7 @@ class StyleTTSZS:
         a.ldq, a.ldk, a.ldv, a.ldo = q.ld, k.ld, v.ld, o.ld
         a.bsq, a.bsk, a.bsv, a.bso = q.bs, k.bs, v.bs, o.bs
         a.R, a.Lq, a.Lk, a.heads, a.dh = q.B, q.T, k.T, S.dn_heads, S.dn_head_dim
+        a.precise = int(q.t.dtype == torch.float32)  # fp32 operands: the fp32 attention kernel
         self._call(self.lib.stzs_attention, a, "attention")
 
     def lstm(self, lw, x: Act, y: Act, key):
@@ -396,6 +409,9 @@ class StyleTTSZS:
         self.conv(lw.ih, x, gx, what=key + ".ih")
         a = L.LstmArgs()
         a.gx, a.whhT, a.y = gx.ptr, self._t(lw.whhT).data_ptr(), y.ptr
+        if lw.whx3 is not None:  # precise: split-operand recurrence, fp32 h out
+            assert y.t.dtype == torch.float32
+            a.whhT, a.precise = self._t(lw.whx3).data_ptr(), 1
         nx = self.lib.stzs_lstm_workspace(x.B, lw.H, 2)
         xchg = self.buf("lstm.xchg", (max(nx, 16),), torch.uint8, zero=True)
         sync = self.buf("lstm.sync", (4096,), torch.uint8, zero=True)
@@ -426,17 +442,17 @@ class StyleTTSZS:
         (input projection on MFMA + the register-resident exchange recurrence of csrc/lstm.hip)."""
         S, W = self.spec, self.W
         B, T = tokens.shape
-        e = self.act("te.e", B, T, S.d_txt)
-        c = self.act("te.c", B, T, S.d_txt)
+        e = self.act("te.e", B, T, S.d_txt, self.adt)
+        c = self.act("te.c", B, T, S.d_txt, self.adt)
         self.launches += 1
-        L.check(self.lib.stzs_embed(tokens.data_ptr(), W.t(W.te_emb).data_ptr(), e.ptr, B, T, S.d_txt, e.ld,
-                                    self.stream()), "embed")
+        emb = self.lib.stzs_embed_f32 if self.adt == torch.float32 else self.lib.stzs_embed
+        L.check(emb(tokens.data_ptr(), W.t(W.te_emb).data_ptr(), e.ptr, B, T, S.d_txt, e.ld, self.stream()), "embed")
         for i in range(S.te_layers):
             self.conv(W.te_conv[i], e, c, pad=S.te_kernel // 2, what=f"te.conv{i}")
             g, b = W.te_ln[i]
             self.rowln(c, e, G=W.t(g).data_ptr(), gs=0, Bt=W.t(b).data_ptr(), bs=0, gadd=0.0,
                        act=L.ACT_LEAKY, slope=0.2, what=f"te.ln{i}")
-        h = self.act("te.h", B, T, S.d_txt)
+        h = self.act("te.h", B, T, S.d_txt, self.adt)
         return self.lstm(W.te_lstm, e, h, "te.lstm")
 
     def log_mel(self, wav: torch.Tensor, dtype=torch.bfloat16) -> Act:
@@ -563,19 +579,20 @@ class StyleTTSZS:
         Ls, d, cd = S.L_s, S.dn_d, S.code_dim
         Lc = T + Ls
         steps = len(sigmas)
-        ctx = self.act("dn.ctx", R, Lc, d)
+        ctx = self.act("dn.ctx", R, Lc, d, self.adt)
         # ctx_txt rows: the conv writes T rows per utterance into a buffer of Lc rows per utterance
         self._conv_rows(W.dn_ctx_txt, h_txt, ctx.t, 0, 0, "dn.ctx_txt")
         pa = Act(prompt)
         self._conv_rows(W.dn_ctx_prm, pa, ctx.t, 0, T, "dn.ctx_prm")
         if cfg:
             self._conv_rows(W.dn_ctx_txt, h_txt, ctx.t, B, 0, "dn.ctx_txt.u")
-            nul = Act(W.t(W.dn_ctx_null)[None])
+            f32 = self.adt == torch.float32
+            nul = Act(W.t(W.dn_ctx_null32 if f32 else W.dn_ctx_null)[None])
             dst = Act(ctx.t[B:]).rows(0, B)
             a = L.CopyArgs()
-            a.x, a.y = nul.ptr, dst.t.data_ptr() + T * ctx.ld * 2
+            a.x, a.y = nul.ptr, dst.t.data_ptr() + T * ctx.ld * ctx.t.element_size()
             a.ldx, a.bsx, a.ldy, a.bsy = d, 0, ctx.ld, Lc * ctx.ld
-            a.B, a.R, a.C, a.in_dtype, a.out_dtype = B, Ls, d, L.BF16, L.BF16
+            a.B, a.R, a.C, a.in_dtype, a.out_dtype = B, Ls, d, nul.dt, ctx.dt
             self._call(self.lib.stzs_copy2d, a, "ctx_null")
         pm = self.mean_rows(prompt, 0, cd, "dn.pm")
         pool = self.buf("dn.pool", (R, d), torch.float32)
@@ -588,7 +605,7 @@ class StyleTTSZS:
             self._call(self.lib.stzs_copy2d, a, "pool_null")
         kv = []
         for l, lw in enumerate(W.dn_layers):
-            kvl = self.act(f"dn.kv{l}", R, Lc, 2 * d)
+            kvl = self.act(f"dn.kv{l}", R, Lc, 2 * d, self.adt)
             self.conv(lw["kv"], ctx, kvl, what=f"dn.kv{l}")
             kv.append(kvl)
         # sigma embeddings for all steps
@@ -601,14 +618,14 @@ class StyleTTSZS:
         temb = self.act("dn.temb", 1, steps, d, torch.float32)
         self.conv(W.dn_t0, Act(fo), t0, epi_act=L.ACT_SILU, what="dn.t0")
         self.conv(W.dn_t1, t0, temb, what="dn.t1")
-        cb = self.buf("dn.cb", (steps * R, d), torch.bfloat16)
+        cb = self.buf("dn.cb", (steps * R, d), self.adt)
         mod = self.buf("dn.mod", (steps * R, 6 * d), torch.float32)
         fmod = self.buf("dn.fmod", (steps * R, 2 * d), torch.float32)
         modx = self.buf("dn.modx", (S.dn_layers, steps * R, 6 * d), torch.float32)
         fmodx = self.buf("dn.fmodx", (1, steps * R, 2 * d), torch.float32)
         self.launches += 1
-        L.check(self.lib.stzs_dn_cond_steps(pool.data_ptr(), temb.t.data_ptr(), cb.data_ptr(), R, d, steps,
-                                            self.stream()), "dn_cond_steps")
+        cond = self.lib.stzs_dn_cond_steps_f32 if cb.dtype == torch.float32 else self.lib.stzs_dn_cond_steps
+        L.check(cond(pool.data_ptr(), temb.t.data_ptr(), cb.data_ptr(), R, d, steps, self.stream()), "dn_cond_steps")
         self.conv(W.dn_ada, Act(cb[:, None]), Act(mod[:, None]), what="dn.ada")
         self.conv(W.dn_final_ada, Act(cb[:, None]), Act(fmod[:, None]), what="dn.final_ada")
         self.launches += 2
@@ -625,11 +642,11 @@ class StyleTTSZS:
         R, kv, modx, fmodx = st["R"], st["kv"], st["modx"], st["fmodx"]
         Ls, d = S.L_s, S.dn_d
         h = self.act("dn.h", R, Ls, d, torch.float32)
-        an = self.act("dn.a", R, Ls, d)
-        qkv = self.act("dn.qkv", R, Ls, 3 * d)
-        o = self.act("dn.o", R, Ls, d)
-        q = self.act("dn.q", R, Ls, d)
-        ff = self.act("dn.ff", R, Ls, S.dn_ffn)
+        an = self.act("dn.a", R, Ls, d, self.adt)
+        qkv = self.act("dn.qkv", R, Ls, 3 * d, self.adt)
+        o = self.act("dn.o", R, Ls, d, self.adt)
+        q = self.act("dn.q", R, Ls, d, self.adt)
+        ff = self.act("dn.ff", R, Ls, S.dn_ffn, self.adt)
         pos = Act(W.t(W.dn_pos)[None])
         fsz = 4
         f8 = self.fp8_denoiser
@@ -725,14 +742,16 @@ class StyleTTSZS:
         S, W = self.spec, self.W
         B, T = h_txt.B, h_txt.T
         pin = S.pr_in
-        xin = self.act("pr.xin", B, T, pin)
+        xin = self.act("pr.xin", B, T, pin, self.adt)
+        assert h_txt.t.dtype == self.adt
         a = L.PrPrepArgs()
         a.codes, a.h, a.y = codes.data_ptr(), h_txt.ptr, xin.ptr
         a.ldc, a.bsc, a.ldh, a.bsh, a.ldy, a.bsy = codes.shape[2], codes.shape[1] * codes.shape[2], h_txt.ld, \
             h_txt.bs, xin.ld, xin.bs
         a.B, a.L, a.T, a.c0, a.Cs, a.Ch, a.yc0 = B, S.L_s, T, S.style_ac, S.style_pr, S.d_txt, S.d_txt
+        a.f32 = int(self.adt == torch.float32)
         self._call(self.lib.stzs_predictor_prep, a, "pr_prep")
-        hout = self.act("pr.hout", B, T, S.pr_hid)
+        hout = self.act("pr.hout", B, T, S.pr_hid, self.adt)
         gb = self.act("pr.gb", B, T, 2 * S.pr_hid, torch.float32)
         for i in range(S.pr_layers):
             self.lstm(W.pr_de[i], xin, hout, f"pr.de{i}")
@@ -740,7 +759,7 @@ class StyleTTSZS:
             self.rowln(hout, Act(xin.t, 0, S.pr_hid), G=gb.ptr, gs=2 * S.pr_hid, Bt=gb.ptr + S.pr_hid * 4,
                        bs=2 * S.pr_hid, gdiv=1, gadd=1.0, what=f"pr.adaln{i}")
         d = xin
-        hd = self.act("pr.hd", B, T, S.pr_hid)
+        hd = self.act("pr.hd", B, T, S.pr_hid, self.adt)
         self.lstm(W.pr_dur_lstm, d, hd, "pr.dur_lstm")
         logits = self.act("pr.logits", B, T, S.dur_bins, torch.float32)
         self.conv(W.pr_dur_proj, hd, Act(logits.t, 0, S.dur_bins), what="pr.dur_proj")
@@ -771,10 +790,10 @@ class StyleTTSZS:
         a = L.AlignArgs()
         a.dur, a.idx, a.total, a.B, a.T, a.T40 = dur.data_ptr(), idx.data_ptr(), total.data_ptr(), B, T, T40
         self._call(self.lib.stzs_alignment, a, "alignment")
-        en = self.act("pr.en", B, T40, pin)
+        en = self.act("pr.en", B, T40, pin, self.adt)
         self.gather(d, idx, en, pin)
         enc_in = self.act("dec.enc_in", B, T40, S.d_txt + 2, self.dec_dt)
-        if self.precise:  # gather the bf16 rows, then widen into the fp32 decoder input
+        if h_txt.t.dtype != enc_in.t.dtype:  # precise decoder on bf16 text rows: gather, then widen to fp32
             e16 = self.act("dec.enc_in16", B, T40, S.d_txt)
             self.gather(h_txt, idx, e16, S.d_txt)
             self.copy2d(e16, enc_in, T40, S.d_txt)
@@ -789,7 +808,7 @@ class StyleTTSZS:
         middle one x2 upsampling) and a 1x1 projection.  en [B, T40, pr_in] bf16 -> F0, N fp32 [B, 2 T40]."""
         S, W = self.spec, self.W
         B, T40 = en.B, en.T
-        xs = self.act("pr.xs", B, T40, S.pr_hid)
+        xs = self.act("pr.xs", B, T40, S.pr_hid, self.adt)
         self.lstm(W.pr_shared, en, xs, "pr.shared")
         sg = self.mean_rows(codes, S.style_ac, S.style_pr, "pr.sg")
         ng = W.pr_norm
@@ -801,12 +820,12 @@ class StyleTTSZS:
         c0, c1, c2 = S.f0n_ch
 
         def branch(br, out):
-            y0 = self.act(f"pr.{br}.y0", B, T40, c0)
-            y1 = self.act(f"pr.{br}.y1", B, T80, c1)
-            y2 = self.act(f"pr.{br}.y2", B, T80, c2)
-            self.blk(W.pr_blk[f"pr.{br}0"], xs, y0, ng, gbp, f"pr.{br}0")
-            self.blk(W.pr_blk[f"pr.{br}1"], y0, y1, ng, gbp, f"pr.{br}1")
-            self.blk(W.pr_blk[f"pr.{br}2"], y1, y2, ng, gbp, f"pr.{br}2")
+            y0 = self.act(f"pr.{br}.y0", B, T40, c0, self.adt)
+            y1 = self.act(f"pr.{br}.y1", B, T80, c1, self.adt)
+            y2 = self.act(f"pr.{br}.y2", B, T80, c2, self.adt)
+            self.blk(W.pr_blk[f"pr.{br}0"], xs, y0, ng, gbp, f"pr.{br}0", self.adt)
+            self.blk(W.pr_blk[f"pr.{br}1"], y0, y1, ng, gbp, f"pr.{br}1", self.adt)
+            self.blk(W.pr_blk[f"pr.{br}2"], y1, y2, ng, gbp, f"pr.{br}2", self.adt)
             self.conv(W.pr_blk[f"pr.{br}_proj"], y2, Act(out, 0, 1), what=f"pr.{br}_proj")
         self.fork(lambda: branch("f0", F0), lambda: branch("n", Nn))
         return F0[:, :, 0], Nn[:, :, 0]

@@ -85,7 +85,7 @@ def sample_style(handle: int, h_txt: torch.Tensor, prompt: torch.Tensor, noise: 
     from .engine import Act
     eng = _eng(handle, h_txt, prompt, noise)
     B, T, D = h_txt.shape
-    ht = eng.buf("op.h_txt", (B, T, (D + 7) // 8 * 8), torch.bfloat16, zero=True)
+    ht = eng.buf("op.h_txt", (B, T, (D + 7) // 8 * 8), eng.adt, zero=True)
     ht[:, :, :D].copy_(h_txt)
     return eng.sample_style(Act(ht, 0, D), prompt.float().contiguous(), noise.float().contiguous(), steps,
                             cfg_scale).clone()
@@ -103,7 +103,7 @@ def predict_prosody(handle: int, h_txt: torch.Tensor, codes: torch.Tensor,
     from .engine import Act
     eng = _eng(handle, h_txt, codes)
     B, T, D = h_txt.shape
-    ht = eng.buf("op.h_txt", (B, T, (D + 7) // 8 * 8), torch.bfloat16, zero=True)
+    ht = eng.buf("op.h_txt", (B, T, (D + 7) // 8 * 8), eng.adt, zero=True)
     ht[:, :, :D].copy_(h_txt)
     pro = eng.predict_prosody(Act(ht, 0, D), codes.float().contiguous(),
                               durations.cpu() if durations is not None else None)
@@ -252,9 +252,11 @@ def _(post, tail, f0, final, n_fft, hop):
 # Activations cross this boundary channels-last, [B, T, C] (the kernels' layout; a torch Conv1d NCT tensor is
 # x.transpose(1, 2)); outputs are fp32 copies.
 
-def _act_in(eng, key, x: torch.Tensor, dtype=torch.bfloat16):
-    """x [B, T, C] -> an engine Act (row pitch padded to 8) holding x in `dtype`."""
+def _act_in(eng, key, x: torch.Tensor, dtype=None):
+    """x [B, T, C] -> an engine Act (row pitch padded to 8) holding x in `dtype` (default: the engine's
+    activation dtype, fp32 in precise mode)."""
     from .engine import Act
+    dtype = eng.adt if dtype is None else dtype
     B, T, Cn = x.shape
     t = eng.buf("op." + key, (B, T, (Cn + 7) // 8 * 8), dtype, zero=True)
     t[:, :, :Cn].copy_(x)
@@ -277,7 +279,7 @@ def bilstm(handle: int, name: str, x: torch.Tensor) -> torch.Tensor:
     else:
         raise RuntimeError(f"stzs::bilstm: unknown LSTM {name!r}")
     xa = _act_in(eng, "lstm.x", x)
-    y = eng.act("op.lstm.y", x.shape[0], x.shape[1], 2 * lw.H)
+    y = eng.act("op.lstm.y", x.shape[0], x.shape[1], 2 * lw.H, eng.adt)
     eng.lstm(lw, xa, y, "op." + name)
     return y.t[:, :, :2 * lw.H].float()
 

@@ -46,8 +46,9 @@ class ConvW:
     narrow32: bool = False  # [NK][32][32] narrow packing (STZS_CONV_W_NARROW32)
     wscale: Optional[object] = None  # fp8 linears: per-output-column fp32 scale [co_pad]
     f8: bool = False
-    w32: Optional[object] = None  # precise mode: fp32 K-step stream (STZS_CONV_W_F32), unpermuted
+    w32: Optional[object] = None  # fp32 K-step stream (STZS_CONV_W_F32, conv_f32), unpermuted
     frag32: bool = False  # fragment-order packing of the register-direct MRF kernel (STZS_CONV_W_FRAG32)
+    wx3: Optional[object] = None  # precise mode: hi | lo bf16 K-step streams (STZS_CONV_W_X3, conv_x3), unpermuted
 
 
 class Arena:
@@ -117,6 +118,21 @@ def kstep_stream_f32(wp: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
+def split_bf16(w: torch.Tensor):
+    """fp32 -> (hi, lo) bf16 with hi = bf16(w), lo = bf16(w - hi): w = hi + lo to ~2^-17 relative (the
+    split-operand precise mode, csrc/conv.hip conv_x3 / csrc/lstm.hip)."""
+    w = w.float()
+    hi = w.to(torch.bfloat16)
+    return hi, (w - hi.float()).to(torch.bfloat16)
+
+
+def kstep_stream_x3(wp: torch.Tensor) -> torch.Tensor:
+    """[ks, co_pad, ci_pad] fp32 -> [2, co_pad/128, ci_pad/32 * ks, 128, 32] bf16: the hi stream, then the lo
+    stream, each the 32-channel-chunk K-step layout of kstep_stream (include/stzs.h STZS_CONV_W_X3)."""
+    hi, lo = split_bf16(wp)
+    return torch.stack([kstep_stream(hi.float(), 32), kstep_stream(lo.float(), 32)]).to(torch.bfloat16)
+
+
 def lane16_perm() -> torch.Tensor:
     """packed row rr = wc*64 + nt*16 + g*4 + r of a 128-column tile holds output channel
     wc*64 + g*16 + nt*4 + r: the MRF kernel's swapped-operand accumulators then give each lane 16
@@ -159,10 +175,12 @@ def narrow32_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
     return t.reshape(nchunk * ks * kpc, 32, 32).contiguous()
 
 
-def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f32=False, frag32=False) -> ConvW:
+def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f32=False, frag32=False,
+              x3=False) -> ConvW:
     """w: Conv1d [Co, Ci, k] / Linear [Co, Ci] / ConvTranspose1d [Ci, Co, 2*ups] (ups > 0).
     lane16: the MRF kernel's layout (Ci % 128 == 0, Co % 16 == 0, plain conv).
-    f32: also pack the precise-mode fp32 stream (ConvW.w32)."""
+    f32: also pack the fp32 stream (ConvW.w32, conv_f32); x3: also pack the precise-mode split hi | lo
+    streams (ConvW.wx3, conv_x3)."""
     if ups:
         Ci, Co, k = w.shape
         assert k == 2 * ups
@@ -184,24 +202,25 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
     wp = torch.zeros(ks, co_pad, ci_pad)
     wp[:, :ncol, :Ci] = wk
     w32 = A.add(name + ".w32", kstep_stream_f32(wp)) if f32 else None
+    wx3 = A.add(name + ".wx3", kstep_stream_x3(wp)) if x3 else None
     if narrow32:
         assert not ups and cic == 128 and Co <= 32, (name, Ci, Co)
         wn = A.add(name + ".wpk", narrow32_stream(wp[:, :32], cic).to(torch.bfloat16))
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True, w32=w32)
+        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True, w32=w32, wx3=wx3)
     if frag32:
         assert not ups and cic == 128 and Co % 8 == 0 and ks in (3, 7, 11), (name, Ci, Co, ks)
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, frag32_perm()].reshape(ks, co_pad, ci_pad)
         wn = A.add(name + ".wfr", frag32_stream(wp).to(torch.bfloat16))
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, 0, False, w32=w32, frag32=True)
+        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, 0, False, w32=w32, frag32=True, wx3=wx3)
     if lane16:
         assert cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, perm].reshape(ks, co_pad, ci_pad)
     wn = A.add(name + ".wpk", kstep_stream(wp, cic).to(torch.bfloat16))
     bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16, w32=w32)
+    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16, w32=w32, wx3=wx3)
 
 
 def quantize_f8_cols(w: torch.Tensor):
@@ -261,7 +280,7 @@ class NormGroup:
     total: int
 
 
-def pack_norm_group(A: Arena, name, P, norm_names, style_dim, f32=False) -> NormGroup:
+def pack_norm_group(A: Arena, name, P, norm_names, style_dim, x3=False) -> NormGroup:
     ws, bs, offs, off = [], [], {}, 0
     for n in norm_names:
         w, b = P[n + ".w"], P[n + ".b"]
@@ -271,7 +290,7 @@ def pack_norm_group(A: Arena, name, P, norm_names, style_dim, f32=False) -> Norm
         bs.append(b)
     W = torch.cat(ws, 0)
     Bv = torch.cat(bs, 0)
-    return NormGroup(pack_conv(A, name, W, Bv, f32=f32), offs, off)
+    return NormGroup(pack_conv(A, name, W, Bv, x3=x3), offs, off)
 
 
 @dataclass
@@ -279,15 +298,21 @@ class LstmW:
     ih: ConvW
     whhT: str
     H: int
+    whx3: Optional[str] = None  # precise mode: hi fragments of both directions, then lo (stzs_lstm_args.precise)
 
 
-def pack_lstm(A: Arena, name, P) -> LstmW:
+def pack_lstm(A: Arena, name, P, x3=False) -> LstmW:
     H = P[name + ".w_hh"].shape[1]
     wih = torch.cat([P[name + ".w_ih"], P[name + ".w_ih_rev"]], 0)
     bias = torch.cat([P[name + ".b_ih"] + P[name + ".b_hh"], P[name + ".b_ih_rev"] + P[name + ".b_hh_rev"]], 0)
-    ih = pack_conv(A, name + ".ih", wih, bias)
+    ih = pack_conv(A, name + ".ih", wih, bias, x3=x3)
     frags = torch.stack([lstm_frags(P[name + ".w_hh"]), lstm_frags(P[name + ".w_hh_rev"])], 0)
-    return LstmW(ih, A.add(name + ".whhT", frags.to(torch.bfloat16)), H)
+    whx3 = None
+    if x3:
+        parts = [split_bf16(P[name + ".w_hh"]), split_bf16(P[name + ".w_hh_rev"])]
+        hl = [torch.stack([lstm_frags(parts[d][h].float()) for d in range(2)], 0) for h in range(2)]
+        whx3 = A.add(name + ".whhx3", torch.stack(hl, 0).to(torch.bfloat16))
+    return LstmW(ih, A.add(name + ".whhT", frags.to(torch.bfloat16)), H, whx3)
 
 
 def lstm_frags(w_hh: torch.Tensor) -> torch.Tensor:
@@ -322,11 +347,11 @@ def _lane16_ok(w) -> bool:
     return Ci > 64 and Co % 16 == 0
 
 
-def pack_blk(A: Arena, P, name, up=False, f32=False) -> BlkW:
+def pack_blk(A: Arena, P, name, up=False, x3=False) -> BlkW:
     w1, w2 = P[name + ".conv1.w"], P[name + ".conv2.w"]
-    c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1), f32=f32)
-    c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2), f32=f32)
-    sc = pack_conv(A, name + ".sc", P[name + ".sc.w"], f32=f32) if name + ".sc.w" in P else None
+    c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1), x3=x3)
+    c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2), x3=x3)
+    sc = pack_conv(A, name + ".sc", P[name + ".sc.w"], x3=x3) if name + ".sc.w" in P else None
     pw = pb = None
     if up:
         pw = A.add(name + ".poolw", P[name + ".pool.w"].reshape(-1, 3).float())
@@ -339,17 +364,21 @@ def pack_blk(A: Arena, P, name, up=False, f32=False) -> BlkW:
 class PackedModel:
     """All hot-path weights of spec v0 in kernel layouts, resident in one device arena."""
 
-    def __init__(self, spec: Spec, P, device, fill=True, precise=False):
-        """precise: also pack fp32 streams of every decoder conv (StyleTTSZS(precise_decoder=True))."""
+    def __init__(self, spec: Spec, P, device, fill=True, precise=False, precise_all=False):
+        """precise: also pack the split-operand (hi | lo) streams of every decoder conv (StyleTTSZS(
+        precise_decoder=True)); precise_all: of every conv, linear and LSTM of the pipeline except the
+        reference-prompt front end, whose output is quantised to discrete codes (StyleTTSZS(precise=True))."""
         S = self.spec = spec
-        f32 = precise
+        xd = precise or precise_all
+        xa = precise_all
         A = self.arena = Arena()
         d = S.dn_d
         # --- text encoder ---
         self.te_emb = A.add("te.emb", P["te.emb"].float())
-        self.te_conv = [pack_conv(A, f"te.conv{i}", P[f"te.conv{i}.w"], P[f"te.conv{i}.b"]) for i in range(S.te_layers)]
+        self.te_conv = [pack_conv(A, f"te.conv{i}", P[f"te.conv{i}.w"], P[f"te.conv{i}.b"], x3=xa)
+                        for i in range(S.te_layers)]
         self.te_ln = [(A.add(f"te.ln{i}.g", P[f"te.ln{i}.g"]), A.add(f"te.ln{i}.b", P[f"te.ln{i}.b"])) for i in range(S.te_layers)]
-        self.te_lstm = pack_lstm(A, "te.lstm", P)
+        self.te_lstm = pack_lstm(A, "te.lstm", P, x3=xa)
         # --- reference-prompt front end (csrc/frontend.hip): DFT basis, window, mel filterbank, encoder ---
         self.fe_dft = pack_conv(A, "fe.dft", dft_basis(S.mel_nfft, S.mel_win))
         self.fe_win = A.add("fe.win", torch.hann_window(S.mel_win).float())
@@ -367,7 +396,7 @@ class PackedModel:
         self.pe_proj = pack_conv(A, "pe.proj", P["pe.proj.w"], P["pe.proj.b"])
         self.pe_vq = A.add("pe.vq", P["pe.vq"].float())  # [G][K][dg] codebooks (stzs_code_quantize)
         # --- denoiser ---
-        L = lambda n: pack_conv(A, n, P[n + ".w"], P[n + ".b"])
+        L = lambda n: pack_conv(A, n, P[n + ".w"], P[n + ".b"], x3=xa)
         self.dn_in = L("dn.in_proj")
         self.dn_pos = A.add("dn.pos", P["dn.pos"].float())
         self.dn_t0, self.dn_t1 = L("dn.t_mlp0"), L("dn.t_mlp1")
@@ -383,6 +412,7 @@ class PackedModel:
         pool_null = null.mean(0) @ P["dn.pool_proj.w"].t() + P["dn.pool_proj.b"]
         self.dn_ctx_null = A.add("dn.ctx_null", ctx_null.to(torch.bfloat16))
         self.dn_pool_null = A.add("dn.pool_null", pool_null.float())
+        self.dn_ctx_null32 = A.add("dn.ctx_null32", ctx_null.float()) if xa else None
         self.dn_layers = []
         for l in range(S.dn_layers):
             p = f"dn.l{l}"
@@ -395,38 +425,39 @@ class PackedModel:
                            ("ff2", ".ff2")):
                 self.dn_layers[-1][key + "8"] = pack_conv_f8(A, p + n + ".f8", P[p + n + ".w"], P[p + n + ".b"])
         # --- predictor ---
-        self.pr_de = [pack_lstm(A, f"pr.de{i}", P) for i in range(S.pr_layers)]
+        self.pr_de = [pack_lstm(A, f"pr.de{i}", P, x3=xa) for i in range(S.pr_layers)]
         self.pr_aln = [L(f"pr.de{i}.aln") for i in range(S.pr_layers)]
-        self.pr_dur_lstm = pack_lstm(A, "pr.dur_lstm", P)
+        self.pr_dur_lstm = pack_lstm(A, "pr.dur_lstm", P, x3=xa)
         self.pr_dur_proj = L("pr.dur_proj")
-        self.pr_shared = pack_lstm(A, "pr.shared", P)
+        self.pr_shared = pack_lstm(A, "pr.shared", P, x3=xa)
         pr_norms = []
         self.pr_blk = {}
         for br in ("f0", "n"):
             for i in range(3):
                 nm = f"pr.{br}{i}"
-                self.pr_blk[nm] = pack_blk(A, P, nm, up=(i == 1))
+                self.pr_blk[nm] = pack_blk(A, P, nm, up=(i == 1), x3=xa)
                 pr_norms += blk_norms(nm)
-            self.pr_blk[f"pr.{br}_proj"] = pack_conv(A, f"pr.{br}_proj", P[f"pr.{br}_proj.w"], P[f"pr.{br}_proj.b"])
-        self.pr_norm = pack_norm_group(A, "pr.norms", P, pr_norms, S.style_pr)
+            self.pr_blk[f"pr.{br}_proj"] = pack_conv(A, f"pr.{br}_proj", P[f"pr.{br}_proj.w"], P[f"pr.{br}_proj.b"],
+                                                     x3=xa)
+        self.pr_norm = pack_norm_group(A, "pr.norms", P, pr_norms, S.style_pr, x3=xa)
         # --- decoder ---
         self.dec_f0 = A.add("dec.f0c", torch.cat([P["dec.f0_conv.w"].reshape(-1), P["dec.f0_conv.b"]]).float())
         self.dec_n = A.add("dec.nc", torch.cat([P["dec.n_conv.w"].reshape(-1), P["dec.n_conv.b"]]).float())
-        self.dec_asr_res = pack_conv(A, "dec.asr_res", P["dec.asr_res.w"], P["dec.asr_res.b"], f32=f32)
+        self.dec_asr_res = pack_conv(A, "dec.asr_res", P["dec.asr_res.w"], P["dec.asr_res.b"], x3=xd)
         dec_norms = []
         self.dec_blk = {}
         for nm, up in [("dec.encode", False), ("dec.decode0", False), ("dec.decode1", False),
                        ("dec.decode2", False), ("dec.decode3", True)]:
-            self.dec_blk[nm] = pack_blk(A, P, nm, up=up, f32=f32)
+            self.dec_blk[nm] = pack_blk(A, P, nm, up=up, x3=xd)
             dec_norms += blk_norms(nm)
         self.src_merge = A.add("gen.src_merge", torch.cat([P["gen.src_merge.w"].reshape(-1), P["gen.src_merge.b"]]).float())
         self.noise_conv, self.ups, self.rb = [], [], []
         for i, (r, k) in enumerate(zip(S.up_rates, S.up_kernels)):
             self.noise_conv.append(pack_conv(A, f"gen.noise_conv{i}", P[f"gen.noise_conv{i}.w"], P[f"gen.noise_conv{i}.b"],
-                                             f32=f32))
+                                             x3=xd))
             wu = P[f"gen.ups{i}.w"]  # ConvTranspose1d [Ci, Co, 2r]
             self.ups.append(pack_conv(A, f"gen.ups{i}", wu, P[f"gen.ups{i}.b"], ups=r,
-                                      lane16=wu.shape[0] > 64 and wu.shape[1] % 16 == 0, f32=f32))
+                                      lane16=wu.shape[0] > 64 and wu.shape[1] % 16 == 0, x3=xd))
             stage = []
             for j, kr in enumerate(S.rb_kernels):
                 res = []
@@ -438,9 +469,9 @@ class PackedModel:
                     fr = S.gen_ch[i] == 128 and kr in (3, 7, 11) and (kr - 1) * dil <= 64
                     res.append(dict(
                         c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16 and not fr, frag32=fr,
-                                     f32=f32),
+                                     x3=xd),
                         c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"], lane16=l16 and not fr, frag32=fr,
-                                     f32=f32),
+                                     x3=xd),
                         a1=A.add(p + ".a1", P[p + ".alpha1"].float()), a2=A.add(p + ".a2", P[p + ".alpha2"].float()),
                         n1=p + ".n1", n2=p + ".n2", k=kr, dil=dil))
                     dec_norms += [p + ".n1", p + ".n2"]
@@ -448,11 +479,12 @@ class PackedModel:
             self.rb.append(stage)
         wpost = P["gen.conv_post.w"]
         self.conv_post = pack_conv(A, "gen.conv_post", wpost, P["gen.conv_post.b"],
-                                   narrow32=wpost.shape[1] > 64 and wpost.shape[0] <= 32, f32=f32)
-        self.dec_norm = pack_norm_group(A, "dec.norms", P, dec_norms, S.style_ac, f32=f32)
+                                   narrow32=wpost.shape[1] > 64 and wpost.shape[0] <= 32, x3=xd)
+        self.dec_norm = pack_norm_group(A, "dec.norms", P, dec_norms, S.style_ac, x3=xd)
         A.finalize(device, fill=fill)
         self.device = device
         self.precise = precise
+        self.precise_all = precise_all
 
     def t(self, name):
         return self.arena[name]

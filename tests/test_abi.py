@@ -41,7 +41,8 @@ def test_workspace_queries():
     from stzs import _lib
     L = _lib.load()
     assert L.stzs_chan_stats_workspace(64, 24001, 128) == 64 * 94 * 128 * 8
-    assert L.stzs_lstm_workspace(64, 256, 2) == 2 * 2 * 64 * 256 * 2
+    # groups x dirs x 2 buffers x 64 rows x (hi | lo) H bf16: sized for the precise split-operand rows
+    assert L.stzs_lstm_workspace(64, 256, 2) == 2 * 2 * 64 * 2 * 256 * 2
 
 
 STRUCTS = {

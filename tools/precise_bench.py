@@ -1,5 +1,5 @@
-"""Throughput of the precise (fp32-MFMA) decoder mode vs the bf16 path on the bench workload shape.
-    python tools/precise_bench.py [B]     -> one JSON line"""
+"""Throughput of the precise modes (split-operand decoder; whole pipeline) vs the bf16 path on the bench
+workload shape.      python tools/precise_bench.py [B] [modes]     -> one JSON line"""
 import json
 import os
 import sys
@@ -17,8 +17,9 @@ from stzs.spec import SPEC_V0 as S  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 P = init_params(S, seed=0)
 res = {}
-for mode in ("bf16", "precise"):
-    eng = StyleTTSZS(S, P, device="cuda:0", precise_decoder=(mode == "precise"))
+modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["bf16", "precise_decoder", "precise"]
+for mode in modes:
+    eng = StyleTTSZS(S, P, device="cuda:0", precise_decoder=(mode == "precise_decoder"), precise=(mode == "precise"))
     tok, ref, eps, dur = (t.cuda() for t in make_inputs(S, B, 0))
     nf = int(dur[0].sum())
     step = lambda: eng.synth(tok, ref, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps, durations=dur,
