@@ -178,7 +178,7 @@ int stzs_quant_rows(const stzs_quant_args* a, void* stream);
 
 /* ---- multi-head attention, softmax(q k^T / sqrt(dh)) v, rows independent ----------------
  * q [R, Lq, ldq], k/v [R, Lk, ldk/ldv], o [R, Lq, ldo]; bf16 (precise = 0, MFMA flash kernel) or fp32
- * (precise = 1: fp32 dot products, libm expf -- the split-operand precise mode); heads x dh = D.
+ * (precise = 1: split-operand bf16x3 products on the same MFMAs, libm expf -- the precise mode); heads x dh = D.
  * (denoiser self-attention over L_s codes, cross-attention to context) */
 typedef struct stzs_attn_args {
     const void* q;

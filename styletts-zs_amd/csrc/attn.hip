@@ -138,70 +138,164 @@ __global__ __launch_bounds__(256) void attn_mfma(const stzs_attn_args a) {
     }
 }
 
-// PRECISE mode (stzs_attn_args.precise = 1): fp32 q / k / v / o, fp32 dot products and libm expf on the VALU,
-// online softmax per 64-key chunk.  One thread per query, one workgroup per (row, head, 256 queries): the
-// denoiser's 50 x (<= a few hundred) x 64 per head is small, this path exists for fp32-level parity.
-constexpr int KC32 = 64;
+// PRECISE mode (stzs_attn_args.precise = 1): fp32 q / k / v / o.  The same flash structure on the same MFMAs
+// with split operands (hi = bf16(x), lo = bf16(x - hi)): S = Qh Kh + Qh Kl + Ql Kh and O += Ph Vh + Ph Vl + Pl Vh
+// (fp32 accumulate, ~fp32 accuracy), the softmax exponentials with libm expf.
 template <int DH>
-__global__ __launch_bounds__(256) void attn_f32(const stzs_attn_args a) {
-    __shared__ float Ks[KC32][DH + 1];
-    __shared__ float Vs[KC32][DH + 1];
-    const int tid = threadIdx.x;
+__global__ __launch_bounds__(256) void attn_x3(const stzs_attn_args a) {
+    constexpr int NKS = DH / 32;
+    constexpr int NDT = DH / 16;
+    constexpr int KP = DH + 8;
+    constexpr int VP = KC + 8;
+    constexpr int PP = KC + 8;
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KC * KP];
+    __shared__ __attribute__((aligned(16))) bf16_t Vt[2][DH * VP];
+    __shared__ __attribute__((aligned(16))) bf16_t Ps[2][4][16 * PP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long r = blockIdx.x;
     const int h = blockIdx.y;
-    const int qi = blockIdx.z * 256 + tid;
-    const bool qok = qi < a.Lq;
+    const int qb = blockIdx.z * 64 + wave * 16;
     const float* Q = reinterpret_cast<const float*>(a.q) + r * a.bsq + h * DH;
     const float* K = reinterpret_cast<const float*>(a.k) + r * a.bsk + h * DH;
     const float* V = reinterpret_cast<const float*>(a.v) + r * a.bsv + h * DH;
     const float scale = 1.f / sqrtf((float)DH);
-    float q[DH], o[DH];
+    auto split8 = [](const float* f, bf16x8& hi, bf16x8& lo) {
+        uint4 hp = pack8(f);
+        float hf[8], lf[8];
+        unpack8(hp, hf);
 #pragma unroll
-    for (int d = 0; d < DH; ++d) {
-        q[d] = qok ? Q[(long)qi * a.ldq + d] : 0.f;
-        o[d] = 0.f;
+        for (int j = 0; j < 8; ++j) lf[j] = f[j] - hf[j];
+        uint4 lp = pack8(lf);
+        hi = __builtin_bit_cast(bf16x8, hp);
+        lo = __builtin_bit_cast(bf16x8, lp);
+    };
+    bf16x8 qh[NKS], ql[NKS];
+    {
+        const int qr = min(qb + (lane & 15), a.Lq - 1);
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            float f[8];
+            load8(Q + (long)qr * a.ldq + ks * 32 + 8 * (lane >> 4), f);
+            split8(f, qh[ks], ql[ks]);
+        }
     }
-    float m = -INFINITY, l = 0.f;
-    for (int c0 = 0; c0 < a.Lk; c0 += KC32) {
-        const int nk = min(KC32, a.Lk - c0);
-        __syncthreads();
-        for (int i = tid; i < KC32 * DH; i += 256) {  // rows past nk zeroed (read, masked)
-            const int kr = i / DH, d = i - kr * DH;
-            const bool ok = kr < nk;
-            Ks[kr][d] = ok ? K[(long)(c0 + kr) * a.ldk + d] : 0.f;
-            Vs[kr][d] = ok ? V[(long)(c0 + kr) * a.ldv + d] : 0.f;
-        }
-        __syncthreads();
-        if (!qok) continue;
-        // (static key indices keep sv in registers; keys past nk are masked, not branched around)
-        float sv[KC32];
-        float mx = m;
+    f32x4 o[NDT];
 #pragma unroll
-        for (int j = 0; j < KC32; ++j) {
-            float acc = 0.f;
+    for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[4], l[4];
 #pragma unroll
-            for (int d = 0; d < DH; ++d) acc = fmaf(q[d], Ks[j][d], acc);
-            sv[j] = j < nk ? acc * scale : -INFINITY;
-            mx = fmaxf(mx, sv[j]);
-        }
-        const float corr = expf(m - mx);
-        l *= corr;
-#pragma unroll
-        for (int d = 0; d < DH; ++d) o[d] *= corr;
-#pragma unroll
-        for (int j = 0; j < KC32; ++j) {
-            const float pj = j < nk ? expf(sv[j] - mx) : 0.f;
-            l += pj;
-#pragma unroll
-            for (int d = 0; d < DH; ++d) o[d] = fmaf(pj, Vs[j][d], o[d]);
-        }
-        m = mx;
+    for (int i = 0; i < 4; ++i) {
+        m[i] = -INFINITY;
+        l[i] = 0.f;
     }
-    if (qok) {
-        float* O = reinterpret_cast<float*>(a.o) + r * a.bso + h * DH + (long)qi * a.ldo;
-        const float inv = 1.f / l;
+    for (int c0 = 0; c0 < a.Lk; c0 += KC) {
+        __syncthreads();
+        for (int i = tid; i < KC * (DH / 8); i += 256) {
+            const int kr = i / (DH / 8), cv = i - kr * (DH / 8);
+            const bool ok = c0 + kr < a.Lk;
+            const int kk = ok ? c0 + kr : 0;
+            float kf[8], vf[8];
+            load8(K + (long)kk * a.ldk + cv * 8, kf);
+            load8(V + (long)kk * a.ldv + cv * 8, vf);
+            if (!ok) {
 #pragma unroll
-        for (int d = 0; d < DH; ++d) O[d] = o[d] * inv;
+                for (int j = 0; j < 8; ++j) kf[j] = vf[j] = 0.f;
+            }
+            bf16x8 kh, kl, vh, vl;
+            split8(kf, kh, kl);
+            split8(vf, vh, vl);
+            *reinterpret_cast<bf16x8*>(&Ks[0][kr * KP + cv * 8]) = kh;
+            *reinterpret_cast<bf16x8*>(&Ks[1][kr * KP + cv * 8]) = kl;
+            const uint4 uh = __builtin_bit_cast(uint4, vh), ul = __builtin_bit_cast(uint4, vl);
+            const uint32_t wh[4] = {uh.x, uh.y, uh.z, uh.w}, wl[4] = {ul.x, ul.y, ul.z, ul.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                Vt[0][(cv * 8 + 2 * j) * VP + kr] = (bf16_t)(wh[j] & 0xFFFF);
+                Vt[0][(cv * 8 + 2 * j + 1) * VP + kr] = (bf16_t)(wh[j] >> 16);
+                Vt[1][(cv * 8 + 2 * j) * VP + kr] = (bf16_t)(wl[j] & 0xFFFF);
+                Vt[1][(cv * 8 + 2 * j + 1) * VP + kr] = (bf16_t)(wl[j] >> 16);
+            }
+        }
+        __syncthreads();
+        f32x4 s[4];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const int ko = (nt * 16 + (lane & 15)) * KP + ks * 32 + 8 * (lane >> 4);
+                const bf16x8 kh = *reinterpret_cast<const bf16x8*>(&Ks[0][ko]);
+                const bf16x8 kl = *reinterpret_cast<const bf16x8*>(&Ks[1][ko]);
+                s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ql[ks], kh, s[nt], 0, 0, 0);
+                s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[ks], kl, s[nt], 0, 0, 0);
+                s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[ks], kh, s[nt], 0, 0, 0);
+            }
+        }
+        float alpha[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const bool ok = c0 + nt * 16 + (lane & 15) < a.Lk;
+                s[nt][i] = ok ? s[nt][i] * scale : -INFINITY;
+                mx = fmaxf(mx, s[nt][i]);
+            }
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+            const float mn = fmaxf(m[i], mx);
+            alpha[i] = expf(m[i] - mn);
+            float sum = 0.f;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const float pv = expf(s[nt][i] - mn);
+                s[nt][i] = pv;
+                sum += pv;
+            }
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
+            l[i] = l[i] * alpha[i] + sum;
+            m[i] = mn;
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[dt][i] *= alpha[i];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int pi = ((lane >> 4) * 4 + i) * PP + nt * 16 + (lane & 15);
+                const bf16_t ph = f2bf(s[nt][i]);
+                Ps[0][wave][pi] = ph;
+                Ps[1][wave][pi] = f2bf(s[nt][i] - bf2f(ph));
+            }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < KC / 32; ++ks) {
+            const int po = (lane & 15) * PP + ks * 32 + 8 * (lane >> 4);
+            const bf16x8 ph = *reinterpret_cast<const bf16x8*>(&Ps[0][wave][po]);
+            const bf16x8 pl = *reinterpret_cast<const bf16x8*>(&Ps[1][wave][po]);
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const int vo = (dt * 16 + (lane & 15)) * VP + ks * 32 + 8 * (lane >> 4);
+                const bf16x8 vh = *reinterpret_cast<const bf16x8*>(&Vt[0][vo]);
+                const bf16x8 vl = *reinterpret_cast<const bf16x8*>(&Vt[1][vo]);
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vh, o[dt], 0, 0, 0);
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vl, o[dt], 0, 0, 0);
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vh, o[dt], 0, 0, 0);
+            }
+        }
+    }
+    float* O = reinterpret_cast<float*>(a.o) + r * a.bso + h * DH;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int q = qb + (lane >> 4) * 4 + i;
+        if (q < a.Lq) {
+            const float inv = 1.f / l[i];
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) O[(long)q * a.ldo + dt * 16 + (lane & 15)] = o[dt][i] * inv;
+        }
     }
 }
 
@@ -213,11 +307,11 @@ extern "C" int stzs_attention(const stzs_attn_args* a, void* stream) {
     if (a->ldq % 8 || a->ldk % 8 || a->ldv % 8 || a->bsq % 8 || a->bsk % 8 || a->bsv % 8) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (a->precise == 1) {
-        dim3 g((unsigned)a->R, a->heads, (a->Lq + 255) / 256);
+        dim3 g((unsigned)a->R, a->heads, (a->Lq + 63) / 64);
         if (a->dh == 64)
-            hipLaunchKernelGGL(attn_f32<64>, g, dim3(256), 0, s, *a);
+            hipLaunchKernelGGL(attn_x3<64>, g, dim3(256), 0, s, *a);
         else if (a->dh == 32)
-            hipLaunchKernelGGL(attn_f32<32>, g, dim3(256), 0, s, *a);
+            hipLaunchKernelGGL(attn_x3<32>, g, dim3(256), 0, s, *a);
         else
             return STZS_ESHAPE;
         STZS_LAUNCH_CHECK();

@@ -773,10 +773,10 @@ __host__ __device__ inline int x3_pitch(int rows_in) {
     return 2 * ((rows_in * PX + 15) & ~15) + NSLOT * XSLOT_C + 3 * 32 * 4 <= 160 * 1024 ? PX : PX_TIGHT;
 }
 constexpr int XSLOT = XSLOT_C;
-template <typename TIn, typename TOut, int PACT>
+template <typename TIn, typename TOut, int PACT, bool FLAT>
 __global__ __launch_bounds__(NTHR, 2) void conv_x3(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int ks = a.ks;
+    const int ks = FLAT ? 1 : a.ks;
     const int rows_in = (BT - 1) * a.stride + (ks - 1) * a.dil + 1;
     const int px = x3_pitch(rows_in);
     unsigned char* thi = smem;
@@ -787,14 +787,22 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3(const stzs_conv_args a) {
     float* c_al = c_sh + 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
-    const int tpb = (a.T_out + BT - 1) / BT;
-    const int bq = blockIdx.x / tpb;
-    const int t0 = (blockIdx.x - bq * tpb) * BT;
+    // FLAT (linears: ks 1, no prologue): 128 consecutive rows of the [B * T] row space per tile
+    int bq = 0, t0 = 0;
+    long row0 = 0;
+    if (FLAT) {
+        row0 = (long)blockIdx.x * BT;
+    } else {
+        const int tpb = (a.T_out + BT - 1) / BT;
+        bq = blockIdx.x / tpb;
+        t0 = (blockIdx.x - bq * tpb) * BT;
+    }
     const int nchunk = a.ci_pad / 32;
     const int NK = nchunk * ks;
     const long stream_el = (long)(a.co_pad / BCO) * NK * (BCO * 32);  // bf16 elements of one (hi | lo) stream
     const bf16_t* Wh = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
-    const TIn* X = reinterpret_cast<const TIn*>(a.x) + (long)bq * a.bsx;
+    const TIn* X = reinterpret_cast<const TIn*>(a.x) + (FLAT ? 0 : (long)bq * a.bsx);
+    const long nR = (long)a.B * a.T_in;
     auto fill = [&](int k) {
         const bf16_t* src = Wh + (long)k * (BCO * 32) + wave * 1024 + lane * 8;
         unsigned char* dst = ring + (k % NSLOT) * XSLOT + wave * 2048;
@@ -848,13 +856,24 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3(const stzs_conv_args a) {
         for (int v = tid; v < rows_in * 4; v += NTHR) {
             const int r = v >> 2, cv = v & 3;
             const int ci = cc * 32 + cv * 8;
-            const int tin = t0 * a.stride - a.pad + r;
+            long off;
+            bool rok;
+            if (FLAT) {
+                const long R = row0 + r;
+                const long bb = R / a.T_in;
+                rok = R < nR;
+                off = bb * a.bsx + (R - bb * a.T_in) * a.ldx;
+            } else {
+                const int tin = t0 * a.stride - a.pad + r;
+                rok = tin >= 0 && tin < a.T_in;
+                off = (long)tin * a.ldx;
+            }
             float o[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) o[j] = 0.f;
-            if (tin >= 0 && tin < a.T_in && ci < a.Ci) {
+            if (rok && ci < a.Ci) {
                 float f[8];
-                load8(X + (long)tin * a.ldx + ci, f);
+                load8(X + off + ci, f);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float y = f[j] * c_sc[cv * 8 + j] + c_sh[cv * 8 + j];
@@ -908,7 +927,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3(const stzs_conv_args a) {
                 }
         }
     }
-    finish<TOut, false, BT>(a, acc, smem, bq, t0, 0);
+    finish<TOut, FLAT, BT>(a, acc, smem, bq, t0, row0);
 }
 
 size_t x3_lds_bytes(int rows_in) {
@@ -1022,9 +1041,12 @@ __attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args*
         const size_t lds = x3_lds_bytes(rows_in);
         if (lds > 160 * 1024) return STZS_ESHAPE;
         void (*k)(stzs_conv_args) = nullptr;
-#define STZS_X3_PICK(TI, TO)                                                            \
-    k = a->pro_act == STZS_ACT_SNAKE ? conv_x3<TI, TO, STZS_ACT_SNAKE>                  \
-        : a->pro_act == STZS_ACT_LEAKY ? conv_x3<TI, TO, STZS_ACT_LEAKY> : conv_x3<TI, TO, STZS_ACT_NONE>;
+        const bool flat = a->ks == 1 && a->stride == 1 && a->pad == 0 && a->ups == 0 && a->pro_mode == STZS_PRO_NONE &&
+                          a->pro_act == STZS_ACT_NONE && a->T_in == a->T_out && !a->stat_part;
+#define STZS_X3_PICK(TI, TO)                                                                         \
+    k = flat ? conv_x3<TI, TO, STZS_ACT_NONE, true>                                                  \
+        : a->pro_act == STZS_ACT_SNAKE ? conv_x3<TI, TO, STZS_ACT_SNAKE, false>                      \
+        : a->pro_act == STZS_ACT_LEAKY ? conv_x3<TI, TO, STZS_ACT_LEAKY, false> : conv_x3<TI, TO, STZS_ACT_NONE, false>;
         if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32) { STZS_X3_PICK(float, float) }
         else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_BF16) { STZS_X3_PICK(float, bf16_t) }
         else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) { STZS_X3_PICK(bf16_t, float) }
@@ -1034,7 +1056,8 @@ __attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args*
         if (a->pro_act != STZS_ACT_NONE && a->pro_act != STZS_ACT_LEAKY && a->pro_act != STZS_ACT_SNAKE)
             return STZS_EINVAL;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        dim3 grid((unsigned)a->B * (unsigned)((a->T_out + BT - 1) / BT), a->co_pad / BCO);
+        dim3 grid(flat ? (unsigned)(((long)a->B * a->T_out + BT - 1) / BT)
+                       : (unsigned)a->B * (unsigned)((a->T_out + BT - 1) / BT), a->co_pad / BCO);
         hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, *a);
         STZS_LAUNCH_CHECK();
         return STZS_OK;

@@ -165,9 +165,13 @@ def test_configs2_rows_batch_invariant(v0, c2):
         assert torch.equal(out[k].cpu(), g[k][r]), k
 
 
-def test_two_shard_streams_match_eager(v0, c2):
+@pytest.mark.parametrize("branch_streams", [False, True])
+def test_two_shard_streams_match_eager(v0, c2, branch_streams):
     """the bench's concurrent form: two engine twins, each shard captured as front + back graphs, replayed on
-    two streams (shard 1 one front phase behind) -> bit-identical to the eager single-stream batch."""
+    two streams (shard 1 one front phase behind) -> bit-identical to the eager single-stream batch.
+    branch_streams: each twin also forks its independent branches (text || prompt encoder, F0 || N predictor
+    branches) onto side streams inside its graphs -- the variant that faulted in round 1 when the branches
+    shared one statistics slab / workspace (now per-branch scratch, engine.py:_scratch)."""
     S, P, eng = v0
     (tok, ref, eps, dur, seeds), g = c2
     dev = eng.device
@@ -177,12 +181,12 @@ def test_two_shard_streams_match_eager(v0, c2):
     res, pairs, sts, tws = [], [], [], []
     for i in range(2):
         tw = eng.twin()
+        tw.branch_streams = branch_streams
         sl = slice(i * nb, (i + 1) * nb)
         st = {}
 
         def front(tw=tw, sl=sl, st=st):
-            h = tw.text_encode(tok_d[sl])
-            pr = tw.prompt_encode(ref_d[sl])
+            h, pr = tw.encode_inputs(tok_d[sl], ref_d[sl])
             codes = tw.sample_style(h, pr, eps_d[sl], bench.STEPS_THROUGHPUT, bench.CFG)
             st["codes"], st["pro"] = codes, tw.predict_prosody(h, codes, dur_d[sl], nf)
 

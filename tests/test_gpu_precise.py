@@ -3,11 +3,11 @@
 bf16 storage cannot meet that bound (rounding the decoder weights to bf16 ALONE moves the oracle's own
 log-mel by 1.3e-2 L1).  Precise mode keeps fp32 activations and computes every conv / linear on
 split bf16 operands (hi*hi + hi*lo + lo*hi, csrc/conv.hip conv_x3, STZS_CONV_W_X3), the LSTM recurrences the
-same way (csrc/lstm.hip, stzs_lstm_args.precise) and the attention in fp32 (csrc/attn.hip attn_f32):
+same way (csrc/lstm.hip, stzs_lstm_args.precise) and the attention the same way (csrc/attn.hip attn_x3):
 StyleTTSZS(precise_decoder=True) for the decoder, StyleTTSZS(precise=True) for the whole pipeline.
 tools/precision_probe.py emulates exactly this arithmetic on the oracle: end-to-end log-mel L1 2.2e-4.
 Stated tolerances: conv_f32 / conv_x3 kernels max-abs 2e-5 / 4e-5 of max|ref| vs fp64 (accumulation order; the
-split drops al*bl, ~2^-16 relative per product); precise LSTM 1e-5 rel-L2, fp32 attention 1e-6 rel-L2 vs fp64;
+split drops al*bl, ~2^-16 relative per product); precise LSTM 1e-5 rel-L2 (measured 5e-6), split-operand attention 1.2e-5 rel-L2 (measured 6e-6) vs fp64;
 teacher-forced decoder log-mel L1 <= 1e-3 (north star) and waveform rel-L2 <= 1e-3; END TO END (configs[1]
 inputs at v0, and a 4-utterance 2-step batch) log-mel L1 <= 1e-3 (north star), prompt codes teacher-forced
 (the bf16 front end's output is a discrete decision, as durations elsewhere).
@@ -219,8 +219,8 @@ def test_attention_precise(gpu_device):
     qd, kd, vd = (t.double().view(R, -1, h, D // h).transpose(1, 2) for t in (q, k, v))
     ref = (torch.softmax(qd @ kd.transpose(-1, -2) / math.sqrt(D // h), -1) @ vd).transpose(1, 2).reshape(R, Lq, D)
     e = rel_err(o.cpu().double(), ref)
-    print(f"fp32 attention: rel-L2 {e:.2e}")
-    assert e < 1e-6
+    print(f"split-operand attention: rel-L2 {e:.2e}")
+    assert e < 1.2e-5
 
 
 def _logmel_l1(a, b, S):
