@@ -25,6 +25,7 @@ h2h     : the same steps timed host to host as well (tokens / reference / noise 
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -346,10 +347,10 @@ def main():
     n_hbm = sum(1 for r in rec if r[3] / (PEAK_HBM_GBS * 1e9) > r[2] / (PEAK_BF16_TFLOPS * 1e12))
     # HBM bytes per launch from the committed PMC passes of this workload (tools/pmc_bench.sh)
     traffic, tsrc = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_mrf.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic, tsrc = json.load(f).get("traffic_bytes_per_launch"), "profiles/r01_pmc_mrf.json"
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_mrf.json")))
+    if pmcs:  # the newest round's PMC passes (tools/pmc_bench.sh)
+        with open(pmcs[-1]) as f:
+            traffic, tsrc = json.load(f).get("traffic_bytes_per_launch"), "profiles/" + os.path.basename(pmcs[-1])
     roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                 frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=traffic, traffic_src=tsrc,
                 alg_bytes_per_launch=round(bsum / nl),

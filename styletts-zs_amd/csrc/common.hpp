@@ -123,3 +123,16 @@ STZS_DEV float wave_max(float v) {
     } while (0)
 
 static inline bool stzs_aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
+// CU count of the current device for grid sizing, queried once per process (a function-local static: C++11
+// thread-safe initialisation, no racing writers).  One process drives one GPU.
+static inline int stzs_cu_count() {
+    static const int n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                     hipSuccess || c <= 0)
+            c = 256;
+        return c;
+    }();
+    return n;
+}

@@ -956,13 +956,7 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     void (*k)(stzs_conv_args);
     if (F8 || (flat && sizeof(TIn) == 2 && (a.flags & STZS_CONV_A_DMA) && a.pro_cscale == 1.f)) {
         // 64-row tiles when 128-row tiles would leave the GPU under-filled (< 2 workgroups per CU)
-        static int n_cu = 0;
-        if (n_cu == 0) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-                n_cu = 256;
-        }
+        const int n_cu = stzs_cu_count();
         const bool small = (long)grid.x * grid.y < 2L * n_cu;
         size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
         const size_t lr = 4 * (size_t)(small ? gslot<64>() : gslot<128>());

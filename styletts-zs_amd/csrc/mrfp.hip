@@ -397,14 +397,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfp_conv_launch(const stzs_conv_
     // only the residual forms: measured (tools/mrfv_bench.py, B 64, stage 1) c2 324 vs 352 us, c2 + accumulate 298
     // vs 351 us; without a residual both kernels sit at the same MFMA + VALU sum (~270 us), mrfv.hip keeps those
     if (!a.res) return 1;
-    static int n_cu = 0;
-    if (n_cu == 0) {
-        int dev = 0, c = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                     hipSuccess || c <= 0)
-            c = 256;
-        n_cu = c;  // (benign race: every thread stores the same value)
-    }
+    const int n_cu = stzs_cu_count();
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
     void (*k)(stzs_conv_args) = nullptr;
     if (a.pro_act == STZS_ACT_SNAKE)
