@@ -454,7 +454,8 @@ typedef struct stzs_params_t {
 } stzs_params_t;
 
 /* packed weight forms (host-side packers; stzs/weights.py pack_conv restated in C++) */
-enum { STZS_PACK_KSTEP = 0, STZS_PACK_LANE16 = 1, STZS_PACK_FRAG32 = 2, STZS_PACK_NARROW32 = 3 };
+enum { STZS_PACK_KSTEP = 0, STZS_PACK_LANE16 = 1, STZS_PACK_FRAG32 = 2, STZS_PACK_NARROW32 = 3,
+       STZS_PACK_X3 = 4 /* precise mode: hi | lo split streams, 32-channel K-steps (STZS_CONV_W_X3) */ };
 /* bytes of the packed bf16 form of a Conv1d weight [Co][Ci][ks] (ups = 0) or ConvTranspose1d weight [Ci][Co][2 ups]
  * (ups > 0, polyphase); 0 if the form does not apply to the shape */
 size_t stzs_pack_conv_size(int Co, int Ci, int ks, int ups, int form);
@@ -466,6 +467,12 @@ int stzs_pack_conv(const float* w, int Co, int Ci, int ks, int ups, int form, vo
 int stzs_pack_lstm(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, const float* w_ih_rev,
                    const float* w_hh_rev, const float* b_ih_rev, const float* b_hh_rev, int In, int H, void* ih_packed,
                    float* ih_bias, void* whh_frags);
+/* the precise-mode LSTM (stzs_lstm_args.precise = 1): W_ih in the STZS_PACK_X3 form (stzs_pack_conv_size(8H, In, 1,
+ * 0, STZS_PACK_X3) bytes), the bias as above, and the hi fragments of both directions followed by the lo ones
+ * (2 * 2 * 4H * H bf16) */
+int stzs_pack_lstm_x3(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, const float* w_ih_rev,
+                      const float* w_hh_rev, const float* b_ih_rev, const float* b_hh_rev, int In, int H,
+                      void* ih_packed, float* ih_bias, void* whh_frags);
 
 /* a3  cfg_euler_step: in {x f32 [R, N], D f32 [R, N]} -> out {x' f32 [R, N]};
  *     i[0] = cfg (R = 2B, conditional rows first), f[0] = scale, f[1] = sigma, f[2] = sigma_next */

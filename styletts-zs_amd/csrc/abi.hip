@@ -21,6 +21,13 @@ inline uint16_t h_bf16(float f) {
     return (uint16_t)((u + r) >> 16);
 }
 
+inline float h_f32(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
 inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 inline size_t rupz(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
@@ -136,6 +143,7 @@ extern "C" size_t stzs_pack_conv_size(int Co, int Ci, int ks, int ups, int form)
             return (!ups && g.cic == 128 && Co % 8 == 0 && (ks == 3 || ks == 7 || ks == 11))
                        ? (size_t)g.ks * g.co_pad * g.ci_pad * 2 : 0;
         case STZS_PACK_NARROW32: return (!ups && g.cic == 128 && Co <= 32) ? (size_t)g.ks * 32 * g.ci_pad * 2 : 0;
+        case STZS_PACK_X3: return 2 * (size_t)g.ks * g.co_pad * g.ci_pad * 2;
         default: return 0;
     }
 }
@@ -148,6 +156,25 @@ extern "C" int stzs_pack_conv(const float* w, int Co, int Ci, int ks, int ups, i
     uint16_t* o = (uint16_t*)packed;
     const int nchunk = g.ci_pad / g.cic, kpc = g.cic / 32, ncot = g.co_pad / 128;
     auto W = [&](int tap, int col, int ci) { return wp[((size_t)tap * g.co_pad + col) * g.ci_pad + ci]; };
+    if (form == STZS_PACK_X3) {
+        // two KSTEP streams with 32-channel chunks: hi = bf16(w), then lo = bf16(w - hi)
+        // (stzs/weights.py kstep_stream_x3): [hl][cot][cc][tap][128 rows][4 positions x 8]
+        size_t n = 0;
+        for (int hl = 0; hl < 2; ++hl)
+            for (int cot = 0; cot < ncot; ++cot)
+                for (int cc = 0; cc < g.ci_pad / 32; ++cc)
+                    for (int tap = 0; tap < g.ks; ++tap)
+                        for (int r = 0; r < 128; ++r)
+                            for (int p = 0; p < 4; ++p) {
+                                const int c = p ^ GSWZ[(r >> 2) & 3];
+                                for (int e = 0; e < 8; ++e) {
+                                    const float v = W(tap, cot * 128 + r, cc * 32 + c * 8 + e);
+                                    const uint16_t hi = h_bf16(v);
+                                    o[n++] = hl ? h_bf16(v - h_f32(hi)) : hi;
+                                }
+                            }
+        return STZS_OK;
+    }
     if (form == STZS_PACK_KSTEP || form == STZS_PACK_LANE16) {
         // [cot][cc][tap][kq][128 rows][4 positions x 8]: position p of row r holds chunk p ^ g((r >> 2) & 3)
         size_t n = 0;
@@ -221,6 +248,40 @@ extern "C" int stzs_pack_lstm(const float* w_ih, const float* w_hh, const float*
                     for (int e = 0; e < 8; ++e)
                         o[n++] = h_bf16(W[(size_t)(ct * 16 + (l & 15)) * H + ks * 32 + 8 * (l >> 4) + e]);
     }
+    return STZS_OK;
+}
+
+extern "C" int stzs_pack_lstm_x3(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
+                                 const float* w_ih_rev, const float* w_hh_rev, const float* b_ih_rev,
+                                 const float* b_hh_rev, int In, int H, void* ih_packed, float* ih_bias, void* whh_frags) {
+    if (!w_ih || !w_hh || !b_ih || !b_hh || !w_ih_rev || !w_hh_rev || !b_ih_rev || !b_hh_rev || !ih_packed ||
+        !ih_bias || !whh_frags)
+        return STZS_EINVAL;
+    if (In <= 0 || H <= 0 || H % 32) return STZS_ESHAPE;
+    const int G4 = 4 * H;
+    std::vector<float> wih((size_t)2 * G4 * In);
+    memcpy(wih.data(), w_ih, sizeof(float) * G4 * In);
+    memcpy(wih.data() + (size_t)G4 * In, w_ih_rev, sizeof(float) * G4 * In);
+    const int rc = stzs_pack_conv(wih.data(), 2 * G4, In, 1, 0, STZS_PACK_X3, ih_packed);
+    if (rc) return rc;
+    for (int j = 0; j < G4; ++j) {
+        ih_bias[j] = b_ih[j] + b_hh[j];
+        ih_bias[G4 + j] = b_ih_rev[j] + b_hh_rev[j];
+    }
+    uint16_t* o = (uint16_t*)whh_frags;  // [hl][dir][4H/16][H/32][64 lanes][8]
+    size_t n = 0;
+    for (int hl = 0; hl < 2; ++hl)
+        for (int dir = 0; dir < 2; ++dir) {
+            const float* W = dir ? w_hh_rev : w_hh;
+            for (int ct = 0; ct < G4 / 16; ++ct)
+                for (int ks = 0; ks < H / 32; ++ks)
+                    for (int l = 0; l < 64; ++l)
+                        for (int e = 0; e < 8; ++e) {
+                            const float v = W[(size_t)(ct * 16 + (l & 15)) * H + ks * 32 + 8 * (l >> 4) + e];
+                            const uint16_t hi = h_bf16(v);
+                            o[n++] = hl ? h_bf16(v - h_f32(hi)) : hi;
+                        }
+        }
     return STZS_OK;
 }
 

@@ -163,7 +163,7 @@ class Params(C.Structure):
     _fields_ = [("i", i32 * 16), ("f", f32 * 8)]
 
 
-PACK_KSTEP, PACK_LANE16, PACK_FRAG32, PACK_NARROW32 = 0, 1, 2, 3
+PACK_KSTEP, PACK_LANE16, PACK_FRAG32, PACK_NARROW32, PACK_X3 = 0, 1, 2, 3, 4
 GENERIC_OPS = ["cfg_euler_step", "duration_head", "length_regulate", "sine_gen", "conv_post_istft", "bilstm",
                "conv_transpose_up", "mrf_resblock"]
 
@@ -200,7 +200,7 @@ EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_ch
            "stzs_stft_frames", "stzs_log_mel", "stzs_pool_rows", "stzs_code_quantize",
            "stzs_dn_cond", "stzs_dn_cond_steps", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed", "stzs_embed_f32", "stzs_dn_cond_steps_f32", "stzs_pack_conv_size", "stzs_pack_conv",
-           "stzs_pack_lstm"] + [f"stzs_{o}{sfx}" for o in GENERIC_OPS for sfx in ("", "_workspace")]
+           "stzs_pack_lstm", "stzs_pack_lstm_x3"] + [f"stzs_{o}{sfx}" for o in GENERIC_OPS for sfx in ("", "_workspace")]
 
 _lib = None
 
@@ -259,6 +259,7 @@ def load():
         "stzs_pack_conv_size": ([i32, i32, i32, i32, i32], C.c_size_t),
         "stzs_pack_conv": ([vp, i32, i32, i32, i32, i32, vp], i32),
         "stzs_pack_lstm": ([vp] * 8 + [i32, i32, vp, vp, vp], i32),
+        "stzs_pack_lstm_x3": ([vp] * 8 + [i32, i32, vp, vp, vp], i32),
     }
     for o in GENERIC_OPS:
         sig[f"stzs_{o}"] = ([P(Tensor), i32, P(Tensor), i32, P(Params), vp, C.c_size_t, vp], i32)

@@ -41,6 +41,48 @@ def test_pack_conv_matches_python(Co, Ci, ks, ups, form):
     assert out.tobytes() == want
 
 
+@pytest.mark.parametrize("Co,Ci,ks,ups", [(128, 128, 3, 0), (80, 96, 3, 0), (1536, 512, 1, 0), (22, 128, 7, 0),
+                                          (256, 512, 20, 10)])
+def test_pack_conv_x3_matches_python(Co, Ci, ks, ups):
+    """the precise-mode split streams (hi | lo, 32-channel K-steps) bit-identical to stzs/weights.py."""
+    from stzs.weights import Arena, pack_conv
+    lib = L.load()
+    g = torch.Generator().manual_seed(Co + 3 * Ci + ks)
+    shape = (Ci, Co, 2 * ups) if ups else (Co, Ci, ks)
+    w = torch.randn(shape, generator=g) / math.sqrt(Ci * ks)
+    A = Arena()
+    cw = pack_conv(A, "t", w, None, ups=ups, x3=True)
+    A.finalize("cpu")
+    want = A[cw.wx3].contiguous().view(torch.uint8).numpy().tobytes()
+    n = lib.stzs_pack_conv_size(Co, Ci, ks, ups, L.PACK_X3)
+    assert n == len(want)
+    out = np.zeros(n, dtype=np.uint8)
+    wc = np.ascontiguousarray(w.numpy(), dtype=np.float32)
+    assert lib.stzs_pack_conv(wc.ctypes.data, Co, Ci, ks, ups, L.PACK_X3, out.ctypes.data) == L.OK
+    assert out.tobytes() == want
+
+
+def test_pack_lstm_x3_matches_python(tiny_params):
+    from stzs.weights import Arena, pack_lstm
+    lib = L.load()
+    P = tiny_params
+    A = Arena()
+    lw = pack_lstm(A, "pr.de0", P, x3=True)
+    A.finalize("cpu")
+    ih_want = A[lw.ih.wx3].contiguous().view(torch.uint8).numpy().tobytes()
+    f_want = A[lw.whx3].contiguous().view(torch.uint8).numpy().tobytes()
+    H, In = lw.H, P["pr.de0.w_ih"].shape[1]
+    ih = np.zeros(lib.stzs_pack_conv_size(8 * H, In, 1, 0, L.PACK_X3), np.uint8)
+    bias = np.zeros(8 * H, np.float32)
+    fr = np.zeros(2 * 2 * 4 * H * H * 2, np.uint8)
+    arrs = [np.ascontiguousarray(P["pr.de0." + n].numpy(), dtype=np.float32)
+            for n in ("w_ih", "w_hh", "b_ih", "b_hh", "w_ih_rev", "w_hh_rev", "b_ih_rev", "b_hh_rev")]
+    assert lib.stzs_pack_lstm_x3(*[a.ctypes.data for a in arrs], In, H, ih.ctypes.data, bias.ctypes.data,
+                                 fr.ctypes.data) == L.OK
+    assert ih.tobytes() == ih_want
+    assert fr.tobytes() == f_want
+
+
 def test_pack_conv_rejects_inapplicable_forms():
     lib = L.load()
     assert lib.stzs_pack_conv_size(22, 128, 7, 0, L.PACK_FRAG32) == 0   # Co % 8
