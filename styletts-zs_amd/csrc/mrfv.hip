@@ -89,13 +89,17 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     const int dP = dil * P;
     const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x) + (long)bq * a.bsx;
     const int cv = tid & 15, rsub = tid >> 4;
-    bf16x8 wf[3][2];
+#ifndef STZS_MRFV_PD
+#define STZS_MRFV_PD 2
+#endif
+    constexpr int PD = STZS_MRFV_PD;  // weight K-steps in flight ahead of the MFMAs
+    bf16x8 wf[PD + 1][2];
     bf16x8 xf[8];
 
     for (int cc = 0; cc < nchunk; ++cc) {
         const int kb = cc * NKC;
-        wload(wf[0], kb);  // the chunk's first two weight K-steps fly during the staging
-        wload(wf[1], kb + 1);
+#pragma unroll
+        for (int i = 0; i < PD; ++i) wload(wf[i], kb + i);  // the chunk's first PD weight K-steps fly during the staging
         __syncthreads();  // every wave is done reading the previous chunk's tile and constants
 #ifndef STZS_MRFV_NOSTAGE
         if (!(a.flags & 1)) {
@@ -210,14 +214,14 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
             for (int mt = 0; mt < 8; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
 #pragma unroll
             for (int s = 0; s < NKC; ++s) {
-                if (s + 2 < NKC) wload(wf[(s + 2) % 3], kb + s + 2);
+                if (s + PD < NKC) wload(wf[(s + PD) % (PD + 1)], kb + s + PD);
                 const int sn = s + 1;
                 const int offn = (sn >> 2) * dP + (sn & 3) * 64;
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
                     const bool z = FIRST && s == 0;
-                    acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % 3][0], xf[mt], z ? zero : acc[0][mt], 0, 0, 0);
-                    acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % 3][1], xf[mt], z ? zero : acc[1][mt], 0, 0, 0);
+                    acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % (PD + 1)][0], xf[mt], z ? zero : acc[0][mt], 0, 0, 0);
+                    acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % (PD + 1)][1], xf[mt], z ? zero : acc[1][mt], 0, 0, 0);
                     if (sn < NKC) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + offn + mt * 16 * P);
                 }
                 if (s + 2 < NKC) {
