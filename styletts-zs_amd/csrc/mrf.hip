@@ -45,8 +45,13 @@ STZS_DEV float row_sum16(float x) {
     return x;
 }
 
-template <int PACT, bool HR, bool HA>
-__global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
+// NR: weight-ring slots (power of 2), filled NR - 1 K-steps ahead.  NR = 4 at two workgroups per CU; NR = 8 (64 KB of
+// ring) when the grid is smaller than the CU count (batch 1: 16-64 workgroups whose K loop is a serial chain of
+// LDS-DMA round trips -- the bytes in flight per CU, not the MFMAs, set its pace).  Same K order: bit-identical.
+template <int PACT, bool HR, bool HA, int NR>
+__global__ __launch_bounds__(NTH, NR == 4 ? 2 : 1) void mrf_conv(const stzs_conv_args a) {
+    constexpr int NSL = NR;
+    constexpr int FD = NR - 1;  // fill distance
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ks = a.ks, dil = a.dil;
     const int rows_in = BT + (ks - 1) * dil;
@@ -72,6 +77,12 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
                                          (__attribute__((address_space(3))) void*)(dst + 1024), 16, 0, 0);
     };
     f32x4 acc[4][4];  // [nt: channel tile][mt: time tile]
+    auto gate_wait = [&]() {  // fill k+1 landed; fills k+2 .. k+FD-1 (2 LDS-DMA instructions each) may fly
+        if constexpr (FD == 3)
+            __builtin_amdgcn_s_waitcnt(0x0F72);
+        else
+            __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * (FD - 2)));
+    };
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -100,8 +111,8 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
 
     const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x) + (long)bq * a.bsx;
     const int cv = tid & 15, rsub = tid >> 4;
-    fill(0);
-    fill(1);
+#pragma unroll
+    for (int i = 0; i < FD - 1; ++i) fill(i);
     int k = 0;
     for (int cc = 0; cc < nchunk; ++cc) {
         __syncthreads();  // every wave is done reading the previous chunk's input tile
@@ -119,9 +130,9 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
                 raw[i] = *reinterpret_cast<const uint4*>(X + (long)tin * a.ldx + cl);
             }
             // per-channel constants, computed once per channel by 128 threads into the ring slot that
-            // stays idle until this chunk's first K-step fills it (slot (k + 3) & 3):
+            // stays idle until this chunk's first K-step fills it (slot (k + FD) & (NSL - 1)):
             //   t = x*ka + kb (revolutions of cos(2 a y)),  out = cos(t) * km + (x*ksc + ksh)
-            float* cs = reinterpret_cast<float*>(ring + ((k + 3) & (NSL - 1)) * SLOT);
+            float* cs = reinterpret_cast<float*>(ring + ((k + FD) & (NSL - 1)) * SLOT);
             if (tid < 128) {
                 const int ch = cc * 128 + tid;
                 const bool ok = ch < a.Ci;
@@ -188,8 +199,8 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
             }
         }
         __syncthreads();
-        if (cc == 0) {  // (the barrier above drained fills 0 and 1)
-            fill(2);
+        if (cc == 0) {  // (the barrier above drained fills 0 .. FD-2)
+            fill(FD - 1);
             readB(fb0, 0);
         }
         readA(fa0, arow0);
@@ -198,9 +209,9 @@ __global__ __launch_bounds__(NTH, 2) void mrf_conv(const stzs_conv_args a) {
         // slot k-1 -> NEXT fragments read between the CURRENT K-step's 16 MFMAs
 #define STZS_MRF_STEP(FX, FW, NX, NW, AOFF)                                     \
     {                                                                           \
-        __builtin_amdgcn_s_waitcnt(0x0F72);                                     \
+        gate_wait();                                                            \
         __builtin_amdgcn_s_barrier();                                           \
-        fill(k + 3);                                                            \
+        fill(k + FD);                                                           \
         __builtin_amdgcn_sched_barrier(0);                                      \
         readB(NW, k + 1);                                                       \
         readA(NX, AOFF);                                                        \
@@ -538,25 +549,34 @@ __attribute__((visibility("hidden"))) int stzs_mrf_conv_launch(const stzs_conv_a
         a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8)) || (a.acc_in && (a.lda % 8 || a.bsa % 8)))
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
-    const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + NSL * SLOT;
-    if (lds > 160 * 1024) return STZS_ESHAPE;
     dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / BCO);
+    // a grid below the CU count (batch 1) gets the deep ring: one workgroup per CU anyway, more bytes in flight
+    const bool deep = (long)grid.x * grid.y < stzs_cu_count();
+    const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + (deep ? 8 : NSL) * SLOT;
+    if (lds > 160 * 1024) return STZS_ESHAPE;
     void (*k)(stzs_conv_args) = nullptr;
-    if (a.pro_act == STZS_ACT_SNAKE) {
-        if (a.res && a.acc_in)
-            k = mrf_conv<STZS_ACT_SNAKE, true, true>;
-        else if (a.res)
-            k = mrf_conv<STZS_ACT_SNAKE, true, false>;
-        else if (a.acc_in)
-            k = mrf_conv<STZS_ACT_SNAKE, false, true>;
-        else
-            k = mrf_conv<STZS_ACT_SNAKE, false, false>;
-    } else if (!a.acc_in) {  // the AdaIN residual blocks of the decoder / prosody predictor
-        if (a.pro_act == STZS_ACT_LEAKY)
-            k = a.res ? mrf_conv<STZS_ACT_LEAKY, true, false> : mrf_conv<STZS_ACT_LEAKY, false, false>;
-        else if (a.pro_act == STZS_ACT_NONE)
-            k = a.res ? mrf_conv<STZS_ACT_NONE, true, false> : mrf_conv<STZS_ACT_NONE, false, false>;
+#define STZS_MRF_PICK(NR)                                                                                        \
+    if (a.pro_act == STZS_ACT_SNAKE) {                                                                           \
+        if (a.res && a.acc_in)                                                                                   \
+            k = mrf_conv<STZS_ACT_SNAKE, true, true, NR>;                                                        \
+        else if (a.res)                                                                                          \
+            k = mrf_conv<STZS_ACT_SNAKE, true, false, NR>;                                                       \
+        else if (a.acc_in)                                                                                       \
+            k = mrf_conv<STZS_ACT_SNAKE, false, true, NR>;                                                       \
+        else                                                                                                     \
+            k = mrf_conv<STZS_ACT_SNAKE, false, false, NR>;                                                      \
+    } else if (!a.acc_in) { /* the AdaIN residual blocks of the decoder / prosody predictor */                   \
+        if (a.pro_act == STZS_ACT_LEAKY)                                                                         \
+            k = a.res ? mrf_conv<STZS_ACT_LEAKY, true, false, NR> : mrf_conv<STZS_ACT_LEAKY, false, false, NR>;  \
+        else if (a.pro_act == STZS_ACT_NONE)                                                                     \
+            k = a.res ? mrf_conv<STZS_ACT_NONE, true, false, NR> : mrf_conv<STZS_ACT_NONE, false, false, NR>;    \
     }
+    if (deep) {
+        STZS_MRF_PICK(8)
+    } else {
+        STZS_MRF_PICK(4)
+    }
+#undef STZS_MRF_PICK
     if (!k) return STZS_ESHAPE;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
