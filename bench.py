@@ -212,7 +212,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from stzs.engine import StyleTTSZS
+    from stzs.engine import LATENCY_DN_SPLITK, StyleTTSZS
     from stzs.params import init_params
     from stzs.spec import SPEC_V0
     S = SPEC_V0
@@ -364,15 +364,17 @@ def main():
     lat = None
     if not args.no_latency:
         tok1, ref1, eps1, dur1 = (t.to(dev) for t in make_inputs(S, 1, seed=1000 + rank))
+        # the batch-1 serving engine: same packed weights, split-K ffn2 (stzs/engine.py LATENCY_DN_SPLITK)
+        elat = StyleTTSZS(S, None, device=dev, packed=W, dn_splitk=LATENCY_DN_SPLITK)
 
         def one():
-            return eng.synth(tok1, ref1, steps=STEPS_LATENCY, cfg_scale=CFG, noise=eps1, durations=dur1, seeds=[7],
+            return elat.synth(tok1, ref1, steps=STEPS_LATENCY, cfg_scale=CFG, noise=eps1, durations=dur1, seeds=[7],
                              n_frames=n_frames)
         one()
         g1 = None
         if graph is not None:
             try:
-                g1, _ = eng.capture(one)
+                g1, _ = elat.capture(one)
             except Exception:
                 g1 = None
         r1 = g1.replay if g1 is not None else one
@@ -385,7 +387,8 @@ def main():
             if i >= 5:
                 ts.append((time.perf_counter() - a) * 1e3)
         lat = dict(p50_ms=round(float(np.percentile(ts, 50)), 3), p90_ms=round(float(np.percentile(ts, 90)), 3),
-                   config="batch 1, 10-step sampling, CFG 5, 5-s target, 3-s reference")
+                   config="batch 1, 10-step sampling, CFG 5, 5-s target, 3-s reference",
+                   dn_splitk=dict(LATENCY_DN_SPLITK))
 
     # ---- configs[4]: 30-s target, batch 1, fp8 denoiser linears, streaming iSTFT (1-s chunks) ----
     lf = None

@@ -87,7 +87,23 @@ typedef struct stzs_conv_args {
      * usual epilogue.  Plain linears only (ks = 1, flags STZS_CONV_A_DMA); NULL otherwise. */
     const float* x_scale;
     const float* w_scale;
+    /* in-launch split-K for bf16 linears (the LDS-DMA GEMM path: ks = 1, STZS_CONV_A_DMA, bf16 x, not fp8):
+     * splitk in {0, 1} = off, {2, 4} = the ci_pad / 32 K-steps (a multiple of splitk) of every 64-row x
+     * 128-column output tile are split over splitk workgroups (grid z).  Each writes its fp32 partial tile to
+     * splitk_ws with write-through stores and takes a ticket on splitk_ctr[tile]; the last arriver reads the
+     * splitk slabs back and sums them in slice order 0, 1, ... (the result depends neither on the arrival order
+     * nor on the row count: batch-invariant) and runs the usual epilogue.  splitk_ws: 16-B aligned,
+     * stzs_conv_splitk_workspace() bytes; splitk_ctr: one uint32 per tile, ZERO before the first launch (every
+     * launch leaves them zero).  Used for the batch-1 denoiser linears, whose 8-32 output tiles would otherwise
+     * stream all of K through 8-32 CUs (configs[1]). */
+    void* splitk_ws;
+    unsigned int* splitk_ctr;
+    int32_t splitk;
+    int32_t pad_sk;
 } stzs_conv_args;
+/* split-K workspace of a linear over `rows` flat rows: fp32 slab bytes; the tile (= counter) count is
+ * bytes / (splitk * 32768).  0 for a bad argument. */
+size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
 #define STZS_CONV_STAT_ROWS 64
 /* flags bit: weights packed with the 16-lane channel permutation of the MRF kernel (stzs/weights.py
  * pack_conv(lane16=True)): inside each 128-column tile, packed row wc*64 + nt*16 + g*4 + r holds

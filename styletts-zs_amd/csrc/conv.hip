@@ -540,7 +540,12 @@ STZS_DEV void glds16(const void* src, void* dst) {
 template <int BTM>
 constexpr int gslot() { return BTM * 64 + SLOT_BYTES; }  // A (BTM rows x 64 B) + B of one K-step
 typedef __attribute__((ext_vector_type(2))) long i64x2;
-template <typename TOut, int BTM, bool F8>
+// SK > 1 (stzs_conv_args.splitk, BTM = 64, bf16): workgroup z of a tile runs K-steps [z NK/SK, (z+1) NK/SK) and
+// hands its fp32 partial to the tile's last arriver (splitk_combine), which then runs the epilogue.
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+template <int BTM, int SK>
+STZS_DEV bool splitk_combine(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem);
+template <typename TOut, int BTM, bool F8, int SK = 1>
 __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     constexpr int MT = BTM / 32;           // 16-row tiles per wave (2 x 2 waves)
     constexpr int GS = gslot<BTM>();
@@ -553,6 +558,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     const long row0 = (long)blockIdx.x * BTM;
     const long nR = (long)a.B * a.T_in;
     const int NK = a.ci_pad / (64 / ESZ);
+    const int NKS = NK / SK;                                  // K-steps of this workgroup's slice
+    const int kb = SK > 1 ? (int)blockIdx.z * NKS : 0;
     const unsigned char* Wt = reinterpret_cast<const unsigned char*>(a.w) + (long)blockIdx.y * NK * SLOT_BYTES;
     const unsigned char* X = reinterpret_cast<const unsigned char*>(a.x);
     long asrc[AP];  // byte offsets
@@ -566,7 +573,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         asrc[i] = (bb * a.bsx + (R - bb * a.T_in) * a.ldx) * ESZ + ((p ^ gswz(r)) << 4);
     }
     auto fill = [&](int k) {
-        const int kc = k < NK ? k : NK - 1;
+        const int kc = kb + (k < NKS ? k : NKS - 1);
         const unsigned char* src = Wt + (long)kc * SLOT_BYTES + wave * 2048 + lane * 16;
         unsigned char* da = smem + (k & 3) * GS + wave * AP * 1024;
         unsigned char* db = smem + (k & 3) * GS + BTM * 64 + wave * 2048;
@@ -634,7 +641,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         ++k;                                                                    \
     }
     int k = 0;
-    const int nsteps = (a.flags & 2) ? 1 : NK;
+    const int nsteps = (a.flags & 2) ? 1 : NKS;
     for (; k + 2 < nsteps;) {
         STZS_GEMM_STEP(fa0, fb0, fa1, fb1)
         STZS_GEMM_STEP(fa1, fb1, fa0, fb0)
@@ -661,7 +668,59 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
                 for (int nt = 0; nt < 4; ++nt) acc[mt][nt][r] *= sx * sw[nt];
             }
     }
+    if constexpr (SK > 1) {
+        if (!splitk_combine<BTM, SK>(a, acc, smem)) return;
+    }
     finish<TOut, true, BTM>(a, acc, smem, 0, 0, row0);
+}
+
+// In-launch split-K hand-off (MI355X guide: cdna_hip_programming.md, "In-launch split-K reduction", the sc1
+// form of the Guideline 16 counter hand-off).  Slab of (tile, slice s): [NV][NTHR] f32x4, thread-linear so
+// every store / load is one coalesced 16-B access per lane.  Producer: write-through (sc1) stores, every
+// wave's vmcnt(0) (which also drains the ring's trailing LDS-DMA fills), workgroup barrier, lane 0 takes a
+// relaxed agent-scope ticket.  The ticket SK - 1 is the last arriver: it resets the counter for the next
+// launch, reads EVERY slab (its own included) with sc1 loads and sums them in slice order, so the value is
+// the same whichever workgroup combines.  Correct for any placement of the slices over CUs / XCDs.
+template <int BTM, int SK>
+STZS_DEV bool splitk_combine(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem) {
+    constexpr int NV = BTM / 32 * 4;         // f32x4 accumulators per thread
+    constexpr int SLAB = NV * NTHR * 16;     // bytes per (tile, slice)
+    const int tid = threadIdx.x;
+    const long tile = blockIdx.x + (long)gridDim.x * blockIdx.y;
+    unsigned char* base = reinterpret_cast<unsigned char*>(a.splitk_ws) + tile * (long)(SK * SLAB);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(base, 0, SK * SLAB, 0x00020000);
+    const int z = blockIdx.z;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i >> 2][i & 3]), wr,
+                                               (z * NV + i) * (NTHR * 16) + tid * 16, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    volatile int* flag = reinterpret_cast<volatile int*>(smem);  // the ring is idle: its fills drained above
+    if (tid == 0) {
+        typedef __attribute__((address_space(1))) unsigned int gu32;
+        gu32* ctr = (gu32*)(a.splitk_ctr + tile);
+        const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (unsigned)(SK - 1);
+        if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return false;
+    u32x4 v[SK][NV];
+#pragma unroll
+    for (int s = 0; s < SK; ++s)
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            v[s][i] = __builtin_amdgcn_raw_buffer_load_b128(wr, (s * NV + i) * (NTHR * 16) + tid * 16, 0, 16);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        f32x4 t = __builtin_bit_cast(f32x4, v[0][i]);
+#pragma unroll
+        for (int s = 1; s < SK; ++s) t += __builtin_bit_cast(f32x4, v[s][i]);
+        acc[i >> 2][i & 3] = t;
+    }
+    return true;
 }
 
 // PRECISE (parity) mode, STZS_CONV_W_F32: fp32 operands on v_mfma_f32_16x16x4_f32 (products exact in
@@ -957,17 +1016,29 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     if (F8 || (flat && sizeof(TIn) == 2 && (a.flags & STZS_CONV_A_DMA) && a.pro_cscale == 1.f)) {
         // 64-row tiles when 128-row tiles would leave the GPU under-filled (< 2 workgroups per CU)
         const int n_cu = stzs_cu_count();
-        const bool small = (long)grid.x * grid.y < 2L * n_cu;
+        bool small = (long)grid.x * grid.y < 2L * n_cu;
         size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
         const size_t lr = 4 * (size_t)(small ? gslot<64>() : gslot<128>());
         lg = lg > lr ? lg : lr;
         auto kg = small ? gemm_glds<TOut, 64, F8> : gemm_glds<TOut, 128, F8>;
+        if (a.splitk > 1) {  // split-K: 64-row tiles at every row count (the K order must not depend on M)
+            const int NK = a.ci_pad / 32;
+            if (F8 || (a.splitk != 2 && a.splitk != 4) || NK % a.splitk || !a.splitk_ws || !a.splitk_ctr ||
+                !stzs_aligned(a.splitk_ws, 16) || !stzs_aligned(a.splitk_ctr, 4))
+                return STZS_EINVAL;
+            if constexpr (!F8) kg = a.splitk == 2 ? gemm_glds<TOut, 64, false, 2> : gemm_glds<TOut, 64, false, 4>;
+            small = true;
+            grid.z = (unsigned)a.splitk;
+            lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
+            lg = lg > 4 * (size_t)gslot<64>() ? lg : 4 * (size_t)gslot<64>();
+        }
         if (small) grid.x = (unsigned)(((long)a.B * a.T_out + 63) / 64);
         (void)hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);
         hipLaunchKernelGGL(kg, grid, dim3(NTHR), lg, s, a);
         STZS_LAUNCH_CHECK();
         return STZS_OK;
     }
+    if (a.splitk > 1) return STZS_EINVAL;  // split-K exists on the LDS-DMA GEMM path only
     if constexpr (F8) {
         return STZS_EDTYPE;  // (unreachable: fp8 is a pure linear)
     } else {
@@ -999,6 +1070,8 @@ __attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args*
         a->stride <= 0)
         return STZS_ESHAPE;
     if (a->ci_pad % a->cic || a->ci_pad < a->Ci || a->co_pad % BCO) return STZS_ESHAPE;
+    if (a->splitk > 1 && (a->flags & (STZS_CONV_W_X3 | STZS_CONV_W_F32 | STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32)))
+        return STZS_EINVAL;
     const int ncol = a->ups > 0 ? a->ups * a->Co : a->Co;
     if (a->co_pad < ncol) return STZS_ESHAPE;
     if (a->ldx % 8 || a->bsx % 8 || a->ldx < ((a->Ci + 7) / 8) * 8) return STZS_ESHAPE;
@@ -1083,4 +1156,10 @@ __attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args*
     if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_BF16) return launch_dt<float, bf16_t>(*a, s);
     if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32) return launch_dt<float, float>(*a, s);
     return STZS_EDTYPE;
+}
+
+extern "C" size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk) {
+    if (rows <= 0 || co_pad <= 0 || co_pad % BCO || (splitk != 2 && splitk != 4)) return 0;
+    const int64_t tiles = (rows + 63) / 64 * (co_pad / BCO);
+    return (size_t)tiles * splitk * (64 / 32 * 4) * NTHR * 16;
 }

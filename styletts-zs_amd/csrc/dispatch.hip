@@ -18,6 +18,7 @@ extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
         if (!stzs_aligned(a->x, 16) || !stzs_aligned(a->w, 16) || !stzs_aligned(a->y, 16)) return STZS_EINVAL;
         if (a->pro_mode == STZS_PRO_ADAIN && (!a->pro_mean || !a->pro_rstd || !a->pro_gb)) return STZS_EINVAL;
         if (a->in_dtype == STZS_F8 || a->x_scale) return STZS_EDTYPE;
+        if (a->splitk > 1) return STZS_EINVAL;
         if (a->stat_part && !stzs_aligned(a->stat_part, 8)) return STZS_EINVAL;
         return stzs_mrfv_conv_launch(*a, reinterpret_cast<hipStream_t>(stream));
     }

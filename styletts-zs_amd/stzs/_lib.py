@@ -40,7 +40,8 @@ class ConvArgs(C.Structure):
                                    "ci_pad", "co_pad", "cic", "ups", "ups_pad", "T_final", "refl", "res_tdiv",
                                    "in_dtype", "out_dtype", "pro_mode", "pro_act", "epi_act", "flags")] + \
                [(n, f32) for n in ("pro_cscale", "pro_slope", "epi_slope", "alpha", "beta", "pad_f")] + \
-               [("stat_part", vp), ("stat_ld", i64), ("x_scale", vp), ("w_scale", vp)]
+               [("stat_part", vp), ("stat_ld", i64), ("x_scale", vp), ("w_scale", vp),
+                ("splitk_ws", vp), ("splitk_ctr", vp), ("splitk", i32), ("pad_sk", i32)]
 
 
 class StatsArgs(C.Structure):
@@ -193,7 +194,8 @@ def params(ints=(), floats=()) -> Params:
 
 
 # every exported symbol of include/stzs.h (tests check the .so exports exactly these)
-EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_chan_stats_workspace",
+EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_conv_splitk_workspace",
+           "stzs_chan_stats_workspace",
            "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
@@ -224,6 +226,7 @@ def load():
         "stzs_strerror": ([i32], C.c_char_p),
         "stzs_version": ([], i32),
         "stzs_conv1d": ([P(ConvArgs), vp], i32),
+        "stzs_conv_splitk_workspace": ([i64, i32, i32], C.c_size_t),
         "stzs_chan_stats_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
         "stzs_chan_stats_final": ([P(StatsArgs), i32, vp], i32),

@@ -30,6 +30,25 @@ from .spec import Spec
 from .weights import ConvW, PackedModel
 
 _DT = {torch.float32: L.F32, torch.bfloat16: L.BF16, torch.float8_e4m3fn: L.F8}
+# split-K slices per bf16 denoiser layer linear (stzs_conv_args.splitk), a per-engine setting.  At batch 1 (100
+# rows with CFG) ffn2 has 8 output tiles, each streaming its 64 K-steps through one CU's LDS-DMA ring; 4 slices
+# spread that over 32 CUs (14.9 -> 10.5 us; configs[1] p50 10.1 -> 9.9 ms).  The K = 512 linears lose (the hand-off
+# costs more than their 16 K-steps), and so does every linear at 6 400 rows (ffn2 26.7 -> 40.5 us; bench value
+# -1.5%), so throughput engines keep it off (DN_SPLITK) and the batch-1 latency engine uses LATENCY_DN_SPLITK
+# (tools/gemm_bench.py, DESIGN.md §5 "Batch-1 latency").  Within one engine the table is a property of the weight,
+# applied at every row count, so its results stay batch-invariant.  STZS_DN_SPLITK overrides the default of an
+# engine built without dn_splitk: "0" = off, or e.g. "ff2=4,o=2".
+DN_SPLITK = {}
+LATENCY_DN_SPLITK = dict(ff2=4)
+
+
+def _dn_splitk_default():
+    v = os.environ.get("STZS_DN_SPLITK")
+    if v is None:
+        return dict(DN_SPLITK)
+    if v.strip() in ("", "0"):
+        return {}
+    return {k: int(n) for k, n in (kv.split("=") for kv in v.split(","))}
 
 
 def _rup(x, m):
@@ -103,7 +122,7 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
-                 packed: PackedModel = None, branch_streams=False, precise=False):
+                 packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
@@ -143,6 +162,9 @@ class StyleTTSZS:
         self._side = []
         self.launches = 0
         self.lstm_spin_limit = 0  # 0 = the library default; tests force tiny values
+        # split-K of the bf16 denoiser layer linears (stzs_conv_args.splitk): a property of the weight, used at
+        # every batch size so results stay batch-invariant; {} turns it off
+        self.dn_splitk = _dn_splitk_default() if dn_splitk is None else dict(dn_splitk)
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
@@ -221,7 +243,7 @@ class StyleTTSZS:
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
-             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, what="conv"):
+             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, splitk=0, what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
         output fused into the conv epilogue (per-tile partials) + one small finalize launch."""
         W = self.W
@@ -275,6 +297,14 @@ class StyleTTSZS:
         elif getattr(cw, "narrow32", False):
             flags |= L.CONV_W_NARROW32  # narrow conv (csrc/mrf.hip)
         a.flags = flags | self.conv_flags
+        while splitk > 1 and (cw.ci_pad // 32) % splitk:  # a function of K only: batch invariance holds
+            splitk //= 2
+        if splitk > 1 and (a.flags & 8) and not cw.f8 and cw.wx3 is None and cw.w32 is None:
+            # in-launch split-K (stzs_conv_args.splitk): per-branch fp32 slabs + self-resetting tile counters
+            nb = self.lib.stzs_conv_splitk_workspace(x.B * x.T, cw.co_pad, splitk)
+            assert nb > 0, (what, splitk)
+            a.splitk, a.splitk_ws = splitk, self._scratch("sk_ws", nb // 4).data_ptr()
+            a.splitk_ctr = self._counters("sk_ctr", nb // (splitk * 32768)).data_ptr()
         st = None
         if stats_key is not None:
             Cc = _rup(cw.Co, 8)
@@ -322,6 +352,17 @@ class StyleTTSZS:
             if t is not None:
                 self._retired.append(t)
             t = self._bufs[key] = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=self.device)
+        return t
+
+    def _counters(self, name, n):
+        """int32 hand-off counters of ONE branch, zero when allocated; every kernel that uses them leaves them zero
+        (the split-K tile tickets).  Grown storages are retired, like _scratch."""
+        key = name + self._branch
+        t = self._bufs.get(key)
+        if t is None or t.numel() < n:
+            if t is not None:
+                self._retired.append(t)
+            t = self._bufs[key] = torch.zeros(max(n, 4096), dtype=torch.int32, device=self.device)
         return t
 
     def _slab(self, n):
@@ -678,26 +719,28 @@ class StyleTTSZS:
         fb = fmodx[0, i * R].data_ptr()
         lns.append(self._ln_args(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls))
         self._call(self.lib.stzs_row_layernorm, lns[0], "ln1")
+        sk = {} if (f8 or self.adt == torch.float32) else self.dn_splitk
         for l, lw in enumerate(W.dn_layers):
             mb = modx[l, i * R].data_ptr()
-            self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, what="qkv")
+            self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, splitk=sk.get("qkv", 0), what="qkv")
             self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
             xo, so = (o8, s_o) if f8 else (o, None)
             if f8:
                 self.quant(o, o8, s_o)
             self.conv(lw["o" + sfx], xo, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=so,
-                      post_ln=lns[3 * l + 1], what="sa_o")
-            self.conv(lw["q" + sfx], ain, q, x_scale=sin, what="ca_q")
+                      post_ln=lns[3 * l + 1], splitk=sk.get("o", 0), what="sa_o")
+            self.conv(lw["q" + sfx], ain, q, x_scale=sin, splitk=sk.get("q", 0), what="ca_q")
             self.attention(q, kv[l].sl(0, d), kv[l].sl(d, d), o)
             if f8:
                 self.quant(o, o8, s_o)
-            self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=lns[3 * l + 2], what="ca_o")
-            self.conv(lw["ff1" + sfx], ain, ff, epi_act=L.ACT_GELU, x_scale=sin, what="ff1")
+            self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=lns[3 * l + 2], splitk=sk.get("co", 0),
+                      what="ca_o")
+            self.conv(lw["ff1" + sfx], ain, ff, epi_act=L.ACT_GELU, x_scale=sin, splitk=sk.get("ff1", 0), what="ff1")
             xf, sf = (ff8, s_ff) if f8 else (ff, None)
             if f8:
                 self.quant(ff, ff8, s_ff)
             self.conv(lw["ff2" + sfx], xf, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=sf,
-                      post_ln=lns[3 * l + 3], what="ff2")
+                      post_ln=lns[3 * l + 3], splitk=sk.get("ff2", 0), what="ff2")
         self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], what="dn.out")
 
     def _ln_args(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=0.0, y_scale=None):
