@@ -42,7 +42,8 @@ def test_workspace_queries():
     L = _lib.load()
     assert L.stzs_chan_stats_workspace(64, 24001, 128) == 64 * 94 * 128 * 8
     # groups x dirs x 2 buffers x 64 rows x (hi | lo) H bf16: sized for the precise split-operand rows
-    assert L.stzs_lstm_workspace(64, 256, 2) == 2 * 2 * 64 * 2 * 256 * 2
+    # (+ the small-batch tagged-granule region: [dir][parity][2 rows][H/2 <= 128] u64 = 8 KB)
+    assert L.stzs_lstm_workspace(64, 256, 2) == 8192 + 2 * 2 * 64 * 2 * 256 * 2
     # split-K slabs: ceil(rows / 64) x (co_pad / 128) tiles x splitk slices x 64 x 128 fp32; bad arguments -> 0
     assert L.stzs_conv_splitk_workspace(100, 512, 4) == 2 * 4 * 4 * 64 * 128 * 4
     assert L.stzs_conv_splitk_workspace(6400, 1536, 2) == 100 * 12 * 2 * 64 * 128 * 4

@@ -377,10 +377,12 @@ def _v0_lstm(In=640, H=256, seed=9):
     return P, lw, A
 
 
-@pytest.mark.parametrize("B,T", [(64, 80), (40, 23), (1, 80)])
+@pytest.mark.parametrize("B,T", [(64, 80), (40, 23), (1, 80), (2, 50), (65, 7)])
 def test_lstm_v0_width(eng, B, T):
     """the benchmarked LSTM shape: H = 256 (8 exchanging workgroups per direction), up to 64 utterances per
-    group (4 MFMA row tiles, multi-row exchange loads) vs torch.nn.LSTM on identical bf16 inputs.
+    group (4 MFMA row tiles, multi-row exchange loads) vs torch.nn.LSTM on identical bf16 inputs; B = 1 / 2 and
+    the 1-row last group of B = 65 hand h over as tagged granules (csrc/lstm.hip TAG_ROWS), run twice: the second
+    call must not see the first call's tags (bit-identical).
     tolerance: max-abs error <= 2e-2 of max|ref| (bf16 h exchanged every step, fp32 cell state)."""
     from oracle.stzs_ref import bilstm
     from stzs.engine import Act
@@ -391,18 +393,25 @@ def test_lstm_v0_width(eng, B, T):
     y = Act(torch.zeros(B, T, 512, dtype=torch.bfloat16, device="cuda:0"))
     eng.lstm(lw, Act(x.to(torch.bfloat16).cuda()), y, f"t.lstm{B}")
     assert eng.check_status() == 0
+    y0 = y.t.clone()
+    y.t.zero_()
+    eng.lstm(lw, Act(x.to(torch.bfloat16).cuda()), y, f"t.lstm{B}")
+    assert eng.check_status() == 0
+    assert torch.equal(y.t, y0)
     e = max_rel(y.t.float().cpu(), ref)
     print("lstm v0", B, T, e, rel_err(y.t.float().cpu(), ref))
     assert e < 2e-2
 
 
-def test_lstm_timeout_surfaces(eng):
+@pytest.mark.parametrize("B", [8, 1])
+def test_lstm_timeout_surfaces(eng, B):
     """a spin that times out (forced: spin limit 1 poll) ORs STZS_STATUS_LSTM_TIMEOUT into the engine's
-    status word; check_status() raises on it and clears it, and a normal run afterwards is clean."""
+    status word; check_status() raises on it and clears it, and a normal run afterwards is clean.  B = 1: the
+    tagged-granule sweep's spin."""
     from stzs.engine import Act
     _P, lw, _A = _v0_lstm()
-    x = Act(torch.randn(8, 200, 640).to(torch.bfloat16).cuda())
-    y = Act(torch.zeros(8, 200, 512, dtype=torch.bfloat16, device="cuda:0"))
+    x = Act(torch.randn(B, 200, 640).to(torch.bfloat16).cuda())
+    y = Act(torch.zeros(B, 200, 512, dtype=torch.bfloat16, device="cuda:0"))
     eng.check_status()
     eng.lstm_spin_limit = 1
     try:
