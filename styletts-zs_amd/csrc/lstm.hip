@@ -34,7 +34,7 @@ namespace {
 constexpr int MROWS = 64;   // utterances per group (4 MFMA row tiles)
 constexpr int UNITS = 32;   // hidden units per workgroup
 constexpr unsigned SPIN_LIMIT = 1u << 22;
-constexpr int TAG_ROWS = 2;                                  // groups with <= 2 valid rows use granules
+constexpr int TAG_ROWS = 2;  // groups with <= TAG_ROWS valid rows use granules (32: bench -3%, the sweep's bytes)
 constexpr int TAG_BYTES = 2 * 2 * TAG_ROWS * (256 / 2) * 8;  // [dir][parity][row][H/2] u64, H <= 256
 
 typedef __attribute__((address_space(1))) unsigned int gu32;
@@ -137,8 +137,16 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
             // sweep h_{s-1}'s granules (tag s) straight into the A tile: no counter, no fence
             const gu64* src = gran + ((s - 1) & 1) * TAG_ROWS * (H / 2);
             const int ng = nrows * (H / 2);
-            for (int e = tid; e < ng; e += 512) {
-                unsigned long long x = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            constexpr int GPT = (TAG_ROWS * 128 + 511) / 512;  // granules per thread, all loads in flight first
+            unsigned long long xg[GPT];
+#pragma unroll
+            for (int i = 0; i < GPT; ++i)
+                if (tid + i * 512 < ng) xg[i] = __hip_atomic_load(src + tid + i * 512, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int i = 0; i < GPT; ++i) {
+                const int e = tid + i * 512;
+                if (e >= ng) break;
+                unsigned long long x = xg[i];
                 unsigned spins = 0;
                 while ((unsigned)(x >> 32) != (unsigned)s && s_ok) {
                     __builtin_amdgcn_s_sleep(1);
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         }
     }
     __syncthreads();
-    if (s_last && a.B - (int)(gridDim.z - 1) * MROWS <= TAG_ROWS && !PR) {  // the last group ran tagged  // the granule region back to zero (tags of this call gone)
+    if (s_last && a.B - (int)(gridDim.z - 1) * MROWS <= TAG_ROWS && !PR) {  // the last group ran tagged: its granules back to zero
         gu64* g0 = (gu64*)(a.xchg);
         for (int e = tid; e < TAG_BYTES / 8; e += 512) __hip_atomic_store(g0 + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
