@@ -68,39 +68,69 @@ __global__ __launch_bounds__(256) void pool_kernel(const stzs_pool_args a) {
     }
 }
 
-// One lane per (row, group), one wave per 64 rows of one group: every lane of a wave scans the same codebook,
-// so its entries are wave-uniform (scalar loads).  The distance is summed serially with explicitly rounded
-// sub / mul / add (the oracle's order); strict < keeps the first minimum.  ~R*G*K*dg*3 flops: negligible.
+// One workgroup per (64 rows, group): the group's codebook (K x DG fp32, <= 64 KB) is staged in LDS once, and
+// the K entries are split over the 4 waves (wave w scans [w K/4, (w+1) K/4) for its lane's row: every lane of a
+// wave reads the same entry -> LDS broadcast).  The distance is summed serially with explicitly rounded sub / mul /
+// add (the oracle's order); strict < keeps the first minimum inside a range, and the 4 range minima are combined
+// in range order with strict <, so the result is the first global minimum -- the serial scan's, bit for bit.
+// (One lane scanning all K from scalar loads was latency-bound: 52 us for the 50 x 32 (row, group) pairs of a
+// batch-1 prompt.)
+constexpr int VQ_WAVES = 4;
 template <int DG>
-__global__ __launch_bounds__(64) void vq_kernel(const stzs_vq_args a) {
-    const int r = blockIdx.x * 64 + threadIdx.x, g = blockIdx.y;
-    if (r >= a.R) return;  // no barriers in this kernel
+__global__ __launch_bounds__(64 * VQ_WAVES) void vq_kernel(const stzs_vq_args a) {
+    extern __shared__ __attribute__((aligned(16))) float cbs[];  // [K][DG], then [VQ_WAVES][64] (d, k) pairs
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * 64 + lane, g = blockIdx.y;
     const float* cb = a.codebook + (long)g * a.K * DG;
-    int best = 0;
-    if (!a.lookup) {
-        float x[DG];
-        const float* X = a.x + (long)r * a.ldx + g * DG;
+    const bool row_ok = r < a.R;
+    if (a.lookup) {
+        if (w != 0 || !row_ok) return;  // (no barrier on this path)
+        const int best = min(max(a.idx[(long)r * a.ldi + g], 0), a.K - 1);
+        const float* c = cb + (long)best * DG;
+        float* Y = a.y + (long)r * a.ldy + g * DG;
 #pragma unroll
-        for (int j = 0; j < DG; ++j) x[j] = X[j];
-        float bd = __builtin_inff();
-        for (int k = 0; k < a.K; ++k) {
-            const float* c = cb + (long)k * DG;
-            float d = 0.f;
-#pragma unroll
-            for (int j = 0; j < DG; ++j) {
-                const float t = __fsub_rn(x[j], c[j]);
-                d = __fadd_rn(d, __fmul_rn(t, t));
-            }
-            if (d < bd) {
-                bd = d;
-                best = k;
-            }
-        }
-        a.idx[(long)r * a.ldi + g] = best;
-    } else {
-        best = min(max(a.idx[(long)r * a.ldi + g], 0), a.K - 1);
+        for (int j = 0; j < DG; ++j) Y[j] = c[j];
+        return;
     }
-    const float* c = cb + (long)best * DG;
+    for (int e = threadIdx.x; e < a.K * DG; e += 64 * VQ_WAVES) cbs[e] = cb[e];
+    float x[DG];
+    const float* X = a.x + (long)(row_ok ? r : 0) * a.ldx + g * DG;
+#pragma unroll
+    for (int j = 0; j < DG; ++j) x[j] = X[j];
+    __syncthreads();
+    const int per = (a.K + VQ_WAVES - 1) / VQ_WAVES;
+    const int k0 = w * per, k1 = min(a.K, k0 + per);
+    float bd = __builtin_inff();
+    int best = k0 < k1 ? k0 : 0;
+    for (int k = k0; k < k1; ++k) {
+        const float* c = cbs + k * DG;
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < DG; ++j) {
+            const float t = __fsub_rn(x[j], c[j]);
+            d = __fadd_rn(d, __fmul_rn(t, t));
+        }
+        if (d < bd) {
+            bd = d;
+            best = k;
+        }
+    }
+    float* pd = cbs + a.K * DG;
+    int* pk = reinterpret_cast<int*>(pd + VQ_WAVES * 64);
+    pd[w * 64 + lane] = bd;
+    pk[w * 64 + lane] = best;
+    __syncthreads();
+    if (w != 0 || !row_ok) return;
+    float gd = pd[lane];
+    int gb = pk[lane];
+#pragma unroll
+    for (int q = 1; q < VQ_WAVES; ++q)
+        if (pd[q * 64 + lane] < gd) {
+            gd = pd[q * 64 + lane];
+            gb = pk[q * 64 + lane];
+        }
+    a.idx[(long)r * a.ldi + g] = gb;
+    const float* c = cbs + gb * DG;
     float* Y = a.y + (long)r * a.ldy + g * DG;
 #pragma unroll
     for (int j = 0; j < DG; ++j) Y[j] = c[j];
@@ -115,10 +145,12 @@ extern "C" int stzs_code_quantize(const stzs_vq_args* a, void* stream) {
         return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     dim3 g((a->R + 63) / 64, a->G);
+    const size_t lds = (size_t)a->K * a->dg * 4 + VQ_WAVES * 64 * 8;
+    if (lds > 64 * 1024) return STZS_ESHAPE;  // codebook of one group staged in LDS
     switch (a->dg) {
-        case 4: hipLaunchKernelGGL(vq_kernel<4>, g, dim3(64), 0, s, *a); break;
-        case 8: hipLaunchKernelGGL(vq_kernel<8>, g, dim3(64), 0, s, *a); break;
-        case 16: hipLaunchKernelGGL(vq_kernel<16>, g, dim3(64), 0, s, *a); break;
+        case 4: hipLaunchKernelGGL(vq_kernel<4>, g, dim3(64 * VQ_WAVES), lds, s, *a); break;
+        case 8: hipLaunchKernelGGL(vq_kernel<8>, g, dim3(64 * VQ_WAVES), lds, s, *a); break;
+        case 16: hipLaunchKernelGGL(vq_kernel<16>, g, dim3(64 * VQ_WAVES), lds, s, *a); break;
         default: return STZS_ESHAPE;
     }
     STZS_LAUNCH_CHECK();
