@@ -49,24 +49,41 @@ __global__ __launch_bounds__(256) void attn_mfma(const stzs_attn_args a) {
     }
     bf16_t* P = Ps[wave];
 
-    for (int c0 = 0; c0 < a.Lk; c0 += KC) {
-        __syncthreads();
-        // stage K rows and V^T for keys [c0, c0 + KC)
-        for (int i = tid; i < KC * (DH / 8); i += 256) {
+    // K / V chunk loads run one chunk ahead in registers: chunk c + 1's global loads are in flight while chunk c
+    // is computed (cross-attention: 3 chunks of 64 keys), the LDS images are written from the registers
+    constexpr int NLD = KC * (DH / 8) / 256;  // 16-B K (and V) words per thread per chunk
+    static_assert(KC * (DH / 8) % 256 == 0, "whole chunk per pass");
+    uint4 pk[NLD], pv[NLD];
+    auto load_chunk = [&](int c0) {
+#pragma unroll
+        for (int j = 0; j < NLD; ++j) {
+            const int i = tid + j * 256;
             const int kr = i / (DH / 8), cv = i - kr * (DH / 8);
             const bool ok = c0 + kr < a.Lk;
             const int kk = ok ? c0 + kr : 0;
-            uint4 kv = *reinterpret_cast<const uint4*>(K + (long)kk * a.ldk + cv * 8);
-            uint4 vv = *reinterpret_cast<const uint4*>(V + (long)kk * a.ldv + cv * 8);
-            if (!ok) kv = vv = make_uint4(0, 0, 0, 0);
+            pk[j] = *reinterpret_cast<const uint4*>(K + (long)kk * a.ldk + cv * 8);
+            pv[j] = *reinterpret_cast<const uint4*>(V + (long)kk * a.ldv + cv * 8);
+            if (!ok) pk[j] = pv[j] = make_uint4(0, 0, 0, 0);
+        }
+    };
+    load_chunk(0);
+    for (int c0 = 0; c0 < a.Lk; c0 += KC) {
+        __syncthreads();
+        // stage K rows and V^T for keys [c0, c0 + KC) from the registers, then start the next chunk's loads
+#pragma unroll
+        for (int j = 0; j < NLD; ++j) {
+            const int i = tid + j * 256;
+            const int kr = i / (DH / 8), cv = i - kr * (DH / 8);
+            const uint4 kv = pk[j], vv = pv[j];
             *reinterpret_cast<uint4*>(Ks + kr * KP + cv * 8) = kv;
             const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                Vt[(cv * 8 + 2 * j) * VP + kr] = (bf16_t)(w[j] & 0xFFFF);
-                Vt[(cv * 8 + 2 * j + 1) * VP + kr] = (bf16_t)(w[j] >> 16);
+            for (int q = 0; q < 4; ++q) {
+                Vt[(cv * 8 + 2 * q) * VP + kr] = (bf16_t)(w[q] & 0xFFFF);
+                Vt[(cv * 8 + 2 * q + 1) * VP + kr] = (bf16_t)(w[q] >> 16);
             }
         }
+        if (c0 + KC < a.Lk) load_chunk(c0 + KC);
         __syncthreads();
         // S = Q K^T for 16 queries x 64 keys
         f32x4 s[4];
