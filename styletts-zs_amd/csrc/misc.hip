@@ -65,8 +65,18 @@ __global__ void mean_rows_kernel(const float* x, float* y, int B, int L, long ld
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     if (i >= (long)B * C) return;
     const int b = (int)(i / C), c = (int)(i - (long)b * C);
+    // 8 rows' loads in flight at a time, summed in row order (the serial loop waited on each load in turn)
+    const float* X = x + b * bsx + c0 + c;
     float s = 0.f;
-    for (int l = 0; l < L; ++l) s += x[b * bsx + l * ldx + c0 + c];
+    int l = 0;
+    for (; l + 8 <= L; l += 8) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = X[(long)(l + j) * ldx];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; l < L; ++l) s += X[(long)l * ldx];
     y[b * ldy + c] = s / L;
 }
 

@@ -29,7 +29,21 @@ __global__ __launch_bounds__(256) void chan_stats_partial(const stzs_stats_args 
     const int r0 = chunk * STAT_ROWS, r1 = min(a.T, r0 + STAT_ROWS);
     const T* X = reinterpret_cast<const T*>(a.x) + (long)b * a.bs;
     if (c < a.C) {
-        for (int r = r0 + ty; r < r1; r += 8) {
+        // four rows' 16-B loads in flight per pass, accumulated in row order (same sums as one row at a time)
+        int r = r0 + ty;
+        for (; r + 24 < r1; r += 32) {
+            float v[4][8];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) load8(X + (long)(r + 8 * u) * a.ld + c, v[u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    s[j] += v[u][j];
+                    q[j] += v[u][j] * v[u][j];
+                }
+        }
+        for (; r < r1; r += 8) {
             float v[8];
             load8(X + (long)r * a.ld + c, v);
 #pragma unroll
