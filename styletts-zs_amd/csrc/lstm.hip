@@ -240,7 +240,8 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
                 const long yo = (long)cb * a.bsy + (long)t * a.ldy + dir * H + p * UNITS + cu0;
                 *reinterpret_cast<uint2*>(Y + yo) = hb;
             }
-            __syncthreads();  // gs / As reuse of the next step
+            // no barrier here: the next step writes As only after every wave passed this step's post-MFMA
+            // barrier (its As reads are consumed), and gs only after the next post-staging barrier
             PROF(5)
             continue;
         }
