@@ -496,6 +496,19 @@ def test_harmonic_source_vs_oracle(eng, tiny_params):
     e = max_rel(har, ref)
     print("source", e, rel_err(har, ref))
     assert e < 1e-2
+    # the per-frame phase prefix: the same IEEE fp64 recurrence (acc = frac(acc + hop * (f0 (h + 1) / sr)), one
+    # rounding per operation, fp32 store before each add) restated in numpy -> bit-exact
+    f = F0.double().numpy()
+    want = np.zeros((B, S.harmonic_num + 1, T80), dtype=np.float32)
+    for b in range(B):
+        for hh in range(S.harmonic_num + 1):
+            acc = np.float64(0.0)
+            for k in range(T80):
+                want[b, hh, k] = np.float32(acc)
+                inc = np.float64(f[b, k] * np.float64(hh + 1)) / np.float64(S.sr)
+                acc = acc + np.float64(S.hop) * inc
+                acc = acc - np.floor(acc)
+    assert np.array_equal(pre.cpu().numpy(), want)
 
 
 def test_istft(eng):
