@@ -35,8 +35,17 @@ __global__ __launch_bounds__(256) void dur_kernel(const stzs_dur_args a) {
     if (i >= (long)a.B * a.T) return;
     const int b = (int)(i / a.T), t = (int)(i - (long)b * a.T);
     const float* L = a.logits + (long)b * a.bsl + (long)t * a.ldl;
+    // 8 logits' loads in flight at a time, the sigmoids summed in bin order (as the one-load-at-a-time loop)
     float acc = 0.f;
-    for (int j = 0; j < a.nbins; ++j) acc = __fadd_rn(acc, 1.f / (1.f + expf(-L[j])));
+    int j = 0;
+    for (; j + 8 <= a.nbins; j += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = L[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, 1.f / (1.f + expf(-v[u])));
+    }
+    for (; j < a.nbins; ++j) acc = __fadd_rn(acc, 1.f / (1.f + expf(-L[j])));
     if (a.dsum) a.dsum[i] = acc;
     int d = (int)rintf(acc);
     if (d < 1) d = 1;
