@@ -142,6 +142,16 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * product is ah*bh + ah*bl + al*bh on bf16 MFMA with fp32 accumulation (~fp32 accuracy at ~3x bf16 work).
  * Requires cic = 32; any in/out dtype; the accurate (libm) prologue activations. */
 #define STZS_CONV_W_X3 1024
+/* flags bit: SMALL-M linear on the whole chip (csrc/rows.hip; the batch-1 denoiser linears): bf16 (or fp32, scaled by
+ * pro_cscale and rounded to bf16) x rows, STZS_PACK_KSTEP weights; every workgroup owns 16 output columns, all rows of
+ * a 64/128-row block and 1/Z of K, operands loaded straight into MFMA fragments.  splitk = Z in {0, 1} (off) or any Z
+ * with ci_pad / 32 = 4 Z {1, 2, 4, 8, 16}: the Z slices hand their fp32 partials to the tile's last arriver through
+ * splitk_ws (stzs_conv_rows_workspace bytes) and splitk_ctr (one zeroed uint32 per tile, left zeroed).  Epilogue:
+ * bias, epi_act NONE | GELU, FLAT gate, residual, alpha, beta * acc_in.  The per-element summation order depends on
+ * K and Z only (batch-invariant).  Replaces gemm_glds for 100-row linears whose 8-32 tiles would stream all of K
+ * through 8-32 CUs (SURVEY §8(a) a2 at B = 1). */
+#define STZS_CONV_ROWS 2048
+size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------
@@ -237,6 +247,11 @@ typedef struct stzs_lstm_args {
 #define STZS_STATUS_LSTM_TIMEOUT 1u
 size_t stzs_lstm_workspace(int B, int H, int ndir);
 int stzs_lstm(const stzs_lstm_args* a, void* stream);
+/* zero an LSTM's exchange state -- the 4096-B `sync` block and the granule region at the start of `xchg` (may be
+ * NULL) -- with a tiny kernel of agent-scope atomic stores (graph-replay coherent, unlike a memset node).  For
+ * callers that keep that state in scratch memory shared with other work (the generic stzs_bilstm does this
+ * before every recurrence). */
+int stzs_lstm_state_reset(void* sync, void* xchg, void* stream);
 
 /* ---- predictor glue ---- */
 /* per-token style: linear resample of codes[:, :, c0:c0+Cs] (L_s rows) to T rows (F.interpolate
@@ -451,8 +466,10 @@ int stzs_embed_f32(const int32_t* tok, const float* emb, float* y, int B, int T,
  * composed in native host code (csrc/abi.hip) over the per-kernel entry points above.  Tensors are caller-owned
  * device memory described by (data, dtype, ndim, shape, stride in ELEMENTS); activations are channels-last
  * [B, T, C] with stride[2] == 1 (the row pitch stride[1] may exceed C).  The workspace is caller-owned device
- * memory of at least the queried size (ws_bytes is checked); ops that hold LSTM exchange counters in it require
- * it zero-initialised before the FIRST call and leave those counters zeroed.  Weights are the packed layouts
+ * scratch of at least the queried size (ws_bytes is checked), with no required contents: it may be shared by
+ * consecutive operators on one stream (the ops holding LSTM exchange state in it reset that state on entry).
+ * Aliasing: outputs must not overlap inputs unless an operator says otherwise (cfg_euler_step allows y == x;
+ * mrf_resblock rejects overlap with STZS_EINVAL).  Weights are the packed layouts
  * produced by stzs_pack_conv / stzs_pack_lstm below (host memory; the caller copies them to the device).
  * The denoiser, decoder pre-blocks and F0/N predictor (a2, a9, a8) compose dozens of weight tensors: they are
  * provided as torch operators over the per-kernel entries (stzs/ops.py), not in this generic form.

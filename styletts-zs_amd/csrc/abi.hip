@@ -476,6 +476,8 @@ extern "C" int stzs_bilstm(STZS_GENERIC_ARGS) {
     void* sync = c.take(4096);
     void* xchg = c.take(stzs_lstm_workspace(B, H, 2));
     float* gx = (float*)c.take((size_t)B * T * 8 * H * 4);
+    // the exchange state lives in the caller's (possibly reused, possibly dirtied) scratch: reset it first
+    STZS_CHECK(stzs_lstm_state_reset(sync, xchg, stream));
     stzs_conv_args a = conv_base();
     conv_weights(a, wih, (const float*)bias.data, 8 * H, In, 1, 0, STZS_PACK_KSTEP);
     a.x = x.data;
@@ -597,6 +599,11 @@ extern "C" int stzs_mrf_resblock(STZS_GENERIC_ARGS) {
     const stzs_tensor_t &x = inputs[0], &gb = inputs[1], &yo = outputs[0];
     if (!act3(x, STZS_BF16) || !act3(yo, STZS_BF16) || !gb.data || gb.dtype != STZS_F32) return STZS_EINVAL;
     const int B = (int)x.shape[0], T = (int)x.shape[1];
+    {  // no in-place form: y is written while later resblocks still read x (and its statistics describe x)
+        const char *x0 = (const char*)x.data, *x1 = x0 + ((B - 1) * x.stride[0] + (T - 1) * x.stride[1] + C) * 2;
+        const char *y0 = (const char*)yo.data, *y1 = y0 + ((B - 1) * yo.stride[0] + (T - 1) * yo.stride[1] + C) * 2;
+        if (y0 < x1 && x0 < y1) return STZS_EINVAL;
+    }
     if (x.shape[2] != C || C % 8 || yo.shape[0] != B || yo.shape[1] != T || yo.shape[2] < C || gb.ndim != 2 ||
         gb.shape[0] != B || gb.shape[1] < (int64_t)nk * nd * 4 * C)
         return STZS_ESHAPE;

@@ -6,6 +6,7 @@
 
 int stzs_conv1d_core(const stzs_conv_args* a, void* stream);           // csrc/conv.hip
 int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/mrfv.hip
+int stzs_rows_gemm_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/rows.hip
 
 extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
     if (a && (a->flags & STZS_CONV_W_FRAG32)) {
@@ -21,6 +22,14 @@ extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
         if (a->splitk > 1) return STZS_EINVAL;
         if (a->stat_part && !stzs_aligned(a->stat_part, 8)) return STZS_EINVAL;
         return stzs_mrfv_conv_launch(*a, reinterpret_cast<hipStream_t>(stream));
+    }
+    if (a && (a->flags & STZS_CONV_ROWS)) {
+        if (!a->x || !a->w || !a->y) return STZS_EINVAL;
+        if (a->B <= 0 || a->T_in <= 0 || a->T_out <= 0 || a->Ci <= 0 || a->Co <= 0) return STZS_ESHAPE;
+        if (a->ci_pad < a->Ci || a->co_pad < a->Co || a->co_pad % 128) return STZS_ESHAPE;
+        if (a->ldx % 8 || a->bsx % 8) return STZS_ESHAPE;
+        if (!stzs_aligned(a->x, 16) || !stzs_aligned(a->w, 16)) return STZS_EINVAL;
+        return stzs_rows_gemm_launch(*a, reinterpret_cast<hipStream_t>(stream));
     }
     return stzs_conv1d_core(a, stream);
 }

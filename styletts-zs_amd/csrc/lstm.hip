@@ -302,7 +302,25 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     }
 }
 
+// zero a caller's LSTM state (the 1024 counter / error / done words of `sync` and the granule region at the start
+// of `xchg`) with agent-scope atomic stores -- the same stores the kernel's own tail uses, so the reset is ordered
+// and coherent with the pollers' sc1 loads under graph replay too (a memset node is not, see the kernel's tail)
+__global__ __launch_bounds__(256) void lstm_state_reset(gu32* sync, gu64* gran) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < 1024) __hip_atomic_store(sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gran && i < TAG_BYTES / 8) __hip_atomic_store(gran + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
+
+extern "C" int stzs_lstm_state_reset(void* sync, void* xchg, void* stream) {
+    if (!sync) return STZS_EINVAL;
+    constexpr int n = 1024 > TAG_BYTES / 8 ? 1024 : TAG_BYTES / 8;
+    hipLaunchKernelGGL(lstm_state_reset, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       (gu32*)sync, (gu64*)xchg);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
 
 extern "C" size_t stzs_lstm_workspace(int B, int H, int ndir) {
     const int groups = (B + MROWS - 1) / MROWS;

@@ -24,6 +24,7 @@ CONV_W_F32 = 64  # include/stzs.h STZS_CONV_W_F32 (fp32-MFMA conv_f32)
 CONV_W_X3 = 1024  # include/stzs.h STZS_CONV_W_X3 (precise mode: split-operand bf16x3 conv_x3)
 CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD remap)
 CONV_MRF_PIPE = 512  # include/stzs.h STZS_CONV_MRF_PIPE (k3 residual MRF convs on csrc/mrfp.hip, opt-in)
+CONV_ROWS = 2048  # include/stzs.h STZS_CONV_ROWS (small-M linear on the whole chip, csrc/rows.hip)
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -195,8 +196,10 @@ def params(ints=(), floats=()) -> Params:
 
 # every exported symbol of include/stzs.h (tests check the .so exports exactly these)
 EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_conv_splitk_workspace",
+           "stzs_conv_rows_workspace",
            "stzs_chan_stats_workspace",
-           "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_predictor_prep",
+           "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm",
+           "stzs_lstm_state_reset", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
            "stzs_stft_frames", "stzs_log_mel", "stzs_pool_rows", "stzs_code_quantize",
@@ -227,6 +230,7 @@ def load():
         "stzs_version": ([], i32),
         "stzs_conv1d": ([P(ConvArgs), vp], i32),
         "stzs_conv_splitk_workspace": ([i64, i32, i32], C.c_size_t),
+        "stzs_conv_rows_workspace": ([i64, i32, i32], C.c_size_t),
         "stzs_chan_stats_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
         "stzs_chan_stats_final": ([P(StatsArgs), i32, vp], i32),
@@ -235,6 +239,7 @@ def load():
         "stzs_attention": ([P(AttnArgs), vp], i32),
         "stzs_lstm_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_lstm": ([P(LstmArgs), vp], i32),
+        "stzs_lstm_state_reset": ([vp, vp, vp], i32),
         "stzs_predictor_prep": ([P(PrPrepArgs), vp], i32),
         "stzs_durations": ([P(DurArgs), vp], i32),
         "stzs_alignment": ([P(AlignArgs), vp], i32),

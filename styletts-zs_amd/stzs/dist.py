@@ -1,7 +1,8 @@
 """Multi-GPU plumbing: utterances shard embarrassingly across ranks, one process
-per GPU; the ONLY collective is the initial weight broadcast from rank 0 -- the whole packed arena
+per GPU; the ONLY collectives are the initial broadcasts from rank 0 -- the whole packed arena
 (one contiguous uint8 buffer holding every parameter the engine reads, front end included) in a
-single RCCL broadcast over xGMI.  No collective runs on the synthesis data path.  The same code runs
+single RCCL broadcast over xGMI, and in shared-speaker mode the reference prompt's discrete codes -- plus
+one max-reduction of the timings after the timed region.  No collective runs on the synthesis data path.  The same code runs
 under gloo on CPU (tests/test_dist.py)."""
 from __future__ import annotations
 
@@ -44,6 +45,27 @@ def broadcast_weights(obj, src: int = 0) -> float:
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return (time.perf_counter() - t0) * 1e3
+
+
+def broadcast_prompt_codes(idx, shape, device, src: int = 0) -> torch.Tensor:
+    """Shared-speaker mode ("plus prompt codes (51 KB per speaker)"): the reference prompt is
+    encoded ONCE, on rank `src` (StyleTTSZS.prompt_encode -> its discrete code indices int32 [1, L_s, G]), and
+    every rank receives the indices with one broadcast; each rank then synthesizes with prompt_idx= (the
+    codebook lookup of the same codes), so no rank repeats the front end.  idx: the indices on `src` (ignored
+    elsewhere); -> the indices on every rank (device tensor)."""
+    buf = torch.empty(tuple(shape), dtype=torch.int32, device=device)
+    if dist.get_rank() == src:
+        buf.copy_(idx.reshape(buf.shape))
+    dist.broadcast(buf, src=src)
+    return buf
+
+
+def reduce_max(values, device) -> list:
+    """max over ranks of a few host floats (the timed region's wall seconds): every rank reports the slowest
+    rank's clock.  One small all_reduce, outside every timed region."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
 
 
 def arena_digest(obj) -> str:

@@ -40,15 +40,25 @@ _DT = {torch.float32: L.F32, torch.bfloat16: L.BF16, torch.float8_e4m3fn: L.F8}
 # engine built without dn_splitk: "0" = off, or e.g. "ff2=4,o=2".
 DN_SPLITK = {}
 LATENCY_DN_SPLITK = dict(ff2=4)
+# small-M linears on the whole chip (csrc/rows.hip, STZS_CONV_ROWS): per denoiser linear the number of K slices Z
+# (1 = no split).  The batch-1 latency engine's table; like the split-K table it is a property of the weight applied
+# at every row count (batch-invariant), and it takes precedence over dn_splitk.  STZS_DN_ROWS overrides the default
+# ({}): "0" = off, or e.g. "qkv=1,ff2=4".
+DN_ROWS = {}
+LATENCY_DN_ROWS = dict(inp=1, qkv=1, o=1, q=1, co=1, ff1=1, ff2=4, out=1)
 
 
-def _dn_splitk_default():
-    v = os.environ.get("STZS_DN_SPLITK")
+def _table_env(var, default):
+    v = os.environ.get(var)
     if v is None:
-        return dict(DN_SPLITK)
+        return dict(default)
     if v.strip() in ("", "0"):
         return {}
     return {k: int(n) for k, n in (kv.split("=") for kv in v.split(","))}
+
+
+def _dn_splitk_default():
+    return _table_env("STZS_DN_SPLITK", DN_SPLITK)
 
 
 def _rup(x, m):
@@ -122,7 +132,7 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
-                 packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None):
+                 packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None, dn_rows=None):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
@@ -165,6 +175,9 @@ class StyleTTSZS:
         # split-K of the bf16 denoiser layer linears (stzs_conv_args.splitk): a property of the weight, used at
         # every batch size so results stay batch-invariant; {} turns it off
         self.dn_splitk = _dn_splitk_default() if dn_splitk is None else dict(dn_splitk)
+        # small-M whole-chip form of the bf16 denoiser linears (csrc/rows.hip): {linear: K slices}; a per-engine
+        # property of the weight like dn_splitk (batch-invariant), taking precedence over it
+        self.dn_rows = _table_env("STZS_DN_ROWS", DN_ROWS) if dn_rows is None else dict(dn_rows)
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
@@ -243,7 +256,7 @@ class StyleTTSZS:
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
-             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, splitk=0, what="conv"):
+             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, splitk=0, rows=0, what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
         output fused into the conv epilogue (per-tile partials) + one small finalize launch."""
         W = self.W
@@ -297,6 +310,22 @@ class StyleTTSZS:
         elif getattr(cw, "narrow32", False):
             flags |= L.CONV_W_NARROW32  # narrow conv (csrc/mrf.hip)
         a.flags = flags | self.conv_flags
+        nk = cw.ci_pad // 32
+        if rows > 0 and not (nk % (4 * rows) == 0 and nk // (4 * rows) in (1, 2, 4, 8, 16)):
+            rows = 0  # (a function of K only: batch invariance holds)
+        if (rows > 0 and cw.ks == 1 and stride == 1 and pad == 0 and not cw.ups and pro is None and
+                pro_act == L.ACT_NONE and not cw.f8 and cw.wx3 is None and cw.w32 is None and stats_key is None and
+                (x.t.dtype == torch.float32 or (x.t.dtype == torch.bfloat16 and cscale == 1.0)) and
+                epi_act in (L.ACT_NONE, L.ACT_GELU) and
+                x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
+            # small-M linear on the whole chip (csrc/rows.hip): 16-column tiles x K split in `rows` slices
+            a.flags = (a.flags & ~8) | L.CONV_ROWS
+            a.splitk = rows if rows > 1 else 0
+            if rows > 1:
+                nb = self.lib.stzs_conv_rows_workspace(x.B * x.T, cw.Co, rows)
+                a.splitk_ws = self._scratch("rows_ws", nb // 4 + 1).data_ptr()
+                a.splitk_ctr = self._counters("rows_ctr", nb // (rows * 16)).data_ptr()
+            splitk = 0
         while splitk > 1 and (cw.ci_pad // 32) % splitk:  # a function of K only: batch invariance holds
             splitk //= 2
         if splitk > 1 and (a.flags & 8) and not cw.f8 and cw.wx3 is None and cw.w32 is None:
@@ -699,7 +728,8 @@ class StyleTTSZS:
             s_o = self.buf("dn.o8s", (R * Ls,), torch.float32)
             s_ff = self.buf("dn.ff8s", (R * Ls,), torch.float32)
         co = edm_coeffs(S, st["sig"][i])
-        self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, what="dn.in")
+        rk = {} if (f8 or self.adt == torch.float32) else self.dn_rows
+        self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, rows=rk.get("inp", 0), what="dn.in")
         if f8:
             ain, sin, sfx = an8, s_an, "8"
         else:
@@ -722,26 +752,29 @@ class StyleTTSZS:
         sk = {} if (f8 or self.adt == torch.float32) else self.dn_splitk
         for l, lw in enumerate(W.dn_layers):
             mb = modx[l, i * R].data_ptr()
-            self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, splitk=sk.get("qkv", 0), what="qkv")
+            self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, splitk=sk.get("qkv", 0), rows=rk.get("qkv", 0),
+                      what="qkv")
             self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
             xo, so = (o8, s_o) if f8 else (o, None)
             if f8:
                 self.quant(o, o8, s_o)
             self.conv(lw["o" + sfx], xo, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=so,
-                      post_ln=lns[3 * l + 1], splitk=sk.get("o", 0), what="sa_o")
-            self.conv(lw["q" + sfx], ain, q, x_scale=sin, splitk=sk.get("q", 0), what="ca_q")
+                      post_ln=lns[3 * l + 1], splitk=sk.get("o", 0), rows=rk.get("o", 0), what="sa_o")
+            self.conv(lw["q" + sfx], ain, q, x_scale=sin, splitk=sk.get("q", 0), rows=rk.get("q", 0), what="ca_q")
             self.attention(q, kv[l].sl(0, d), kv[l].sl(d, d), o)
             if f8:
                 self.quant(o, o8, s_o)
             self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=lns[3 * l + 2], splitk=sk.get("co", 0),
-                      what="ca_o")
-            self.conv(lw["ff1" + sfx], ain, ff, epi_act=L.ACT_GELU, x_scale=sin, splitk=sk.get("ff1", 0), what="ff1")
+                      rows=rk.get("co", 0), what="ca_o")
+            self.conv(lw["ff1" + sfx], ain, ff, epi_act=L.ACT_GELU, x_scale=sin, splitk=sk.get("ff1", 0),
+                      rows=rk.get("ff1", 0), what="ff1")
             xf, sf = (ff8, s_ff) if f8 else (ff, None)
             if f8:
                 self.quant(ff, ff8, s_ff)
             self.conv(lw["ff2" + sfx], xf, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=sf,
-                      post_ln=lns[3 * l + 3], splitk=sk.get("ff2", 0), what="ff2")
-        self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], what="dn.out")
+                      post_ln=lns[3 * l + 3], splitk=sk.get("ff2", 0), rows=rk.get("ff2", 0), what="ff2")
+        self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], rows=rk.get("out", 0),
+                  what="dn.out")
 
     def _ln_args(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=0.0, y_scale=None):
         """stzs_rowln_args of a modulated LayerNorm x -> y (launched by stzs_row_layernorm, or fused into a
@@ -1140,7 +1173,9 @@ class StyleTTSZS:
 
     def capture(self, fn):
         """Capture `fn()` into one HIP graph.  fn must be replay-safe: device-resident inputs, cached
-        buffers (a warm-up call on a side stream allocates them), no host syncs.  -> (graph, fn's output)"""
+        buffers (a warm-up call on a side stream allocates them), no host syncs (synth() skips its status
+        check while capturing).  -> (CheckedGraph, fn's output); graph.check() raises after a replay whose LSTM
+        exchange timed out (the captured kernels OR the flag into this engine's status word)."""
         cur = torch.cuda.current_stream(self.device)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(cur)
@@ -1154,14 +1189,26 @@ class StyleTTSZS:
         for k, ent in self._bufs.items():
             if isinstance(k, tuple):
                 ent[3] = True
-        return g, out
+        return CheckedGraph(g, self), out
+
+    def _capturing(self) -> bool:
+        return torch.cuda.is_current_stream_capturing()
 
     def synth(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None, codes=None,
-              n_frames=None, prompt_idx=None):
+              n_frames=None, prompt_idx=None, check=True):
         """tokens int [B, T_txt]; ref_wav fp32 [B|1, N]; noise fp32 [B, L_s, code]; durations int [B, T_txt]
         (host tensor, or device tensor + n_frames: no device sync); seeds: per-utterance source-noise
         seeds; prompt_idx: teacher-forced discrete prompt codes [B|1, L_s, G] (ref_wav then unused).
-        -> dict(wav=[B, 600*T40], prompt_idx=[B|1, L_s, G], ...)"""
+        check: raise RuntimeError if an LSTM exchange of this call timed out (its durations / prosody would be
+        wrong) -- one 4-B device read, skipped while a graph is being captured (CheckedGraph.check() then);
+        check=False leaves it to the caller (check_status(), or the returned `status` word).
+        -> dict(wav=[B, 600*T40], prompt_idx=[B|1, L_s, G], status=int32 [1], ...)"""
+        out = self._synth(tokens, ref_wav, steps, cfg_scale, noise, durations, seeds, codes, n_frames, prompt_idx)
+        if check and not self._capturing():
+            self.check_status()
+        return out
+
+    def _synth(self, tokens, ref_wav, steps, cfg_scale, noise, durations, seeds, codes, n_frames, prompt_idx):
         S = self.spec
         dev = self.device
         tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
@@ -1178,11 +1225,11 @@ class StyleTTSZS:
         pro = self.predict_prosody(h, codes, durations, n_frames)
         seeds = list(range(B)) if seeds is None else seeds
         wav = self.decode(pro, codes, seeds)
-        return dict(wav=wav, codes=codes, h_txt=h, prompt=prompt, prompt_idx=pidx, **pro)
+        return dict(wav=wav, codes=codes, h_txt=h, prompt=prompt, prompt_idx=pidx, status=self.status, **pro)
 
 
     def synth_stream(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None,
-                     codes=None, n_frames=None, chunk_s=1.0, prompt_idx=None):
+                     codes=None, n_frames=None, chunk_s=1.0, prompt_idx=None, check=True):
         """configs[4] long-form synthesis with the streaming iSTFT decoder: the text,
         style, prosody and conv stack run over the whole target (AdaIN instance statistics are
         utterance-global), then the waveform is emitted in `chunk_s`-second chunks.  Yields
@@ -1203,6 +1250,23 @@ class StyleTTSZS:
         post = self.decode(pro, codes, seeds, istft=False)
         frames = max(1, int(round(chunk_s * S.sr / S.istft_hop)))
         yield from self.istft_stream(post, frames)
+        if check and not self._capturing():
+            self.check_status()
+
+
+class CheckedGraph:
+    """a captured HIP graph of one engine + that engine's LSTM status check (StyleTTSZS.capture).  replay()
+    enqueues the graph; check() reads the engine's status word (one 4-B device read, i.e. a sync) and raises if
+    any LSTM exchange of the replays since the last check timed out."""
+
+    def __init__(self, graph, eng):
+        self.graph, self.eng = graph, eng
+
+    def replay(self):
+        self.graph.replay()
+
+    def check(self):
+        return self.eng.check_status()
 
 
 class _OffsetAct(Act):

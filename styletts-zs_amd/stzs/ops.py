@@ -68,7 +68,7 @@ def synth(handle: int, tokens: torch.Tensor, ref_wav: torch.Tensor, noise: torch
           durations: torch.Tensor, steps: int, cfg_scale: float, seeds: List[int]) -> torch.Tensor:
     eng = _eng(handle, tokens, ref_wav, noise)
     out = eng.synth(tokens, ref_wav, steps=steps, cfg_scale=cfg_scale, noise=noise, durations=durations.cpu(),
-                    seeds=list(seeds))
+                    seeds=list(seeds))  # raises on an LSTM exchange timeout (synth's status check)
     return out["wav"].clone()
 
 
@@ -107,6 +107,7 @@ def predict_prosody(handle: int, h_txt: torch.Tensor, codes: torch.Tensor,
     ht[:, :, :D].copy_(h_txt)
     pro = eng.predict_prosody(Act(ht, 0, D), codes.float().contiguous(),
                               durations.cpu() if durations is not None else None)
+    eng.check_status()  # an LSTM exchange timeout makes every output of this call invalid: raise
     return pro["dur"].clone(), pro["idx"].clone(), pro["F0"].contiguous().clone(), pro["N"].contiguous().clone()
 
 
@@ -252,6 +253,12 @@ def _(post, tail, f0, final, n_fft, hop):
 # Activations cross this boundary channels-last, [B, T, C] (the kernels' layout; a torch Conv1d NCT tensor is
 # x.transpose(1, 2)); outputs are fp32 copies.
 
+def _out(view: torch.Tensor) -> torch.Tensor:
+    """an fp32 COPY of an engine buffer view: never the view itself (in fp32 engines `.float()` would return the
+    cached buffer, which the next call of the op overwrites), so outputs never alias engine storage."""
+    return view.to(torch.float32, copy=True)
+
+
 def _act_in(eng, key, x: torch.Tensor, dtype=None):
     """x [B, T, C] -> an engine Act (row pitch padded to 8) holding x in `dtype` (default: the engine's
     activation dtype, fp32 in precise mode)."""
@@ -281,7 +288,8 @@ def bilstm(handle: int, name: str, x: torch.Tensor) -> torch.Tensor:
     xa = _act_in(eng, "lstm.x", x)
     y = eng.act("op.lstm.y", x.shape[0], x.shape[1], 2 * lw.H, eng.adt)
     eng.lstm(lw, xa, y, "op." + name)
-    return y.t[:, :, :2 * lw.H].float()
+    eng.check_status()
+    return _out(y.t[:, :, :2 * lw.H])
 
 
 def _spec(handle):
@@ -318,6 +326,7 @@ def f0n_predictor(handle: int, en: torch.Tensor, codes: torch.Tensor) -> Tuple[t
     """a8: aligned predictor features en [B, T40, pr_in], codes [B, L_s, code] -> (F0, N) fp32 [B, 2 T40]."""
     eng = _eng(handle, en, codes)
     F0, Nn = eng.f0n_predictor(_act_in(eng, "en", en), codes.float().contiguous())
+    eng.check_status()
     return F0.contiguous().clone(), Nn.contiguous().clone()
 
 
@@ -337,7 +346,7 @@ def decoder_pre(handle: int, asr: torch.Tensor, F0: torch.Tensor, N: torch.Tenso
     enc_in.t[:, :, :D].copy_(asr)
     pro = dict(asr_buf=enc_in, F0=F0.float().contiguous(), N=N.float().contiguous(), T40=T40)
     gen_in, _ = eng.decoder_pre(pro, codes.float().contiguous())
-    return gen_in.t[:, :, :S.dec_out].float()
+    return _out(gen_in.t[:, :, :S.dec_out])
 
 
 @register_fake("stzs::decoder_pre")
@@ -351,7 +360,7 @@ def sine_gen(handle: int, F0: torch.Tensor, seeds: List[int]) -> torch.Tensor:
     eng = _eng(handle, F0)
     S = eng.spec
     har = eng.sine_gen(F0.float().contiguous(), list(seeds))
-    return har.t[:, :, :S.har_ch].float()
+    return _out(har.t[:, :, :S.har_ch])
 
 
 @register_fake("stzs::sine_gen")
@@ -371,7 +380,7 @@ def conv_transpose_up(handle: int, x: torch.Tensor, har: torch.Tensor, stage: in
     hb = eng.buf("op.har", (B, Tf, (hc + 31) // 32 * 32), eng.dec_dt, zero=True)
     hb[:, :, :hc].copy_(har)
     xu = eng.upsample(_act_in(eng, "ups.x", x, eng.dec_dt), Act(hb, 0, hc), int(stage))
-    return xu.t[:, :, :S.gen_ch[stage]].float()
+    return _out(xu.t[:, :, :S.gen_ch[stage]])
 
 
 @register_fake("stzs::conv_transpose_up")
@@ -388,7 +397,7 @@ def mrf_resblock(handle: int, x: torch.Tensor, codes: torch.Tensor, stage: int) 
     eng = _eng(handle, x, codes)
     gbd = eng.dec_style(codes.float().contiguous())
     y = eng.mrf(_act_in(eng, "mrf.x", x, eng.dec_dt), int(stage), gbd, eng.W.dec_norm)
-    return y.t[:, :, :x.shape[2]].float()
+    return _out(y.t[:, :, :x.shape[2]])
 
 
 @register_fake("stzs::mrf_resblock")

@@ -66,6 +66,7 @@ class BucketScheduler:
                 dur_ov = torch.stack([reqs[i].durations for i in ch]) if forced else None
                 du = eng.predict_durations(h, codes, dur_ov)
                 tot = du["dur"].to(torch.int64).sum(1).cpu()  # host sync: frame counts decide phase 2
+                eng.check_status()  # a timed-out LSTM exchange would make these durations wrong: raise
                 for j, i in enumerate(ch):
                     per[i] = dict(h=h.t[j].clone(), d=du["d"].t[j].clone(), dur=du["dur"][j].clone(),
                                   codes=codes[j].clone(), T40=int(tot[j]), seed=reqs[i].seed)
@@ -91,6 +92,7 @@ class BucketScheduler:
                 wav = eng.decode(pro, codes, [per[i]["seed"] for i in ch])
                 for j, i in enumerate(ch):
                     out[i] = wav[j].clone()
+        eng.check_status()  # the phase-2 prosody LSTMs
         self.stats = dict(requests=len(reqs), phase1_batches=n1, phase2_batches=n2,
                           frame_buckets=sorted(g2.keys()))
         return out

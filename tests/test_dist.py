@@ -1,5 +1,6 @@
-"""Multi-process path without GPUs (gloo, world_size 2): the weight-arena broadcast (the ONLY
-collective of the design) and the utterance sharding."""
+"""Multi-process path without GPUs (gloo, world_size 2 / 4): the weight-arena broadcast and the shared-speaker
+prompt-code broadcast (the only data collectives of the design), the timed-loop max reduction and
+the utterance sharding."""
 import hashlib
 import os
 import socket
@@ -91,6 +92,44 @@ def test_gloo_bench_rank_setup():
     assert set(r0["seeds"]).isdisjoint(r1["seeds"]) and r0["seeds"] == [0, 1, 2, 3]
     assert r0["tok"] != r1["tok"] and r0["eps"] != r1["eps"]
     assert r0["nframes"] == r1["nframes"]
+
+
+def _speaker_worker(rank, world, port, out):
+    """shared-speaker mode + the timed-loop reduction on CPU tensors: rank 0 holds the prompt's discrete codes
+    (here seeded indices standing in for StyleTTSZS.prompt_encode's), every rank receives them byte for byte;
+    reduce_max returns the slowest rank's clock on every rank (bench.py's max over ranks)."""
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from stzs.dist import broadcast_prompt_codes, reduce_max
+    from stzs.spec import SPEC_V0
+    S = SPEC_V0
+    G = S.code_dim // S.vq_group
+    src = torch.randint(0, S.vq_size, (1, S.L_s, G), generator=torch.Generator().manual_seed(3),
+                        dtype=torch.int32) if rank == 0 else None
+    got = broadcast_prompt_codes(src, (1, S.L_s, G), torch.device("cpu"))
+    mx = reduce_max([1.0 + rank, 10.0 - rank, 0.25 * (rank + 1)], torch.device("cpu"))
+    out[rank] = dict(codes=hashlib.sha256(got.numpy().tobytes()).hexdigest(), shape=tuple(got.shape),
+                     dtype=str(got.dtype), mx=mx,
+                     want=hashlib.sha256(torch.randint(0, S.vq_size, (1, S.L_s, G),
+                                                       generator=torch.Generator().manual_seed(3),
+                                                       dtype=torch.int32).numpy().tobytes()).hexdigest())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_shared_speaker_codes_and_time_reduction(world):
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_speaker_worker, args=(world, port, out), nprocs=world, join=True)
+    rs = [out[r] for r in range(world)]
+    assert all(r["codes"] == rs[0]["want"] for r in rs)  # byte-identical prompt codes on every rank
+    assert all(r["shape"] == rs[0]["shape"] and r["dtype"] == "torch.int32" for r in rs)
+    want = [float(world), 10.0, 0.25 * world]
+    assert all(r["mx"] == want for r in rs)
 
 
 def test_broadcast_weights_accepts_engine_like():

@@ -94,15 +94,20 @@ def test_generic_sine_gen_and_conv_post_istft(eng, tiny, tiny_params):
     assert torch.equal(wav, want)
 
 
-def test_generic_bilstm(eng, tiny, tiny_params):
+@pytest.mark.parametrize("B", [1, 2, 3])
+def test_generic_bilstm(eng, tiny, tiny_params, B):
+    """B 1 / 2 take the tagged-granule exchange, B 3 the counter form.  The LSTM state lives in the caller's scratch:
+    the op resets it on entry, so a workspace dirtied by random bytes and by another operator between calls (the
+    reuse the per-op _workspace queries invite) gives the same bits."""
     S, P, dev = tiny, tiny_params, eng.device
     lib = L.load()
     g = torch.Generator().manual_seed(63)
     In, H = S.pr_in, S.lstm_h
-    x = torch.randn(3, 13, In, generator=g).to(torch.bfloat16).to(dev)
+    x = torch.randn(B, 13, In, generator=g).to(torch.bfloat16).to(dev)
     from stzs.engine import Act
-    y_e = eng.act("t.gen.lstm", 3, 13, 2 * H)
+    y_e = eng.act("t.gen.lstm", B, 13, 2 * H)
     eng.lstm(eng.W.pr_de[0], Act(x), y_e, "t.gen")
+    eng.check_status()
     ih = np.zeros(lib.stzs_pack_conv_size(8 * H, In, 1, 0, L.PACK_KSTEP), np.uint8)
     bias = np.zeros(8 * H, np.float32)
     fr = np.zeros(2 * 4 * H * H * 2, np.uint8)
@@ -110,20 +115,28 @@ def test_generic_bilstm(eng, tiny, tiny_params):
             for n in ("w_ih", "w_hh", "b_ih", "b_hh", "w_ih_rev", "w_hh_rev", "b_ih_rev", "b_hh_rev")]
     assert lib.stzs_pack_lstm(*[a.ctypes.data for a in arrs], In, H, ih.ctypes.data, bias.ctypes.data,
                               fr.ctypes.data) == L.OK
-    y = torch.zeros(3, 13, 2 * H, dtype=torch.bfloat16, device=dev)
+    y = torch.zeros(B, 13, 2 * H, dtype=torch.bfloat16, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     ins = [x, torch.from_numpy(ih).to(dev), torch.from_numpy(bias).to(dev), torch.from_numpy(fr).to(dev)]
     rc, ws = _call("bilstm", ins, [y, status], L.params([H]))
     assert rc == L.OK
     assert torch.equal(y, y_e.t[:, :, :2 * H]) and int(status.item()) == 0
-    # the workspace's counters are left zeroed: a second call on the same workspace agrees
-    lib_ = L.load()
     ti = (L.Tensor * 4)(*[L.tensor(t) for t in ins])
     to = (L.Tensor * 2)(L.tensor(y), L.tensor(status))
-    y.zero_()
-    rc = lib_.stzs_bilstm(ti, 4, to, 2, C.byref(L.params([H])), ws.data_ptr(), ws.numel(),
-                          C.c_void_p(torch.cuda.current_stream().cuda_stream))
-    assert rc == L.OK and torch.equal(y, y_e.t[:, :, :2 * H])
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for dirt in ("none", "random", "other_op"):
+        if dirt == "random":
+            ws.random_(0, 256, generator=torch.Generator(device=dev).manual_seed(5))
+        elif dirt == "other_op":  # another operator's scratch use of the same bytes (its alignment totals)
+            d = torch.randint(1, 4, (B, 600), dtype=torch.int32, device=dev)
+            idx = torch.empty(B, 1200, dtype=torch.int32, device=dev)
+            ti2, to2 = (L.Tensor * 1)(L.tensor(d)), (L.Tensor * 1)(L.tensor(idx))
+            ws.fill_(0x5A)
+            assert lib.stzs_length_regulate(ti2, 1, to2, 1, C.byref(L.params()), ws.data_ptr(), ws.numel(), st) == L.OK
+        y.zero_()
+        rc = lib.stzs_bilstm(ti, 4, to, 2, C.byref(L.params([H])), ws.data_ptr(), ws.numel(), st)
+        assert rc == L.OK and torch.equal(y, y_e.t[:, :, :2 * H]), dirt
+        assert int(status.item()) == 0, dirt
 
 
 @pytest.mark.parametrize("stage", [0, 1])
@@ -196,6 +209,20 @@ def test_generic_mrf_resblock(gpu_device, tiny, tiny_params, spec):
     rc, _ = _call("mrf_resblock", [x, gb] + ins, [y], p)
     assert rc == L.OK
     assert torch.equal(y, want[:, :, :C_])
+
+
+def test_generic_mrf_resblock_rejects_in_place(gpu_device, tiny, tiny_params):
+    """y overlapping x is rejected before any launch (resblocks after the first still read x)."""
+    S = tiny
+    C_ = S.gen_ch[1]
+    x = torch.zeros(1, 64, C_, dtype=torch.bfloat16, device=gpu_device)
+    nk, nd = len(S.rb_kernels), len(S.rb_dils)
+    gb = torch.zeros(1, nk * nd * 4 * C_, device=gpu_device)
+    dummy = torch.zeros(16, device=gpu_device)
+    p = L.params([C_] + list(S.rb_kernels) + list(S.rb_dils) + [nk, nd, L.PACK_KSTEP])
+    ins = [x, gb] + [dummy] * (6 * nk * nd)
+    assert _call("mrf_resblock", ins, [x], p)[0] == L.EINVAL
+    assert _call("mrf_resblock", ins, [x[:, 10:]], p)[0] in (L.EINVAL, L.ESHAPE)
 
 
 def test_generic_rejects_short_workspace(eng):

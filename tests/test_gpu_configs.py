@@ -2,7 +2,8 @@
 dims, against the CPU oracle (oracle/stzs_ref.py).  The inputs are bench.py's own synthetic inputs
 (bench.make_inputs: seeded tokens 16/s, 3-s noise reference, eps, forced [3,2] durations -> 5.000 s).
 
-configs[1] (batch 1, 10-step CFG-5) is checked stage by stage, each GPU stage teacher-forced with the oracle's
+configs[1] (batch 1, 10-step CFG-5) is checked on BOTH engines that run it -- the default one and the batch-1
+latency engine whose p50 bench.py reports (split-K ffn2, LATENCY_DN_SPLITK) -- stage by stage, each GPU stage teacher-forced with the oracle's
 inputs (rounded to bf16 where the GPU stores bf16), then end to end.  configs[2] (batch 64, 2-step CFG-5)
 is checked on sampled rows against the oracle, and every row of the 64-utterance batch must be BIT-IDENTICAL
 to the same utterance synthesized in a smaller batch (no cross-row interference in any kernel), and the
@@ -47,6 +48,19 @@ def v0(gpu_device):
     return SPEC_V0, P, StyleTTSZS(SPEC_V0, P, device=gpu_device)
 
 
+@pytest.fixture(scope="module", params=["throughput", "latency"])
+def c1eng(request, v0):
+    """the configs[1] engines: the default (throughput) engine and the batch-1 LATENCY engine bench.py times for
+    its p50 (same weights, split-K ffn2: stzs/engine.py LATENCY_DN_SPLITK) -- both against the oracle."""
+    from stzs.engine import LATENCY_DN_SPLITK, StyleTTSZS
+    S, P, eng = v0
+    if request.param == "throughput":
+        return eng
+    e = StyleTTSZS(S, None, device=eng.device, packed=eng.W, dn_splitk=LATENCY_DN_SPLITK)
+    assert e.dn_splitk == {"ff2": 4}
+    return e
+
+
 def _act(eng, h):
     from stzs.engine import Act
     t = torch.zeros(*h.shape, dtype=torch.bfloat16, device=eng.device)
@@ -67,10 +81,11 @@ def _dur_guarded_equal(d_gpu, dsum_gpu, d_ref, dsum_ref):
     return bool(((d_gpu == d_ref) | tie).all()), err, int(tie.sum())
 
 
-def test_configs1_stagewise(v0):
+def test_configs1_stagewise(v0, c1eng):
     """configs[1]: batch 1, 5-s target, 10-step sampling, CFG 5 -- each stage teacher-forced."""
     from oracle import stzs_ref as R
-    S, P, eng = v0
+    S, P, _ = v0
+    eng = c1eng
     tok, ref, eps, dur = bench.make_inputs(S, 1, seed=1000)
     dev = eng.device
     # text encoder (CNN + BiLSTM)
@@ -100,7 +115,7 @@ def test_configs1_stagewise(v0):
     wav = eng.decode(dict(asr_buf=enc_in, F0=pr["F0"].to(dev), N=pr["N"].to(dev), T40=T40), codes_ref.to(dev),
                      seeds).cpu()
     e_dec, m_dec = rel_err(wav, wav_ref), _logmel_l1(wav, wav_ref, S)
-    print(f"configs[1] stagewise: text {e_text:.3e} sampler {e_samp:.3e} F0 {e_f0:.3e} N {e_n:.3e} "
+    print(f"configs[1] stagewise ({eng.dn_splitk or 'no split-K'}): text {e_text:.3e} sampler {e_samp:.3e} F0 {e_f0:.3e} N {e_n:.3e} "
           f"dsum err {derr:.3e} (ties {nties}) decoder wav {e_dec:.3e} log-mel L1 {m_dec:.3e}")
     assert e_text < TOL_TEXT
     assert e_samp < TOL_SAMPLER
@@ -108,10 +123,11 @@ def test_configs1_stagewise(v0):
     assert e_dec < TOL_DEC_WAV and m_dec < TOL_DEC_MEL
 
 
-def test_configs1_end_to_end(v0):
+def test_configs1_end_to_end(v0, c1eng):
     """configs[1] whole synth() vs the oracle teacher-forced only at the discrete prompt codes."""
     from oracle import stzs_ref as R
-    S, P, eng = v0
+    S, P, _ = v0
+    eng = c1eng
     tok, ref, eps, dur = bench.make_inputs(S, 1, seed=1000)
     out = eng.synth(tok, ref, steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG, noise=eps, durations=dur, seeds=[7])
     gidx = out["prompt_idx"].cpu()
@@ -120,7 +136,7 @@ def test_configs1_end_to_end(v0):
     flips = int((gidx != oidx).sum())
     e_c, e_f0 = rel_err(out["codes"].cpu(), o["codes"]), rel_err(out["F0"].cpu(), o["F0"])
     e_w, m_w = rel_err(out["wav"].cpu(), o["wav"]), _logmel_l1(out["wav"].cpu(), o["wav"], S)
-    print(f"configs[1] e2e: prompt-code flips {flips}/{gidx.numel()} (min margin of flips "
+    print(f"configs[1] e2e ({eng.dn_splitk or 'no split-K'}): prompt-code flips {flips}/{gidx.numel()} (min margin of flips "
           f"{margin[gidx != oidx].min().item() if flips else float('nan'):.2e}) codes {e_c:.3e} F0 {e_f0:.3e} "
           f"wav {e_w:.3e} log-mel L1 {m_w:.3e}")
     assert out["wav"].shape == o["wav"].shape == (1, bench.TARGET_S * S.sr)

@@ -249,3 +249,29 @@ def test_precise_end_to_end_mel_l1(v0_precise, case):
     print(f"precise e2e {case}: text {e_h:.2e} codes {e_c:.2e} F0 {e_f0:.2e} wav {e_w:.2e} log-mel L1 {m_w:.3e}")
     assert torch.equal(out["dur"].cpu(), o["dur"].to(out["dur"].dtype))
     assert m_w <= 1e-3
+
+
+def test_precise_batch64_rows(v0_precise):
+    """the bench's precise leg exactly (bench.precise_mode: B = 64, make_inputs(S, 64, 7), 2-step CFG 5, seeds 0..63):
+    rows 0 / 31 / 63 of the 64-utterance batch are BIT-IDENTICAL to the same utterances synthesized alone (the
+    multi-row hi | lo LSTM exchange, the flat-row split-operand GEMM tiles and the per-utterance statistics keep rows
+    independent), and row 31 meets the north-star log-mel L1 <= 1e-3 against the fp32 oracle."""
+    import bench
+    from oracle import stzs_ref as R
+    S, P, eng = v0_precise
+    Bb = 64
+    tok, ref, eps, dur = bench.make_inputs(S, Bb, 7)
+    out = eng.synth(tok, ref, steps=bench.STEPS_THROUGHPUT, cfg_scale=bench.CFG, noise=eps, durations=dur,
+                    seeds=list(range(Bb)))
+    keep = {k: out[k].detach().clone().cpu() for k in ("wav", "codes", "F0", "prompt_idx")}
+    for r in (0, 31, 63):
+        o1 = eng.synth(tok[r:r + 1], ref[r:r + 1], steps=bench.STEPS_THROUGHPUT, cfg_scale=bench.CFG,
+                       noise=eps[r:r + 1], durations=dur[r:r + 1], seeds=[r])
+        for k in ("prompt_idx", "codes", "F0", "wav"):
+            assert torch.equal(o1[k].cpu(), keep[k][r:r + 1]), (r, k)
+    r = 31
+    o = R.synth(P, S, tok[r:r + 1], ref[r:r + 1], bench.STEPS_THROUGHPUT, bench.CFG, eps[r:r + 1], dur[r:r + 1],
+                seeds=[r], prompt_idx=keep["prompt_idx"][r:r + 1])
+    m_w = _logmel_l1(keep["wav"][r:r + 1], o["wav"], S)
+    print(f"precise B=64 row {r}: codes {rel_err(keep['codes'][r:r + 1], o['codes']):.2e} log-mel L1 {m_w:.3e}")
+    assert m_w <= 1e-3

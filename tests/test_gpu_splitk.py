@@ -127,7 +127,8 @@ def test_denoiser_splitk_vs_unsplit(gpu_device):
     the same function up to fp32 re-association of the K sums.  Those ~1e-7 differences flip the bf16 rounding of
     a few activations, which the 10 CFG-5 Euler steps amplify to the size of the bf16 path's own error: measured
     4.6e-3 rel-L2 on the codes (the bf16 sampler vs the fp32 oracle: 4.0e-3, test_gpu_configs.py TOL_SAMPLER
-    1e-2), so the bound is that tolerance; the stage-wise oracle tests run with split-K on."""
+    1e-2), so the bound is that tolerance.  The split engine ITSELF is also checked against the fp32 oracle, stage-wise
+    and end to end at configs[1] (tests/test_gpu_configs.py, the `latency` engine of the c1eng fixture)."""
     from stzs.engine import LATENCY_DN_SPLITK, StyleTTSZS
     from stzs.params import init_params
     from stzs.spec import SPEC_V0

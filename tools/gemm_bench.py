@@ -20,6 +20,8 @@ M = int(os.environ.get("M", 6400))
 FLAGS = [int(f, 0) for f in os.environ.get("FLAGS", "0,2,4").split(",")]
 F8 = os.environ.get("F8", "0") == "1"
 SKS = [int(v) for v in os.environ.get("SK", "0").split(",")]  # split-K counts (stzs_conv_args.splitk)
+# ROWS="0,1,2,4": 0 = the LDS-DMA GEMM (gemm_glds), Z >= 1 = the small-M form (csrc/rows.hip) with K in Z slices
+ROWS = [int(v) for v in os.environ.get("ROWS", "0").split(",")]
 cases = [("ffn1 gelu", 512, 2048, torch.bfloat16, L.ACT_GELU, False), ("qkv", 512, 1536, torch.bfloat16, L.ACT_NONE, False),
          ("out gated f32", 512, 512, torch.float32, L.ACT_NONE, True), ("ffn2 gated f32", 2048, 512, torch.float32, L.ACT_NONE, True)]
 for name, K, N, odt, act, gated in cases:
@@ -39,10 +41,10 @@ for name, K, N, odt, act, gated in cases:
     res = Act(torch.zeros(M // 50, 50, N, device="cuda:0", dtype=odt)) if gated else None
     gate = torch.ones(M // 50, N, device="cuda:0")
     flops = 2.0 * M * N * K
-    for flags, sk in [(f, k) for f in FLAGS for k in SKS]:
+    for flags, sk, rz in [(f, k, z) for f in FLAGS for k in SKS for z in ROWS]:
         def run():
             eng.conv(cw, x, y, epi_act=act, res=res, gate=gate.data_ptr() if gated else None, gate_bs=N, flags=flags,
-                     x_scale=xs, splitk=sk)
+                     x_scale=xs, splitk=sk, rows=rz)
         def run20():
             for _ in range(20):
                 run()
@@ -55,5 +57,5 @@ for name, K, N, odt, act, gated in cases:
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 20 * 1e3
-        print(f"{name:16s} {'fp8' if F8 else 'bf16'} M={M} K={K} N={N} flags={flags} splitk={sk}: {us:7.1f} us  "
+        print(f"{name:16s} {'fp8' if F8 else 'bf16'} M={M} K={K} N={N} flags={flags} splitk={sk} rows={rz}: {us:7.1f} us  "
               f"{flops / us / 1e6:7.1f} TF/s", flush=True)
