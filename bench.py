@@ -218,7 +218,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from stzs.engine import LATENCY_DN_SPLITK, StyleTTSZS
+    from stzs.engine import LATENCY_DN_ROWS, LATENCY_DN_SPLITK, StyleTTSZS, latency_engine
     from stzs.params import init_params
     from stzs.spec import SPEC_V0
     S = SPEC_V0
@@ -384,8 +384,9 @@ def main():
     lat = None
     if not args.no_latency:
         tok1, ref1, eps1, dur1 = (t.to(dev) for t in make_inputs(S, 1, seed=1000 + rank))
-        # the batch-1 serving engine: same packed weights, split-K ffn2 (stzs/engine.py LATENCY_DN_SPLITK)
-        elat = StyleTTSZS(S, None, device=dev, packed=W, dn_splitk=LATENCY_DN_SPLITK)
+        # the batch-1 serving engine: same packed weights, whole-chip small-M denoiser linears (stzs/engine.py
+        # latency_engine: LATENCY_DN_ROWS, LATENCY_DN_SPLITK)
+        elat = latency_engine(S, W, dev)
 
         def one():
             return elat.synth(tok1, ref1, steps=STEPS_LATENCY, cfg_scale=CFG, noise=eps1, durations=dur1, seeds=[7],
@@ -409,7 +410,7 @@ def main():
         lstm_timeouts += int(int(elat.status.item()) != 0)
         lat = dict(p50_ms=round(float(np.percentile(ts, 50)), 3), p90_ms=round(float(np.percentile(ts, 90)), 3),
                    config="batch 1, 10-step sampling, CFG 5, 5-s target, 3-s reference",
-                   dn_splitk=dict(LATENCY_DN_SPLITK))
+                   dn_splitk=dict(LATENCY_DN_SPLITK), dn_rows=dict(LATENCY_DN_ROWS))
 
     # ---- configs[4]: 30-s target, batch 1, fp8 denoiser linears, streaming iSTFT (1-s chunks) ----
     lf = None

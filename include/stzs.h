@@ -471,8 +471,8 @@ int stzs_embed_f32(const int32_t* tok, const float* emb, float* y, int B, int T,
  * Aliasing: outputs must not overlap inputs unless an operator says otherwise (cfg_euler_step allows y == x;
  * mrf_resblock rejects overlap with STZS_EINVAL).  Weights are the packed layouts
  * produced by stzs_pack_conv / stzs_pack_lstm below (host memory; the caller copies them to the device).
- * The denoiser, decoder pre-blocks and F0/N predictor (a2, a9, a8) compose dozens of weight tensors: they are
- * provided as torch operators over the per-kernel entries (stzs/ops.py), not in this generic form.
+ * The denoiser, decoder pre-blocks and F0/N predictor (a2, a9, a8) compose dozens of weight tensors: their input
+ * lists follow the STZS_DN_* / STZS_DP_* / STZS_FN_* enums at the end of this header.
  * ====================================================================================================== */
 typedef struct stzs_tensor_t {
     void* data;
@@ -552,6 +552,64 @@ size_t stzs_conv_transpose_up_workspace(const stzs_tensor_t* inputs, int n_in, c
 int stzs_mrf_resblock(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out,
                       const stzs_params_t* p, void* workspace, size_t ws_bytes, void* stream);
 size_t stzs_mrf_resblock_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+
+/* ---- composite operators (csrc/abi_ops.hip): the engine's launch sequences in native host code, bit-identical to
+ * stzs/engine.py; bf16 activations (the precise mode stays on the Python engine).  Inputs in the enum order below;
+ * "w" = a packed STZS_PACK_KSTEP linear (AdaIN-block k3 convs: STZS_PACK_LANE16 when Ci > 64 and Co % 16 == 0),
+ * "b" = its fp32 bias.  Workspace: the operator's own query (a dry pass of the same code). */
+
+/* a2 denoiser_fwd: ONE EDM-preconditioned denoiser evaluation D(x, sigma) = c_skip x + c_out F(c_in x, sigma) with
+ *     classifier-free-guidance rows: in {x f32 [R, L_s, code] (R = 2B with cfg: conditional rows, then null-prompt
+ *     rows), h_txt bf16 [B, T, d_txt], prompt f32 [B, L_s, code], then the weights below} -> out {D f32 [R, L_s, code]};
+ *     i[0] = cfg, i[1] = layers, i[2] = heads, i[3] = d, i[4] = ffn width, i[5] = Fourier features (<= 256);
+ *     f[0] = sigma, f[1] = sigma_data.  (stzs/engine.py denoiser_prepare + denoiser_step) */
+enum {
+    STZS_DN_X = 0, STZS_DN_HTXT, STZS_DN_PROMPT,
+    STZS_DN_IN_W, STZS_DN_IN_B, STZS_DN_POS /* f32 [L_s, d] */,
+    STZS_DN_T0_W, STZS_DN_T0_B, STZS_DN_T1_W, STZS_DN_T1_B,
+    STZS_DN_POOL_W, STZS_DN_POOL_B, STZS_DN_CTX_TXT_W, STZS_DN_CTX_TXT_B, STZS_DN_CTX_PRM_W, STZS_DN_CTX_PRM_B,
+    STZS_DN_ADA_W, STZS_DN_ADA_B, STZS_DN_ADA_TABLE /* f32 [layers, 6d] */, STZS_DN_FINAL_ADA_W, STZS_DN_FINAL_ADA_B,
+    STZS_DN_OUT_W, STZS_DN_OUT_B,
+    STZS_DN_CTX_NULL /* bf16 [L_s, d]: null-prompt context rows (cfg) */, STZS_DN_POOL_NULL /* f32 [d] (cfg) */,
+    STZS_DN_NIN_BASE /* then per layer l, at STZS_DN_NIN_BASE + STZS_DN_PER_LAYER * l: */
+};
+enum {
+    STZS_DN_L_QKV_W = 0, STZS_DN_L_QKV_B, STZS_DN_L_O_W, STZS_DN_L_O_B, STZS_DN_L_Q_W, STZS_DN_L_Q_B,
+    STZS_DN_L_KV_W, STZS_DN_L_KV_B, STZS_DN_L_CO_W, STZS_DN_L_CO_B, STZS_DN_L_FF1_W, STZS_DN_L_FF1_B,
+    STZS_DN_L_FF2_W, STZS_DN_L_FF2_B, STZS_DN_L_LN_G /* f32 [d] */, STZS_DN_L_LN_B, STZS_DN_PER_LAYER
+};
+int stzs_denoiser_fwd(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out, const stzs_params_t* p,
+                      void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_denoiser_fwd_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+
+/* a9 decoder_pre: in {asr bf16 [B, T40, d_txt] (aligned text features), F0 f32 [B, T80], N f32 [B, T80] (same row
+ *     stride), codes f32 [B, L_s, code], F0 conv f32 [4] (w0 w1 w2 bias), N conv f32 [4], asr_res w, b, AdaIN norm
+ *     group w [total x style_ac], b, then 5 blocks (encode, decode0..3) x 7: conv1 w, conv1 b, conv2 w, conv2 b,
+ *     sc w (data NULL when din == dout), pool w f32 [din x 3], pool b f32 [din] (decode3 only, else NULL)} ->
+ *     out {generator input bf16 [B, T80, >= dec_out]}; i[0] = dec_enc, i[1] = dec_asr_res, i[2] = dec_out,
+ *     i[3] = style_ac (acoustic code channels pooled for AdaIN), i[4] = columns of the norm group (its first ones:
+ *     norm1 | norm2 gamma-beta of the 5 blocks in order).  (stzs/engine.py decoder_pre) */
+enum {
+    STZS_DP_ASR = 0, STZS_DP_F0, STZS_DP_N, STZS_DP_CODES, STZS_DP_F0CONV, STZS_DP_NCONV, STZS_DP_ASR_RES_W,
+    STZS_DP_ASR_RES_B, STZS_DP_NORM_W, STZS_DP_NORM_B, STZS_DP_BLK0, STZS_DP_NIN = STZS_DP_BLK0 + 35
+};
+int stzs_decoder_pre(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out, const stzs_params_t* p,
+                     void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_decoder_pre_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
+
+/* a8 f0n_predictor: in {en bf16 [B, T40, pr_in] (aligned predictor features), codes f32 [B, L_s, code], shared BiLSTM
+ *     (stzs_pack_lstm: ih packed, ih bias, W_hh^T fragments), AdaIN norm group w [total x style_pr], b, then per
+ *     branch (F0, N) 3 blocks x 7 tensors (as decoder_pre; block 1 up-samples x2) + projection w, b (Co = 1)} ->
+ *     out {F0 f32 [B, T80], N f32 [B, T80] (, status i32 [1]: OR-ed STZS_STATUS_LSTM_TIMEOUT)}; i[0] = LSTM hidden H,
+ *     i[1..3] = branch widths c0, c1, c2, i[4] = first prosodic code channel, i[5] = prosodic channels, i[6] = norm
+ *     group columns.  (stzs/engine.py f0n_predictor) */
+enum {
+    STZS_FN_EN = 0, STZS_FN_CODES, STZS_FN_LSTM_IH, STZS_FN_LSTM_BIAS, STZS_FN_LSTM_WHH, STZS_FN_NORM_W, STZS_FN_NORM_B,
+    STZS_FN_BR0, STZS_FN_PER_BRANCH = 23, STZS_FN_NIN = STZS_FN_BR0 + 2 * 23
+};
+int stzs_f0n_predictor(const stzs_tensor_t* inputs, int n_in, stzs_tensor_t* outputs, int n_out, const stzs_params_t* p,
+                       void* workspace, size_t ws_bytes, void* stream);
+size_t stzs_f0n_predictor_workspace(const stzs_tensor_t* inputs, int n_in, const stzs_params_t* p);
 
 #ifdef __cplusplus
 }

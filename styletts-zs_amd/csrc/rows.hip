@@ -71,53 +71,61 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
     __shared__ __attribute__((aligned(16))) float4 red[4][MT][64];
     __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ct = blockIdx.x;                 // 16-column tile
-    const long r0 = (long)blockIdx.y * (16 * MT);  // row block
+    const int ct = blockIdx.x;               // 16-column tile
+    const int r0 = blockIdx.y * (16 * MT);   // row block
     const int z = blockIdx.z, Z = gridDim.z;
-    const long nR = (long)a.B * a.T_in;
+    const int T = a.T_in, nR = a.B * T;
     const int NK = a.ci_pad / 32;
     const int NKZ = NK / Z;
     const int kbase = z * NKZ + wave;  // this wave's K-steps: kbase + 4 j, j < KPW
-    // ---- epilogue operands first (their latency hides under the K loop) ----
-    // slot (mt, lane) holds rows r0 + mt*16 + (lane>>4)*4 + i (i < 4) of column n = ct*16 + (lane & 15); thread
-    // tid owns slots tid + 256 s
+    // flat row R -> (utterance, step): q = trunc(R * (1 / T)) is within one of R / T for R < 2^22, one
+    // correction step makes it exact (a handful of VALU ops instead of hipcc's integer-division expansion)
+    const float invT = 1.f / (float)T;
+    auto bdiv = [&](int R) -> int {
+        int q = (int)((float)R * invT);
+        const int r = R - q * T;
+        q += r < 0 ? -1 : (r >= T ? 1 : 0);
+        return q;
+    };
+    auto roff = [&](int R, int64_t ld, int64_t bs) -> int64_t {
+        R = R < nR ? R : nR - 1;
+        const int bb = bdiv(R);
+        return (int64_t)bb * bs + (int64_t)(R - bb * T) * ld;
+    };
+    // ---- epilogue operands first: UNCONDITIONAL loads from valid addresses (an absent operand reads a stand-in and
+    // is dropped by a select), so hipcc keeps them in flight under the K loop instead of draining each one ----
+    // slot (mt, lane) holds rows r0 + mt*16 + (lane>>4)*4 + i (i < 4) of column n = ct*16 + (lane & 15); thread tid
+    // owns slots tid + 256 s
     constexpr int NSLOT = (MT * 64 + NTHR - 1) / NTHR;
     const int n = ct * 16 + (lane & 15);
     const bool col_ok = n < a.Co;
     const int nc = col_ok ? n : a.Co - 1;
-    const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
-    const TOut* AI = reinterpret_cast<const TOut*>(a.acc_in);
-    float res_v[NSLOT][4], ai_v[NSLOT][4];
-    const float bias = a.bias ? a.bias[nc] : 0.f;
+    const bool hr = a.res != nullptr, ha = a.acc_in != nullptr, hg = a.gate != nullptr, hb = a.bias != nullptr;
+    const TOut* Rp = reinterpret_cast<const TOut*>(hr ? a.res : a.y);
+    const TOut* AI = reinterpret_cast<const TOut*>(ha ? a.acc_in : a.y);
+    const int64_t ldr = hr ? a.ldr : a.ldy, bsr = hr ? a.bsr : a.bsy, lda = ha ? a.lda : a.ldy, bsa = ha ? a.bsa : a.bsy;
+    const float* stand_in = reinterpret_cast<const float*>(a.w);  // >= 64 B per output column: index nc is valid
+    const float braw = (hb ? a.bias : stand_in)[nc];
+    float res_v[NSLOT][4], ai_v[NSLOT][4], g_v[NSLOT][4];
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
-        const int slot = tid + s * NTHR;
-        const int mt = slot >> 6;
+        const int mt = ((tid + s * NTHR) >> 6) % MT;  // slots past MT*64 (none for MT 4 / 8) alias valid rows
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            res_v[s][i] = 0.f;
-            ai_v[s][i] = 0.f;
-            long R = r0 + mt * 16 + (lane >> 4) * 4 + i;
-            R = R < nR ? R : nR - 1;
-            const long bb = R / a.T_in, t = R - bb * a.T_in;
-            if (slot < MT * 64) {
-                if (Rp) res_v[s][i] = DT<TOut>::ld(Rp + bb * a.bsr + t * a.ldr + nc);
-                if (AI) ai_v[s][i] = DT<TOut>::ld(AI + bb * a.bsa + t * a.lda + nc);
-            }
+            const int R = r0 + mt * 16 + (lane >> 4) * 4 + i;
+            res_v[s][i] = DT<TOut>::ld(Rp + roff(R, ldr, bsr) + nc);
+            ai_v[s][i] = DT<TOut>::ld(AI + roff(R, lda, bsa) + nc);
+            const int Rc = R < nR ? R : nR - 1;
+            g_v[s][i] = (hg ? a.gate : stand_in)[hg ? (int64_t)bdiv(Rc) * a.gate_bs + nc : (int64_t)nc];
         }
     }
     // ---- operand addresses ----
     const TIn* X = reinterpret_cast<const TIn*>(a.x);
-    long aoff[MT];
+    int64_t aoff[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        long R = r0 + mt * 16 + (lane & 15);
-        R = R < nR ? R : nR - 1;
-        const long bb = R / a.T_in;
-        aoff[mt] = bb * a.bsx + (R - bb * a.T_in) * a.ldx + 8 * (lane >> 4);
-    }
+    for (int mt = 0; mt < MT; ++mt) aoff[mt] = roff(r0 + mt * 16 + (lane & 15), a.ldx, a.bsx) + 8 * (lane >> 4);
     const int cot = ct >> 3, rr = (ct & 7) * 16 + (lane & 15);
-    const unsigned char* Wb = reinterpret_cast<const unsigned char*>(a.w) + ((long)cot * NK * 128 + rr) * 64 +
+    const unsigned char* Wb = reinterpret_cast<const unsigned char*>(a.w) + ((int64_t)cot * NK * 128 + rr) * 64 +
                               (((lane >> 4) ^ gswz(rr)) << 4);
     const float sc = a.pro_cscale;
     constexpr int RING = sizeof(TIn) == 2 ? 4 : 2;  // K-steps per wave whose loads are in flight
@@ -127,7 +135,7 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
     auto issue = [&](int j) {
         const int k = kbase + 4 * j;
         const int slot = j % RING;
-        br[slot] = *reinterpret_cast<const uint4*>(Wb + (long)k * 128 * 64);
+        br[slot] = *reinterpret_cast<const uint4*>(Wb + (int64_t)k * 128 * 64);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) ar[slot][mt] = AFrag<TIn>::load(X + aoff[mt] + k * 32);
     };
@@ -136,6 +144,9 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < (KPW < RING ? KPW : RING); ++j) issue(j);
+    // keep every issued load ahead of the first MFMA (hipcc otherwise interleaves them to save registers, leaving
+    // only a few loads in flight per wave)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < KPW; ++j) {
         const int slot = j % RING;
@@ -143,7 +154,10 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
         bf16x8 fa[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) fa[mt] = AFrag<TIn>::cvt(ar[slot][mt], sc);
-        if (j + RING < KPW) issue(j + RING);
+        if (j + RING < KPW) {
+            issue(j + RING);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb, acc[mt], 0, 0, 0);
     }
@@ -164,9 +178,9 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
     }
     if constexpr (SPLIT) {
         // in-launch split-K hand-off: slab [tile][z][slot] f32x4, write-through stores, drain, barrier, ticket
-        const long tile = (long)blockIdx.y * gridDim.x + ct;
+        const int64_t tile = (int64_t)blockIdx.y * gridDim.x + ct;
         const int SLAB = MT * 64 * 16;
-        unsigned char* base = reinterpret_cast<unsigned char*>(a.splitk_ws) + tile * (long)Z * SLAB;
+        unsigned char* base = reinterpret_cast<unsigned char*>(a.splitk_ws) + tile * (int64_t)Z * SLAB;
         const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(base, 0, Z * SLAB, 0x00020000);
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) {
@@ -188,17 +202,18 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
         for (int s = 0; s < NSLOT; ++s) {
             const int slot = tid + s * NTHR;
             if (slot < MT * 64) {
-                f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
-                for (int q = 0; q < Z; ++q) {  // every slab (its own too) by sc1 loads, summed in slice order
-                    const f32x4 p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, q * SLAB + slot * 16, 0, 16));
-                    t = q == 0 ? p : t + p;
-                }
+                u32x4 pv[16];
+                for (int q = 0; q < Z; ++q)  // every slab (its own too) by sc1 loads, all in flight
+                    pv[q] = __builtin_amdgcn_raw_buffer_load_b128(wr, q * SLAB + slot * 16, 0, 16);
+                f32x4 t = __builtin_bit_cast(f32x4, pv[0]);
+                for (int q = 1; q < Z; ++q) t += __builtin_bit_cast(f32x4, pv[q]);  // slice order
                 v[s] = t;
             }
         }
     }
     // ---- fused epilogue ----
     TOut* Y = reinterpret_cast<TOut*>(a.y);
+    const float bias = hb ? braw : 0.f;
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
         const int slot = tid + s * NTHR;
@@ -206,15 +221,14 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
         const int mt = slot >> 6;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const long R = r0 + mt * 16 + (lane >> 4) * 4 + i;
+            const int R = r0 + mt * 16 + (lane >> 4) * 4 + i;
             if (R >= nR) break;
-            const long bb = R / a.T_in, t = R - bb * a.T_in;
             float x = epi_act<EACT>(v[s][i] + bias, a.epi_slope);
-            if (a.gate) x *= a.gate[bb * a.gate_bs + n];
-            if (Rp) x += res_v[s][i];
+            x = hg ? x * g_v[s][i] : x;
+            x = hr ? x + res_v[s][i] : x;
             x *= a.alpha;
-            if (AI) x += a.beta * ai_v[s][i];
-            DT<TOut>::st(Y + bb * a.bsy + t * a.ldy + n, x);
+            x = ha ? x + a.beta * ai_v[s][i] : x;
+            DT<TOut>::st(Y + roff(R, a.ldy, a.bsy) + n, x);
         }
     }
 }
@@ -273,7 +287,7 @@ int stzs_rows_gemm_launch(const stzs_conv_args& a, hipStream_t s) {
     if (a.in_dtype == STZS_BF16 ? a.pro_cscale != 1.f : false) return STZS_EINVAL;
     const int NK = a.ci_pad / 32;
     const int Z = a.splitk > 1 ? a.splitk : 1;
-    if (a.ci_pad % 32 || NK % (4 * Z)) return STZS_ESHAPE;  // every wave of every slice runs the same K-step count
+    if (a.ci_pad % 32 || NK % (4 * Z) || Z > 16) return STZS_ESHAPE;  // every wave of every slice runs the same K-step count
     const int kpw = NK / (4 * Z);
     if (kpw != 1 && kpw != 2 && kpw != 4 && kpw != 8 && kpw != 16) return STZS_ESHAPE;
     if (Z > 1 && (!a.splitk_ws || !a.splitk_ctr || !stzs_aligned(a.splitk_ws, 16) || !stzs_aligned(a.splitk_ctr, 4)))

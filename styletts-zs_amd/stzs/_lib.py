@@ -167,7 +167,11 @@ class Params(C.Structure):
 
 PACK_KSTEP, PACK_LANE16, PACK_FRAG32, PACK_NARROW32, PACK_X3 = 0, 1, 2, 3, 4
 GENERIC_OPS = ["cfg_euler_step", "duration_head", "length_regulate", "sine_gen", "conv_post_istft", "bilstm",
-               "conv_transpose_up", "mrf_resblock"]
+               "conv_transpose_up", "mrf_resblock", "denoiser_fwd", "decoder_pre", "f0n_predictor"]
+# input-list layouts of the composite generic operators (include/stzs.h STZS_DN_* / STZS_DP_* / STZS_FN_*)
+DN_NIN_BASE, DN_PER_LAYER = 25, 16
+DP_BLK0, DP_NIN = 10, 45
+FN_BR0, FN_PER_BRANCH, FN_NIN = 7, 23, 53
 
 
 def tensor(t, dtype=None) -> Tensor:

@@ -1254,6 +1254,13 @@ class StyleTTSZS:
             self.check_status()
 
 
+def latency_engine(spec: Spec, packed: PackedModel, device="cuda:0") -> "StyleTTSZS":
+    """the batch-1 serving engine bench.py times for the configs[1] p50 (and tests/test_gpu_configs.py checks against
+    the oracle): the same packed weights, the denoiser layer linears on the whole-chip small-M form
+    (LATENCY_DN_ROWS, csrc/rows.hip) and split-K ffn2 wherever the rows form does not apply (LATENCY_DN_SPLITK)."""
+    return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS)
+
+
 class CheckedGraph:
     """a captured HIP graph of one engine + that engine's LSTM status check (StyleTTSZS.capture).  replay()
     enqueues the graph; check() reads the engine's status word (one 4-B device read, i.e. a sync) and raises if

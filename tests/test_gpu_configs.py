@@ -3,7 +3,7 @@ dims, against the CPU oracle (oracle/stzs_ref.py).  The inputs are bench.py's ow
 (bench.make_inputs: seeded tokens 16/s, 3-s noise reference, eps, forced [3,2] durations -> 5.000 s).
 
 configs[1] (batch 1, 10-step CFG-5) is checked on BOTH engines that run it -- the default one and the batch-1
-latency engine whose p50 bench.py reports (split-K ffn2, LATENCY_DN_SPLITK) -- stage by stage, each GPU stage teacher-forced with the oracle's
+latency engine whose p50 bench.py reports (stzs/engine.py latency_engine) -- stage by stage, each GPU stage teacher-forced with the oracle's
 inputs (rounded to bf16 where the GPU stores bf16), then end to end.  configs[2] (batch 64, 2-step CFG-5)
 is checked on sampled rows against the oracle, and every row of the 64-utterance batch must be BIT-IDENTICAL
 to the same utterance synthesized in a smaller batch (no cross-row interference in any kernel), and the
@@ -51,13 +51,13 @@ def v0(gpu_device):
 @pytest.fixture(scope="module", params=["throughput", "latency"])
 def c1eng(request, v0):
     """the configs[1] engines: the default (throughput) engine and the batch-1 LATENCY engine bench.py times for
-    its p50 (same weights, split-K ffn2: stzs/engine.py LATENCY_DN_SPLITK) -- both against the oracle."""
-    from stzs.engine import LATENCY_DN_SPLITK, StyleTTSZS
+    its p50 (stzs/engine.py latency_engine: whole-chip small-M denoiser linears + split-K) -- both against the oracle."""
+    from stzs.engine import LATENCY_DN_ROWS, latency_engine
     S, P, eng = v0
     if request.param == "throughput":
         return eng
-    e = StyleTTSZS(S, None, device=eng.device, packed=eng.W, dn_splitk=LATENCY_DN_SPLITK)
-    assert e.dn_splitk == {"ff2": 4}
+    e = latency_engine(S, eng.W, eng.device)
+    assert e.dn_rows == LATENCY_DN_ROWS and e.dn_rows
     return e
 
 
@@ -115,7 +115,7 @@ def test_configs1_stagewise(v0, c1eng):
     wav = eng.decode(dict(asr_buf=enc_in, F0=pr["F0"].to(dev), N=pr["N"].to(dev), T40=T40), codes_ref.to(dev),
                      seeds).cpu()
     e_dec, m_dec = rel_err(wav, wav_ref), _logmel_l1(wav, wav_ref, S)
-    print(f"configs[1] stagewise ({eng.dn_splitk or 'no split-K'}): text {e_text:.3e} sampler {e_samp:.3e} F0 {e_f0:.3e} N {e_n:.3e} "
+    print(f"configs[1] stagewise ({'latency engine' if eng.dn_rows else 'throughput engine'}): text {e_text:.3e} sampler {e_samp:.3e} F0 {e_f0:.3e} N {e_n:.3e} "
           f"dsum err {derr:.3e} (ties {nties}) decoder wav {e_dec:.3e} log-mel L1 {m_dec:.3e}")
     assert e_text < TOL_TEXT
     assert e_samp < TOL_SAMPLER
@@ -136,7 +136,7 @@ def test_configs1_end_to_end(v0, c1eng):
     flips = int((gidx != oidx).sum())
     e_c, e_f0 = rel_err(out["codes"].cpu(), o["codes"]), rel_err(out["F0"].cpu(), o["F0"])
     e_w, m_w = rel_err(out["wav"].cpu(), o["wav"]), _logmel_l1(out["wav"].cpu(), o["wav"], S)
-    print(f"configs[1] e2e ({eng.dn_splitk or 'no split-K'}): prompt-code flips {flips}/{gidx.numel()} (min margin of flips "
+    print(f"configs[1] e2e ({'latency engine' if eng.dn_rows else 'throughput engine'}): prompt-code flips {flips}/{gidx.numel()} (min margin of flips "
           f"{margin[gidx != oidx].min().item() if flips else float('nan'):.2e}) codes {e_c:.3e} F0 {e_f0:.3e} "
           f"wav {e_w:.3e} log-mel L1 {m_w:.3e}")
     assert out["wav"].shape == o["wav"].shape == (1, bench.TARGET_S * S.sr)
@@ -251,3 +251,20 @@ def test_two_shard_streams_match_eager(v0, c2, branch_streams):
         cur.wait_stream(s)
     conc_ok = check("concurrent")
     assert seq_ok and conc_ok
+
+
+def test_latency_engine_batch_invariant(v0):
+    """the latency engine (whole-chip small-M denoiser linears, split-K) keeps utterances independent: three
+    utterances synthesized as one batch == each synthesized alone, bit for bit (the K structure of every linear is a
+    property of the weight, never of the row count; batch 1 takes the tagged LSTM exchange, batch 3 the counter form)."""
+    from stzs.engine import latency_engine
+    S, P, eng = v0
+    e = latency_engine(S, eng.W, eng.device)
+    tok, ref, eps, dur, seeds = bench.rank_inputs(S, 3, 5)
+    kw = dict(steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG)
+    out = e.synth(tok, ref, noise=eps, durations=dur, seeds=seeds, **kw)
+    keep = {k: out[k].detach().clone().cpu() for k in ("codes", "F0", "wav")}
+    for i in range(3):
+        o1 = e.synth(tok[i:i + 1], ref[i:i + 1], noise=eps[i:i + 1], durations=dur[i:i + 1], seeds=[seeds[i]], **kw)
+        for k in ("codes", "F0", "wav"):
+            assert torch.equal(o1[k].cpu(), keep[k][i:i + 1]), (i, k)
