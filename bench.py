@@ -46,6 +46,7 @@ B_THROUGHPUT = 64
 STEPS_THROUGHPUT = 2
 CFG = 5.0
 STEPS_LATENCY = 10
+CHUNK_HALO = 10   # configs[4] chunked decoder: aligned frames of context each side of a 1-s chunk
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 PEAK_HBM_GBS = 8000.0
 
@@ -133,31 +134,37 @@ def longform(S, P, dev, runs=7):
     eps = torch.randn(1, S.L_s, S.code_dim, generator=g).to(dev)
     dur = torch.tensor([[3, 2] * (T // 2)], dtype=torch.int32).to(dev)
     nf = int(40 * 30)
-    first, total = [], []
-    for i in range(runs + 1):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        n = 0
-        for j, (_, w) in enumerate(e8.synth_stream(tok, ref, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps,
-                                                   durations=dur, seeds=[3], n_frames=nf, chunk_s=1.0,
-                                                   check=False)):
-            if j == 0:
-                torch.cuda.synchronize()
-                t1 = time.perf_counter()
-            n += w.shape[1]
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        assert n == 30 * S.sr
-        if i:
-            first.append((t1 - t0) * 1e3)
-            total.append((t2 - t0) * 1e3)
+
+    def timed(halo):
+        first, total = [], []
+        for i in range(runs + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n = 0
+            for j, (_, w) in enumerate(e8.synth_stream(tok, ref, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps,
+                                                       durations=dur, seeds=[3], n_frames=nf, chunk_s=1.0,
+                                                       check=False, chunked_halo=halo)):
+                if j == 0:
+                    torch.cuda.synchronize()
+                    t1 = time.perf_counter()
+                n += w.shape[1]
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            assert n == 30 * S.sr
+            if i:
+                first.append((t1 - t0) * 1e3)
+                total.append((t2 - t0) * 1e3)
+        return round(float(np.percentile(first, 50)), 3), round(float(np.percentile(total, 50)), 3)
+    f_w, t_w = timed(None)
+    f_c, t_c = timed(CHUNK_HALO)
     lstm_to = int(int(e8.status.item()) != 0)
     del e8
     return dict(lstm_timeouts=lstm_to, config="configs[4]: batch 1, 30-s target, 2-step CFG-5, fp8 e4m3 denoiser linears, "
                        "streaming iSTFT in 1-s chunks, eager", audio_s=30.0,
-                p50_first_chunk_ms=round(float(np.percentile(first, 50)), 3),
-                p50_total_ms=round(float(np.percentile(total, 50)), 3),
-                realtime_factor=round(30.0 / (float(np.percentile(total, 50)) * 1e-3), 1))
+                p50_first_chunk_ms=f_w, p50_total_ms=t_w, realtime_factor=round(30.0 / (t_w * 1e-3), 1),
+                chunked=dict(halo_frames=CHUNK_HALO, p50_first_chunk_ms=f_c, p50_total_ms=t_c,
+                             note="chunked decoder (engine.decode_chunked): 1-s chunks decoded over +-halo windows with "
+                                  "window-local statistics; parity vs oracle decode_chunked (tests/test_gpu_stream.py)"))
 
 
 def precise_mode(S, P, dev, B=64, steps=5):

@@ -88,8 +88,10 @@ struct Ctx {
     explicit Ctx(void* ws, bool dry_, void* s) : cv(dry_ ? nullptr : ws), dry(dry_), stream(s) {}
     void* take(size_t n) { return cv.take(n); }
     float* f32(size_t n) { return (float*)take(n * 4); }
-    // a zeroed channels-last buffer [B, T, rup(C, 8)] (zeroed: kernels read padding channels of some of them)
-    int act(Act& a, int B, int T, int C, int dt, bool zero = true) {
+    // a channels-last buffer [B, T, rup(C, 8)]; zeroed when it has padding channels (a conv's 16-B staging reads a
+    // partly valid 8-channel vector whole and weights it by zero-padded weights: garbage there would be NaN * 0)
+    // or when the caller asks (buffers only partly written by their producers)
+    int act(Act& a, int B, int T, int C, int dt, bool zero = false) {
         a = Act();
         a.B = B;
         a.T = T;
@@ -99,7 +101,7 @@ struct Ctx {
         a.bs = (int64_t)T * a.ld;
         const size_t n = (size_t)B * a.bs * esz(dt);
         a.base = (char*)take(n);
-        if (!dry && zero && hipMemsetAsync(a.base, 0, n, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+        if (!dry && (zero || a.ld != C) && hipMemsetAsync(a.base, 0, n, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
             return STZS_EHIP;
         return STZS_OK;
     }
@@ -253,12 +255,12 @@ int blk(Ctx& c, const BlkIn& bw, const Act& x, const Act& out, const float* gb, 
     CK(stats(c, x, s1));
     const int To = bw.up ? 2 * T : T;
     Act r;
-    CK(c.act(r, B, To, bw.dout, dt, false));
+    CK(c.act(r, B, To, bw.dout, dt));
     const CW c1{&bw.t[0], &bw.t[1], bw.dout, bw.din, 3, blk_form(bw.dout, bw.din)};
     const CW c2{&bw.t[2], &bw.t[3], bw.dout, bw.dout, 3, blk_form(bw.dout, bw.dout)};
     if (bw.up) {
         Act u;
-        CK(c.act(u, B, To, bw.din, dt, false));
+        CK(c.act(u, B, To, bw.din, dt));
         if (!c.dry) {
             stzs_dwup_args d;
             memset(&d, 0, sizeof d);
@@ -300,7 +302,7 @@ int blk(Ctx& c, const BlkIn& bw, const Act& x, const Act& out, const float* gb, 
     Act res = x;
     if (bw.t[4].data) {
         Act scb;
-        CK(c.act(scb, B, T, bw.dout, dt, false));
+        CK(c.act(scb, B, T, bw.dout, dt));
         CK(conv(c, CW{&bw.t[4], nullptr, bw.dout, bw.din, 1, STZS_PACK_KSTEP}, x, scb));
         res = scb;
     }
@@ -322,7 +324,7 @@ int bilstm(Ctx& c, const Act& x, const stzs_tensor_t& wih, const stzs_tensor_t& 
     void* sync = c.take(4096);
     void* xchg = c.take(stzs_lstm_workspace(x.B, H, 2));
     Act gx;
-    CK(c.act(gx, x.B, x.T, 8 * H, STZS_F32, false));
+    CK(c.act(gx, x.B, x.T, 8 * H, STZS_F32));
     CK(conv(c, CW{&wih, &bias, 8 * H, x.C, 1, STZS_PACK_KSTEP}, x, gx));
     if (c.dry) return STZS_OK;
     CK(stzs_lstm_state_reset(sync, xchg, c.stream));
@@ -400,7 +402,7 @@ int denoiser(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int 
     auto W = [&](int wi, int Co, int Ci) { return CW{&in[wi], &in[wi + 1], Co, Ci, 1, STZS_PACK_KSTEP}; };
     // ---- step-invariant context (denoiser_prepare, one sigma) ----
     Act ctx;
-    CK(c.act(ctx, R, Lc, d, STZS_BF16));
+    CK(c.act(ctx, R, Lc, d, STZS_BF16, true));
     Act ht = act_of(Ht);
     auto rows_of = [&](const Act& base, int b0, int nb, int t0, int C) {  // rows [t0, ...) of utterances [b0, b0 + nb)
         Act y = base;
@@ -453,7 +455,7 @@ int denoiser(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int 
     Act kv[16];
     if (NL > 16) return STZS_ESHAPE;
     for (int l = 0; l < NL; ++l) {
-        CK(c.act(kv[l], R, Lc, 2 * d, STZS_BF16, false));
+        CK(c.act(kv[l], R, Lc, 2 * d, STZS_BF16));
         CK(conv(c, W(STZS_DN_NIN_BASE + STZS_DN_PER_LAYER * l + STZS_DN_L_KV_W, 2 * d, d), ctx, kv[l]));
     }
     // sigma embedding: EDM c_noise = log(sigma) / 4 -> Fourier features -> MLP (SiLU) -> temb
@@ -461,9 +463,9 @@ int denoiser(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int 
     const double c_in = 1.0 / sqrt(sg * sg + (double)sd * sd), c_skip = (double)sd * sd / (sg * sg + (double)sd * sd),
                  c_out = sg * sd / sqrt(sg * sg + (double)sd * sd), c_noise = log(sg) / 4.0;
     Act four, t0, temb;
-    CK(c.act(four, 1, 1, nf, STZS_F32, false));
-    CK(c.act(t0, 1, 1, d, STZS_F32, false));
-    CK(c.act(temb, 1, 1, d, STZS_F32, false));
+    CK(c.act(four, 1, 1, nf, STZS_F32));
+    CK(c.act(t0, 1, 1, d, STZS_F32));
+    CK(c.act(temb, 1, 1, d, STZS_F32));
     if (!c.dry) {
         Four f;
         const int half = nf / 2;
@@ -484,9 +486,9 @@ int denoiser(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int 
         CK(conv(c, W(STZS_DN_T1_W, d, d), t0, temb));
     }
     Act cb, mod, fmod;
-    CK(c.act(cb, R, 1, d, STZS_BF16, false));
-    CK(c.act(mod, R, 1, 6 * d, STZS_F32, false));
-    CK(c.act(fmod, R, 1, 2 * d, STZS_F32, false));
+    CK(c.act(cb, R, 1, d, STZS_BF16));
+    CK(c.act(mod, R, 1, 6 * d, STZS_F32));
+    CK(c.act(fmod, R, 1, 2 * d, STZS_F32));
     float* modx = c.f32((size_t)NL * R * 6 * d);
     float* fmodx = c.f32((size_t)R * 2 * d);
     if (!c.dry) CK(stzs_dn_cond_steps(pool, (const float*)temb.ptr(), cb.ptr(), R, d, 1, c.stream));
@@ -502,12 +504,12 @@ int denoiser(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int 
     }
     // ---- one NFE (denoiser_step) ----
     Act h, an, qkv, o, q, ff;
-    CK(c.act(h, R, Ls, d, STZS_F32, false));
-    CK(c.act(an, R, Ls, d, STZS_BF16, false));
-    CK(c.act(qkv, R, Ls, 3 * d, STZS_BF16, false));
-    CK(c.act(o, R, Ls, d, STZS_BF16, false));
-    CK(c.act(q, R, Ls, d, STZS_BF16, false));
-    CK(c.act(ff, R, Ls, ffn, STZS_BF16, false));
+    CK(c.act(h, R, Ls, d, STZS_F32));
+    CK(c.act(an, R, Ls, d, STZS_BF16));
+    CK(c.act(qkv, R, Ls, 3 * d, STZS_BF16));
+    CK(c.act(o, R, Ls, d, STZS_BF16));
+    CK(c.act(q, R, Ls, d, STZS_BF16));
+    CK(c.act(ff, R, Ls, ffn, STZS_BF16));
     Act xa;
     xa.base = (char*)X.data;
     xa.B = R;
@@ -655,11 +657,11 @@ int decoder_pre(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, i
     float* gb;
     CK(norm_gb(c, in[STZS_DP_NORM_W], in[STZS_DP_NORM_B], sa, B, sty, total, gb));
     Act enc;
-    CK(c.act(enc, B, T40, dtx + 2, STZS_BF16));
+    CK(c.act(enc, B, T40, dtx + 2, STZS_BF16, true));
     CK(copy2d(c, Asr.data, Asr.stride[1], Asr.stride[0], STZS_BF16, enc.ptr(), enc.ld, enc.bs, STZS_BF16, B, T40, dtx));
     Act cats[2];
-    CK(c.act(cats[0], B, T40, dcat, STZS_BF16));
-    CK(c.act(cats[1], B, T40, dcat, STZS_BF16));
+    CK(c.act(cats[0], B, T40, dcat, STZS_BF16, true));
+    CK(c.act(cats[1], B, T40, dcat, STZS_BF16, true));
     const int cF = denc + dres, cN = cF + 1;
     for (int j = 0; j < 2; ++j) {
         if (!c.dry) {
@@ -720,7 +722,7 @@ int f0n(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int n_out
     uint32_t* status = (n_out > 2 && out[2].data) ? (uint32_t*)out[2].data : nullptr;
     const int hid = 2 * H;
     Act xs;
-    CK(c.act(xs, B, T40, hid, STZS_BF16, false));
+    CK(c.act(xs, B, T40, hid, STZS_BF16));
     CK(bilstm(c, act_of(En), in[STZS_FN_LSTM_IH], in[STZS_FN_LSTM_BIAS], in[STZS_FN_LSTM_WHH], H, xs, status));
     float* sg;
     CK(mean_rows(c, Cd, sc0, spr, sg));
@@ -731,9 +733,9 @@ int f0n(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int n_out
     for (int br = 0; br < 2; ++br) {
         const stzs_tensor_t* bt = in + STZS_FN_BR0 + STZS_FN_PER_BRANCH * br;
         Act y[3];
-        CK(c.act(y[0], B, T40, c0, STZS_BF16, false));
-        CK(c.act(y[1], B, T80, c1, STZS_BF16, false));
-        CK(c.act(y[2], B, T80, c2, STZS_BF16, false));
+        CK(c.act(y[0], B, T40, c0, STZS_BF16));
+        CK(c.act(y[1], B, T80, c1, STZS_BF16));
+        CK(c.act(y[2], B, T80, c2, STZS_BF16));
         Act x = xs;
         for (int j = 0; j < 3; ++j) {
             const int off1 = o_, off2 = o_ + 2 * din_[j];

@@ -354,9 +354,11 @@ void (*pick(int ks, bool one, bool al))(stzs_conv_args) {
 }  // namespace
 
 int stzs_mrfp_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrfp.hip (1: not applicable)
+int stzs_ups_conv_launch(const stzs_conv_args& a, hipStream_t s);   // csrc/ups.hip (polyphase ConvTranspose)
 
 // internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32 weights
 __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s) {
+    if (a.ups > 0) return stzs_ups_conv_launch(a, s);
     const int rows_in = BT + (a.ks - 1) * a.dil;
     if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || rows_in > 16 * (a.ks == 3 ? sb_rows(3) : a.ks == 7 ? sb_rows(7) : SB_MAX) ||
         a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.gate || a.epi_act != STZS_ACT_NONE || a.ups ||

@@ -1069,12 +1069,13 @@ class StyleTTSZS:
         self._call(self.lib.stzs_istft, a, "istft")
         return wav
 
-    def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None, istft=True):
+    def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None, istft=True, har: Act = None):
         """a10-a13: harmonic source, per stage the noise conv + ConvTranspose up-sampling and the MRF, then
-        conv_post and the iSTFT."""
+        conv_post and the iSTFT.  har: precomputed harmonic-source features (the chunked decoder's window slice)."""
         S, W = self.spec, self.W
         ng = W.dec_norm
-        har = self.sine_gen(F0, seeds)
+        if har is None:
+            har = self.sine_gen(F0, seeds)
         if trace is not None:
             trace["har"] = har
         for i in range(len(S.up_rates)):
@@ -1090,6 +1091,59 @@ class StyleTTSZS:
         if not istft:
             return post
         return self.istft(post)
+
+    def _istft_chunk(self, rows_ptr, ldp, bsp, B, f0, Fc, fin, wav, tails, i):
+        """one streaming-iSTFT launch: conv_post frames [f0, f0 + Fc) at rows_ptr (row pitch ldp, batch stride bsp,
+        fp32) -> samples [n0, n1) of wav [B, Nout], the 3-frame tail carried in the ping-pong buffers.  -> (n0, n1)"""
+        S = self.spec
+        n0, n1 = C.c_int64(), C.c_int64()
+        halo = self.lib.stzs_istft_stream_span(f0, Fc, fin, S.n_fft, S.istft_hop, C.byref(n0), C.byref(n1))
+        L.check(min(halo, 0), "istft_stream_span")
+        assert halo <= 8
+        a = L.IstftStreamArgs()
+        a.post = rows_ptr
+        a.tail_in = tails[i % 2].data_ptr() if f0 > 0 else None
+        a.tail_out = tails[(i + 1) % 2].data_ptr() if not fin else None
+        a.wav = wav.data_ptr() + n0.value * 4
+        a.ldp, a.bsp, a.bsw, a.ldt = ldp, bsp, wav.shape[1], tails[0].shape[2]
+        a.B, a.f0, a.Fc, a.final_chunk, a.n_fft, a.hop_s = B, f0, Fc, fin, S.n_fft, S.istft_hop
+        self._call(self.lib.stzs_istft_stream, a, "istft_stream")
+        return n0.value, n1.value
+
+    def decode_chunked(self, pro: dict, codes: torch.Tensor, seeds, chunk: int, halo: int):
+        """configs[4] CHUNKED streaming decoder (oracle/stzs_ref.py decode_chunked): each chunk of `chunk` aligned
+        frames is decoded over its window of +-`halo` frames -- pre-blocks and generator on the window alone, AdaIN with
+        WINDOW-local InstanceNorm statistics -- on the slice of the whole utterance's harmonic-source features (global
+        phase prefix and noise counters); its own conv_post frames go through the streaming iSTFT with the carried
+        tail.  The first chunk's audio is ready after one window's decode instead of the whole utterance's.
+        Yields (first_sample, wav chunk [B, n]) views of one [B, 600 T40] buffer."""
+        S = self.spec
+        enc_in, F0, Nn, T40 = pro["asr_buf"], pro["F0"], pro["N"], pro["T40"]
+        B = enc_in.B
+        fpf = S.frame40 // S.istft_hop
+        har = self.sine_gen(F0, seeds)
+        Nout = T40 * S.frame40
+        wav = self.buf("gen.wav_chunked", (B, Nout), torch.float32)
+        ncol = _rup(S.n_fft + 2, 4)
+        tails = [self.buf("gen.ctail0", (B, 8, ncol), torch.float32), self.buf("gen.ctail1", (B, 8, ncol), torch.float32)]
+        dt = self.dec_dt
+        for i, a0 in enumerate(range(0, T40, chunk)):
+            b0 = min(a0 + chunk, T40)
+            wa, wb = max(0, a0 - halo), min(T40, b0 + halo)
+            n = wb - wa
+            enc_w = self.act("dec.enc_in_w", B, n, S.d_txt + 2, dt)
+            self.copy2d(Act(enc_in.t[:, wa:wb], 0, S.d_txt), enc_w, n, S.d_txt, bsx=enc_in.bs)
+            Tfw = fpf * n + 1
+            har_w = Act(self.buf("gen.har_w", (B, Tfw, har.ld), dt, zero=True), 0, S.har_ch)
+            self.copy2d(Act(har.t[:, fpf * wa:fpf * wb + 1], 0, S.har_ch), har_w, Tfw, S.har_ch, bsx=har.bs)
+            F0w, Nw = F0[:, 2 * wa:2 * wb], Nn[:, 2 * wa:2 * wb]
+            gen_in, gbd = self.decoder_pre(dict(asr_buf=enc_w, F0=F0w, N=Nw, T40=n), codes)
+            post = self.generator(gen_in, F0w, seeds, gbd, istft=False, har=har_w)
+            fin = int(b0 == T40)
+            r0 = fpf * (a0 - wa)
+            n0, n1 = self._istft_chunk(post.ptr + r0 * post.ld * 4, post.ld, post.bs, B, fpf * a0,
+                                       fpf * (b0 - a0) + fin, fin, wav, tails, i)
+            yield n0, wav[:, n0:n1]
 
     def istft_stream(self, post: Act, chunk_frames: int):
         """iSTFT of conv_post frames [B, Tf, 22] in chunks of `chunk_frames` frames,
@@ -1229,11 +1283,14 @@ class StyleTTSZS:
 
 
     def synth_stream(self, tokens, ref_wav, steps=2, cfg_scale=1.0, noise=None, durations=None, seeds=None,
-                     codes=None, n_frames=None, chunk_s=1.0, prompt_idx=None, check=True):
+                     codes=None, n_frames=None, chunk_s=1.0, prompt_idx=None, check=True, chunked_halo=None):
         """configs[4] long-form synthesis with the streaming iSTFT decoder: the text,
         style, prosody and conv stack run over the whole target (AdaIN instance statistics are
         utterance-global), then the waveform is emitted in `chunk_s`-second chunks.  Yields
-        (first_sample, wav_chunk [B, n]) device views; their concatenation equals synth()["wav"]."""
+        (first_sample, wav_chunk [B, n]) device views; their concatenation equals synth()["wav"].
+        chunked_halo=H: the CHUNKED decoder instead (decode_chunked: every `chunk_s` chunk decoded over a window of
+        +-H aligned frames with window-local statistics -- a different function, parity vs oracle decode_chunked):
+        the first chunk is ready after the front and one window's decode."""
         S = self.spec
         dev = self.device
         tokens = tokens.to(dev, torch.int32) if tokens.device != dev or tokens.dtype != torch.int32 else tokens
@@ -1247,9 +1304,13 @@ class StyleTTSZS:
             codes = self.sample_style(h, prompt, noise.to(dev, torch.float32), steps, cfg_scale)
         pro = self.predict_prosody(h, codes, durations, n_frames)
         seeds = list(range(B)) if seeds is None else seeds
-        post = self.decode(pro, codes, seeds, istft=False)
-        frames = max(1, int(round(chunk_s * S.sr / S.istft_hop)))
-        yield from self.istft_stream(post, frames)
+        if chunked_halo is not None:  # the chunked decoder: chunk-local statistics, first audio after one window
+            yield from self.decode_chunked(pro, codes, seeds, max(1, int(round(chunk_s * S.sr / S.frame40))),
+                                           int(chunked_halo))
+        else:
+            post = self.decode(pro, codes, seeds, istft=False)
+            frames = max(1, int(round(chunk_s * S.sr / S.istft_hop)))
+            yield from self.istft_stream(post, frames)
         if check and not self._capturing():
             self.check_status()
 

@@ -208,12 +208,13 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
         wn = A.add(name + ".wpk", narrow32_stream(wp[:, :32], cic).to(torch.bfloat16))
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
         return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True, w32=w32, wx3=wx3)
-    if frag32:
-        assert not ups and cic == 128 and Co % 8 == 0 and ks in (3, 7, 11), (name, Ci, Co, ks)
+    if frag32:  # register-direct MRF convs (csrc/mrfv.hip) and the polyphase ConvTranspose (csrc/ups.hip, ups > 0)
+        assert cic == 128 and ((not ups and Co % 8 == 0 and ks in (3, 7, 11)) or (ups and Co % 32 == 0)), \
+            (name, Ci, Co, ks, ups)
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, frag32_perm()].reshape(ks, co_pad, ci_pad)
         wn = A.add(name + ".wfr", frag32_stream(wp).to(torch.bfloat16))
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, 0, False, w32=w32, frag32=True, wx3=wx3)
+        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, w32=w32, frag32=True, wx3=wx3)
     if lane16:
         assert cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
@@ -456,8 +457,11 @@ class PackedModel:
             self.noise_conv.append(pack_conv(A, f"gen.noise_conv{i}", P[f"gen.noise_conv{i}.w"], P[f"gen.noise_conv{i}.b"],
                                              x3=xd))
             wu = P[f"gen.ups{i}.w"]  # ConvTranspose1d [Ci, Co, 2r]
+            # 128-channel input chunks, Co % 32 == 0: the input-staged-once polyphase kernel (csrc/ups.hip)
             self.ups.append(pack_conv(A, f"gen.ups{i}", wu, P[f"gen.ups{i}.b"], ups=r,
-                                      lane16=wu.shape[0] > 64 and wu.shape[1] % 16 == 0, x3=xd))
+                                      frag32=wu.shape[0] > 64 and wu.shape[1] % 32 == 0,
+                                      lane16=wu.shape[0] > 64 and wu.shape[1] % 16 == 0 and wu.shape[1] % 32 != 0,
+                                      x3=xd))
             stage = []
             for j, kr in enumerate(S.rb_kernels):
                 res = []

@@ -229,3 +229,206 @@ def test_generic_rejects_short_workspace(eng):
     x = torch.zeros(2, 30, dtype=torch.int32, device=eng.device)
     idx = torch.zeros(2, 60, dtype=torch.int32, device=eng.device)
     assert _call("length_regulate", [x], [idx], L.params(), ws_bytes=4)[0] == L.ESHAPE
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# composite operators (csrc/abi_ops.hip): a2 denoiser_fwd, a9 decoder_pre, a8 f0n_predictor.  Weights either from the
+# C++ packers applied to the torch parameters (tiny spec: the path a non-Python host takes) or from the engine's
+# packed arena (v0; the packers are bit-identical to it, tests/test_abi_generic.py).  Both must reproduce the engine
+# path BIT FOR BIT (same kernels, same arguments, same order).
+
+def _none_tensor():
+    return L.Tensor()  # data NULL: an absent optional tensor (sc / pool of a block)
+
+
+class _Weights:
+    """packed weights by engine-arena view (src="arena") or by the C++ packers from the parameters (src="packer")."""
+
+    def __init__(self, eng, P, src):
+        self.eng, self.P, self.src, self.dev = eng, P, src, eng.device
+        self.keep = []
+
+    def _t(self, t):
+        if t.dim() > 4:  # packed fragment streams are raw bytes to the ABI: a flat view
+            t = t.reshape(-1)
+        self.keep.append(t)
+        return L.tensor(t)
+
+    def conv(self, cw, pname, ks=None, form=L.PACK_KSTEP, w=None, b=None):
+        """[w, b] descriptors of a packed conv: cw = the engine's ConvW, pname = its parameter prefix."""
+        if self.src == "arena":
+            W = self.eng.W
+            return [self._t(W.t(cw.w)), self._t(W.t(cw.b)) if cw.b is not None else _none_tensor()]
+        w = self.P[pname + ".w"] if w is None else w
+        if w.dim() == 2:
+            w = w[:, :, None]
+        bias = (self.P.get(pname + ".b") if b is None else b)
+        pk = _pack(w, w.shape[0], w.shape[1], w.shape[2], 0, form, self.dev)
+        return [self._t(pk), self._t(bias.float().to(self.dev)) if bias is not None else _none_tensor()]
+
+    def raw(self, name_or_t):
+        W = self.eng.W
+        return self._t(W.t(name_or_t) if isinstance(name_or_t, str) else name_or_t)
+
+    def blk(self, bw):
+        """the 7 tensors of an AdaIN block (include/stzs.h STZS_DP_BLK0 layout)."""
+        n = bw.name
+        f1 = L.PACK_LANE16 if bw.conv1.lane16 else L.PACK_KSTEP
+        f2 = L.PACK_LANE16 if bw.conv2.lane16 else L.PACK_KSTEP
+        out = self.conv(bw.conv1, n + ".conv1", form=f1) + self.conv(bw.conv2, n + ".conv2", form=f2)
+        out.append(self.conv(bw.sc, n + ".sc")[0] if bw.sc is not None else _none_tensor())
+        out += [self.raw(bw.pool_w), self.raw(bw.pool_b)] if bw.up else [_none_tensor(), _none_tensor()]
+        return out
+
+    def norm_group(self, ng, names):
+        if self.src == "arena":
+            return self.conv(ng.lin, None)
+        w = torch.cat([self.P[n + ".w"] for n in names], 0)
+        b = torch.cat([self.P[n + ".b"] for n in names], 0)
+        return self.conv(None, None, w=w, b=b)
+
+    def lstm(self, lw, name):
+        if self.src == "arena":
+            W = self.eng.W
+            return [self._t(W.t(lw.ih.w)), self._t(W.t(lw.ih.b)), self._t(W.t(lw.whhT))]
+        lib = L.load()
+        P = self.P
+        In, H = P[name + ".w_ih"].shape[1], P[name + ".w_hh"].shape[1]
+        ih = np.zeros(lib.stzs_pack_conv_size(8 * H, In, 1, 0, L.PACK_KSTEP), np.uint8)
+        bias = np.zeros(8 * H, np.float32)
+        fr = np.zeros(2 * 4 * H * H * 2, np.uint8)
+        arrs = [np.ascontiguousarray(P[name + "." + k].numpy(), dtype=np.float32)
+                for k in ("w_ih", "w_hh", "b_ih", "b_hh", "w_ih_rev", "w_hh_rev", "b_ih_rev", "b_hh_rev")]
+        assert lib.stzs_pack_lstm(*[a.ctypes.data for a in arrs], In, H, ih.ctypes.data, bias.ctypes.data,
+                                  fr.ctypes.data) == L.OK
+        return [self._t(torch.from_numpy(x).to(self.dev)) for x in (ih, bias, fr)]
+
+
+def _run_generic(op, ins, outs, p):
+    lib = L.load()
+    ti = (L.Tensor * len(ins))(*ins)
+    to = (L.Tensor * len(outs))(*[L.tensor(t) for t in outs])
+    n = getattr(lib, f"stzs_{op}_workspace")(ti, len(ins), C.byref(p))
+    assert n > 0, op
+    ws = torch.empty(n, dtype=torch.uint8, device=outs[0].device)
+    ws.random_(0, 256)  # scratch with no required contents
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = getattr(lib, f"stzs_{op}")(ti, len(ins), to, len(outs), C.byref(p), ws.data_ptr(), n, s)
+    short = getattr(lib, f"stzs_{op}")(ti, len(ins), to, len(outs), C.byref(p), ws.data_ptr(), n - 256, s)
+    torch.cuda.synchronize()
+    return rc, short
+
+
+def _engine(spec, gpu_device, tiny, tiny_params):
+    from stzs.engine import StyleTTSZS
+    if spec == "tiny":
+        return tiny, tiny_params, StyleTTSZS(tiny, tiny_params, device=gpu_device)
+    from stzs.params import init_params
+    from stzs.spec import SPEC_V0
+    P = init_params(SPEC_V0, seed=0)
+    return SPEC_V0, P, StyleTTSZS(SPEC_V0, P, device=gpu_device)
+
+
+CASES_SRC = [("tiny", "packer"), ("v0", "arena")]
+
+
+@pytest.mark.parametrize("spec,src", CASES_SRC)
+@pytest.mark.parametrize("cfg,sigma", [(True, 3.0), (True, 0.5), (False, 0.5)])
+def test_generic_denoiser_fwd(gpu_device, tiny, tiny_params, spec, src, cfg, sigma):
+    """one full NFE through the C-ABI (context, K/V, sigma conditioning, 6 layers, EDM output) == engine.denoiser_fwd"""
+    from stzs.engine import Act
+    S, P, eng = _engine(spec, gpu_device, tiny, tiny_params)
+    dev = eng.device
+    g = torch.Generator().manual_seed(71)
+    B, T = 2, 23
+    h = (torch.randn(B, T, S.d_txt, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    prompt = (torch.randn(B, S.L_s, S.code_dim, generator=g) * 0.3).to(dev)
+    R = 2 * B if cfg else B
+    x0 = torch.randn(B, S.L_s, S.code_dim, generator=g) * sigma
+    x = (torch.cat([x0, x0]) if cfg else x0).to(dev)
+    want = eng.denoiser_fwd(Act(h), prompt, x, sigma, cfg).clone()
+    W, Wt = eng.W, _Weights(eng, P, src)
+    ins = [Wt._t(x), Wt._t(h), Wt._t(prompt)]
+    ins += Wt.conv(W.dn_in, "dn.in_proj") + [Wt.raw(W.dn_pos)] + Wt.conv(W.dn_t0, "dn.t_mlp0") + \
+        Wt.conv(W.dn_t1, "dn.t_mlp1") + Wt.conv(W.dn_pool, "dn.pool_proj") + Wt.conv(W.dn_ctx_txt, "dn.ctx_txt") + \
+        Wt.conv(W.dn_ctx_prm, "dn.ctx_prm") + Wt.conv(W.dn_ada, "dn.ada") + [Wt.raw(W.dn_table)] + \
+        Wt.conv(W.dn_final_ada, "dn.final_ada") + Wt.conv(W.dn_out, "dn.out") + [Wt.raw(W.dn_ctx_null),
+                                                                                  Wt.raw(W.dn_pool_null)]
+    assert len(ins) == L.DN_NIN_BASE
+    for l, lw in enumerate(W.dn_layers):
+        pf = f"dn.l{l}"
+        for k, n in (("qkv", ".sa_qkv"), ("o", ".sa_o"), ("q", ".ca_q"), ("kv", ".ca_kv"), ("co", ".ca_o"),
+                     ("ff1", ".ff1"), ("ff2", ".ff2")):
+            ins += Wt.conv(lw[k], pf + n)
+        ins += [Wt.raw(lw["ln_g"]), Wt.raw(lw["ln_b"])]
+    D = torch.full((R, S.L_s, S.code_dim), float("nan"), device=dev)
+    p = L.params([int(cfg), S.dn_layers, S.dn_heads, S.dn_d, S.dn_ffn, S.dn_fourier], [sigma, S.sigma_data])
+    rc, short = _run_generic("denoiser_fwd", ins, [D], p)
+    assert rc == L.OK and short == L.ESHAPE
+    assert torch.equal(D, want), (D - want).abs().max().item()
+
+
+@pytest.mark.parametrize("spec,src", CASES_SRC)
+def test_generic_decoder_pre(gpu_device, tiny, tiny_params, spec, src):
+    S, P, eng = _engine(spec, gpu_device, tiny, tiny_params)
+    dev = eng.device
+    g = torch.Generator().manual_seed(72)
+    B, T40 = 2, 37
+    asr = torch.randn(B, T40, S.d_txt, generator=g).to(torch.bfloat16).to(dev)
+    F0 = (100 + 150 * torch.rand(B, 2 * T40, generator=g)).to(dev)
+    Nn = torch.randn(B, 2 * T40, generator=g).to(dev)
+    codes = (torch.randn(B, S.L_s, S.code_dim, generator=g) * 0.3).to(dev)
+    enc_in = eng.act("dec.enc_in", B, T40, S.d_txt + 2)
+    enc_in.t[:, :, :S.d_txt] = asr
+    gen_in, _ = eng.decoder_pre(dict(asr_buf=enc_in, F0=F0, N=Nn, T40=T40), codes)
+    want = gen_in.t[:, :, :S.dec_out].clone()
+    W, Wt = eng.W, _Weights(eng, P, src)
+    names = []
+    for nm in ("dec.encode", "dec.decode0", "dec.decode1", "dec.decode2", "dec.decode3"):
+        names += [nm + ".norm1", nm + ".norm2"]
+    ins = [Wt._t(asr), Wt._t(F0), Wt._t(Nn), Wt._t(codes), Wt.raw(W.dec_f0), Wt.raw(W.dec_n)] + \
+        Wt.conv(W.dec_asr_res, "dec.asr_res") + Wt.norm_group(W.dec_norm, names)
+    for nm in ("dec.encode", "dec.decode0", "dec.decode1", "dec.decode2", "dec.decode3"):
+        ins += Wt.blk(W.dec_blk[nm])
+    assert len(ins) == L.DP_NIN
+    total = W.dec_norm.total if src == "arena" else sum(P[n + ".w"].shape[0] for n in names)
+    out = torch.full((B, 2 * T40, S.dec_out), float("nan"), dtype=torch.bfloat16, device=dev)
+    p = L.params([S.dec_enc, S.dec_asr_res, S.dec_out, S.style_ac, total])
+    rc, short = _run_generic("decoder_pre", ins, [out], p)
+    assert rc == L.OK and short == L.ESHAPE
+    assert torch.equal(out, want)
+
+
+@pytest.mark.parametrize("spec,src", CASES_SRC)
+@pytest.mark.parametrize("B", [1, 3])
+def test_generic_f0n_predictor(gpu_device, tiny, tiny_params, spec, src, B):
+    from stzs.engine import Act
+    S, P, eng = _engine(spec, gpu_device, tiny, tiny_params)
+    dev = eng.device
+    g = torch.Generator().manual_seed(73)
+    T40 = 41
+    en = torch.randn(B, T40, S.pr_in, generator=g).to(torch.bfloat16).to(dev)
+    codes = (torch.randn(B, S.L_s, S.code_dim, generator=g) * 0.3).to(dev)
+    F0w, Nw = eng.f0n_predictor(Act(en), codes)
+    F0w, Nw = F0w.contiguous().clone(), Nw.contiguous().clone()
+    eng.check_status()
+    W, Wt = eng.W, _Weights(eng, P, src)
+    names = []
+    for br in ("f0", "n"):
+        for i in range(3):
+            names += [f"pr.{br}{i}.norm1", f"pr.{br}{i}.norm2"]
+    ins = [Wt._t(en), Wt._t(codes)] + Wt.lstm(W.pr_shared, "pr.shared") + Wt.norm_group(W.pr_norm, names)
+    for br in ("f0", "n"):
+        for i in range(3):
+            ins += Wt.blk(W.pr_blk[f"pr.{br}{i}"])
+        ins += Wt.conv(W.pr_blk[f"pr.{br}_proj"], f"pr.{br}_proj")
+    assert len(ins) == L.FN_NIN
+    total = W.pr_norm.total if src == "arena" else sum(P[n + ".w"].shape[0] for n in names)
+    F0 = torch.full((B, 2 * T40), float("nan"), device=dev)
+    Nn = torch.full((B, 2 * T40), float("nan"), device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    c0, c1, c2 = S.f0n_ch
+    p = L.params([S.lstm_h, c0, c1, c2, S.style_ac, S.style_pr, total])
+    rc, short = _run_generic("f0n_predictor", ins, [F0, Nn, status], p)
+    assert rc == L.OK and short == L.ESHAPE and int(status.item()) == 0
+    assert torch.equal(F0, F0w) and torch.equal(Nn, Nw)

@@ -18,10 +18,10 @@ def eng(gpu_device, tiny, tiny_params):
     return StyleTTSZS(tiny, tiny_params, device=gpu_device)
 
 
-def _pack(w, b, ups=0, lane16=False, narrow32=False):
+def _pack(w, b, ups=0, lane16=False, narrow32=False, frag32=False):
     from stzs.weights import Arena, pack_conv
     A = Arena()
-    cw = pack_conv(A, "t", w, b, ups=ups, lane16=lane16, narrow32=narrow32)
+    cw = pack_conv(A, "t", w, b, ups=ups, lane16=lane16, narrow32=narrow32, frag32=frag32)
     A.finalize("cuda:0")
     cw.w = A[cw.w]
     cw.b = A[cw.b] if cw.b is not None else None
@@ -142,6 +142,35 @@ def test_convtranspose_polyphase(eng, Ci, Co, s, refl, l16):
     e = max_rel(out, ref)
     print(Ci, Co, s, refl, e)
     assert e < 1.5e-2
+
+
+@pytest.mark.parametrize("B,T,Ci,Co,s,refl", [(2, 40, 512, 256, 10, 0), (3, 300, 256, 128, 6, 1), (2, 129, 384, 96, 4, 1),
+                                              (1, 200, 512, 256, 10, 0), (2, 1000, 256, 128, 6, 1)])
+def test_convtranspose_staged_once_bit_identical(eng, B, T, Ci, Co, s, refl):
+    """the input-staged-once polyphase ConvTranspose (csrc/ups.hip, FRAG32 weights: every column tile of a
+    workgroup over one resident input tile) == the MRF-family LANE16 form, BIT FOR BIT (same staged operands, same
+    K order), and both within the bf16 tolerance of the fp32 reference."""
+    g = torch.Generator().manual_seed(Ci + s + T)
+    k, pad = 2 * s, s // 2
+    x = bf(torch.randn(B, T, Ci, generator=g))
+    w = torch.randn(Ci, Co, k, generator=g) / math.sqrt(Co * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    Tn = T * s + refl
+    res = bf(torch.randn(B, Tn, Co, generator=g))
+    ref = convT_ref(x, w, b, stride=s, pad=pad, refl=refl, pro_act="leaky", slope=0.1, res=res)
+    from stzs import _lib as L
+    outs = []
+    for form in ("lane16", "frag32"):
+        cw, _A = _pack(w, b, ups=s, lane16=form == "lane16", frag32=form == "frag32")
+        yd = _act(torch.full((B, Tn, Co), float("nan"), dtype=torch.bfloat16, device="cuda:0"))
+        eng.conv(cw, _act(x.to(torch.bfloat16).cuda()), yd, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=pad,
+                 T_final=T * s, refl=refl, res=_act(res.to(torch.bfloat16).cuda()))
+        torch.cuda.synchronize()
+        outs.append(yd.t.clone())
+    e = max_rel(outs[1].float().cpu(), ref)
+    print(B, T, Ci, Co, s, refl, "staged-once vs ref", e)
+    assert e < 1.5e-2
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_chan_stats(eng):

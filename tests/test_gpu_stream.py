@@ -140,3 +140,50 @@ def test_longform_30s_stream(gpu_device, v0):
     assert torch.isfinite(full).all()
     assert ec < 5e-2
     assert e < 3e-1
+
+
+CHUNK_HALO = 10  # aligned frames of context on each side of a 1-s (40-frame) chunk
+
+
+@pytest.mark.parametrize("spec", ["tiny", "v0"])
+def test_chunked_decoder_vs_chunked_oracle(gpu_device, v0, spec):
+    """the CHUNKED streaming decoder (window-local statistics, global harmonic source) against the oracle's chunked
+    restatement (oracle/stzs_ref.py decode_chunked), teacher-forced on the same aligned features / F0 / N / codes:
+    bf16 decoder bound of tests/test_gpu_configs.py (waveform 1.05e-1 rel-L2, log-mel L1 7.5e-2); chunk boundaries
+    land where the oracle's do, and the streamed pieces tile the waveform."""
+    from oracle import stzs_ref as R
+    from stzs.engine import StyleTTSZS
+    from stzs.params import init_params
+    from stzs.spec import SPEC_TINY
+    if spec == "tiny":
+        S = SPEC_TINY
+        P = init_params(S, seed=0)
+        T40, chunk = 53, 8
+    else:
+        S, P = v0
+        T40, chunk = 1200, 40  # 30 s in 1-s chunks (configs[4])
+    eng = StyleTTSZS(S, P, device=gpu_device)
+    g = torch.Generator().manual_seed(31)
+    B = 1
+    asr = torch.randn(B, T40, S.d_txt, generator=g).to(torch.bfloat16).float()
+    F0 = 100 + 150 * torch.rand(B, 2 * T40, generator=g)
+    F0[:, :6] = 0.0
+    N = torch.randn(B, 2 * T40, generator=g)
+    codes = torch.randn(B, S.L_s, S.code_dim, generator=g) * 0.3
+    enc_in = eng.act("dec.enc_in", B, T40, S.d_txt + 2)
+    enc_in.t[:, :, :S.d_txt] = asr.to(torch.bfloat16).to(gpu_device)
+    pro = dict(asr_buf=enc_in, F0=F0.to(gpu_device), N=N.to(gpu_device), T40=T40)
+    parts = [(n0, w.clone()) for n0, w in eng.decode_chunked(pro, codes.to(gpu_device), [9], chunk, CHUNK_HALO)]
+    torch.cuda.synchronize()
+    nxt = 0
+    for (n0, w), (a, b, _, _) in zip(parts, R.chunk_windows(T40, chunk, CHUNK_HALO)):
+        assert n0 == nxt
+        nxt += w.shape[1]
+    assert nxt == T40 * S.frame40 and len(parts) == len(R.chunk_windows(T40, chunk, CHUNK_HALO))
+    wav = torch.cat([w for _, w in parts], 1).cpu()
+    ref, _ = R.decode_chunked(P, S, asr, F0, N, codes, [9], chunk, CHUNK_HALO)
+    e = rel_err(wav, ref)
+    m = (R.log_mel(wav, S) - R.log_mel(ref, S)).abs().mean().item()
+    print(f"chunked decoder {spec}: {len(parts)} chunks, waveform rel-L2 {e:.3e}, log-mel L1 {m:.3e}")
+    assert torch.isfinite(wav).all()
+    assert e < 1.05e-1 and m < 7.5e-2

@@ -252,3 +252,25 @@ def test_golden_v0_reproduces():
     assert torch.equal(o["prompt_idx"], t["prompt_idx"])
     for k in ("codes", "F0", "N", "wav"):
         torch.testing.assert_close(o[k], t[k], atol=1e-4, rtol=1e-3, msg=k)
+
+
+def test_decode_chunked_reduces_to_decode(tiny, tiny_params):
+    """the chunked decoder's restatement: with a halo covering the whole utterance every window IS the utterance,
+    so the chunk frames concatenate to exactly the whole-utterance conv_post / waveform; with a short halo the
+    chunk-local statistics make it a different (but finite, same-length) function."""
+    from oracle import stzs_ref as R
+    S, P = tiny, tiny_params
+    g = torch.Generator().manual_seed(0)
+    B, T40 = 2, 23
+    asr = torch.randn(B, T40, S.d_txt, generator=g)
+    F0 = 100 + 100 * torch.rand(B, 2 * T40, generator=g)
+    N = torch.randn(B, 2 * T40, generator=g)
+    codes = torch.randn(B, S.L_s, S.code_dim, generator=g) * 0.3
+    full = R.decode(P, S, asr, F0, N, codes, [3, 4])
+    wc, posts = R.decode_chunked(P, S, asr, F0, N, codes, [3, 4], chunk=8, halo=T40)
+    assert torch.equal(wc, full)
+    assert [p.shape[2] for p in posts] == [8 * 120, 8 * 120, 7 * 120 + 1]
+    w3, _ = R.decode_chunked(P, S, asr, F0, N, codes, [3, 4], chunk=8, halo=3)
+    assert w3.shape == full.shape and torch.isfinite(w3).all()
+    assert ((w3 - full).norm() / full.norm()).item() > 1e-3
+    assert R.chunk_windows(23, 8, 3) == [(0, 8, 0, 11), (8, 16, 5, 19), (16, 23, 13, 23)]
