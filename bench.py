@@ -13,6 +13,7 @@ timing  : W warm-up steps, then K steps bracketed by barrier + synchronize, max 
 roofline: the dominant kernel (the generator MRF convs -- mrfv_conv at stage 1, mrf_conv at stage 0 -- 89% of decoder FLOPs) timed
           per launch with HIP events on its own stream in an instrumented eager pass right after
           the timed region; achieved = algorithmic FLOP / average launch time (bound: MFMA).
+          roofline.stages: sum t_roof / sum t_meas per synth() stage and per kernel family (stage_roofline).
 cpu     : the CPU oracle (oracle/stzs_ref.py, torch fp32) on a bounded sample of the same
           workload (rank 0, N=1 only), threads = the process's affinity cores (capped by OMP_NUM_THREADS, the
           job's CPU share, when set); core counts and the host ISA are reported.
@@ -167,6 +168,90 @@ def longform(S, P, dev, runs=7):
                                   "window-local statistics; parity vs oracle decode_chunked (tests/test_gpu_stream.py)"))
 
 
+def _family(w, shp):
+    """kernel family of a recorded launch (stage-roofline breakdown)."""
+    if w in ("rb.c1", "rb.c2"):
+        return f"mrf k{shp[0]} stage {0 if shp[3] > 128 else 1}"
+    if w.startswith("ups"):
+        return f"ConvT {w}"
+    if w.endswith(".rec"):
+        return "lstm recurrence"
+    if w in ("attention",):
+        return "attention"
+    if w.endswith(".ln") or w.startswith("te.ln") or w in ("ln1", "rowln"):
+        return "row LayerNorm"
+    if w in ("chan_stats", "harmonic_source", "istft", "quant"):
+        return w
+    if shp is not None and shp[0] == 1:
+        return "linears (ks=1: gemm_glds / rows)"
+    return "other convs (k>1)"
+
+
+def stage_roofline(eng, S, tok_d, ref_d, eps_d, dur_d, seeds, n_frames):
+    """SURVEY.md §8(d) per stage: sum t_roof / sum t_meas, one eager pass of the bench workload (batch B on one
+    stream).  t_meas = the stage's span between HIP events on the launching stream; t_roof = sum over the stage's
+    modelled launches (every conv / linear, attention, LSTM recurrence, LayerNorm rows, statistics, harmonic source,
+    iSTFT; each timed with its own events) of max(FLOP / P_bf16, bytes / BW_hbm).  Unmodelled launches (CFG + Euler,
+    statistics finalize, gathers, duration head, copies) count in t_meas with no t_roof: the fractions are lower
+    bounds.  Families: the same over every launch of one kernel family, t_meas = their own event times."""
+    stages = {}
+    W = eng.W
+
+    def mark(name, fn):
+        eng.stage = name
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn()
+        e1.record()
+        stages[name] = (e0, e1)
+        return r
+
+    def gen(gen_in, F0, gbd):
+        har = eng.sine_gen(F0, seeds)
+        x = gen_in
+        for i in range(len(S.up_rates)):
+            x = eng.mrf(eng.upsample(x, har, i), i, gbd, W.dec_norm)
+        return x
+
+    eng.start_timer("*")
+    try:
+        h, pr = mark("text+prompt", lambda: eng.encode_inputs(tok_d, ref_d))
+        codes = mark("sampler", lambda: eng.sample_style(h, pr, eps_d, STEPS_THROUGHPUT, CFG))
+        pro = mark("predictor", lambda: eng.predict_prosody(h, codes, dur_d, n_frames))
+        gen_in, gbd = mark("decoder_pre", lambda: eng.decoder_pre(pro, codes))
+        x = mark("generator", lambda: gen(gen_in, pro["F0"], gbd))
+        mark("conv_post+istft", lambda: eng.istft(eng.conv_post(x)))
+    finally:
+        eng.stage = ""
+        rec = eng.stop_timer()
+    roof = lambda f, b: max(f / (PEAK_BF16_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9))
+    out, fam = {}, {}
+    for name, (e0, e1) in stages.items():
+        rs = [r for r in rec if r[5] == name]
+        tm = e0.elapsed_time(e1) * 1e-3
+        tr = sum(roof(r[2], r[3]) for r in rs)
+        out[name] = dict(t_meas_us=round(tm * 1e6, 1), t_roof_us=round(tr * 1e6, 1), frac=round(tr / tm, 4),
+                         modelled_us=round(sum(r[1] for r in rs) * 1e6, 1), launches_modelled=len(rs),
+                         gflop=round(sum(r[2] for r in rs) / 1e9, 2), gbytes=round(sum(r[3] for r in rs) / 1e9, 3))
+    for r in rec:
+        f = fam.setdefault(_family(r[0], r[4]), [0, 0.0, 0.0, 0.0, 0.0])
+        f[0] += 1
+        f[1] += r[1]
+        f[2] += roof(r[2], r[3])
+        f[3] += r[2]
+        f[4] += r[3]
+    fams = {k: dict(launches=v[0], t_meas_us=round(v[1] * 1e6, 1), t_roof_us=round(v[2] * 1e6, 1),
+                    frac=round(v[2] / v[1], 4) if v[1] > 0 else None,
+                    tflops=round(v[3] / v[1] / 1e12, 1) if v[1] > 0 else None,
+                    alg_gbs=round(v[4] / v[1] / 1e9, 1) if v[1] > 0 else None)
+            for k, v in sorted(fam.items(), key=lambda kv: -kv[1][1])}
+    tm_all = sum(v["t_meas_us"] for v in out.values())
+    tr_all = sum(v["t_roof_us"] for v in out.values())
+    return dict(method="eager pass, one stream, batch %d; HIP events per stage and per modelled launch" % tok_d.shape[0],
+                total=dict(t_meas_us=round(tm_all, 1), t_roof_us=round(tr_all, 1), frac=round(tr_all / tm_all, 4)),
+                stages=out, families=fams)
+
+
 def precise_mode(S, P, dev, B=64, steps=5):
     """throughput of the PRECISE mode -- the whole pipeline (text encoder, style diffusion, predictor, decoder) on
     fp32 activations and split-operand bf16x3 products, the mode that meets the north-star log-mel L1 <= 1e-3
@@ -206,6 +291,7 @@ def main():
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-longform", action="store_true")
     ap.add_argument("--no-precise", action="store_true")
+    ap.add_argument("--no-stages", action="store_true", help="skip the per-stage roofline pass")
     ap.add_argument("--streams", type=int, default=2,
                     help="split the per-GPU batch over this many concurrently replayed graphs (engine twins)")
     ap.add_argument("--stagger", type=int, default=1, help="start shard j > 0 one front phase late")
@@ -386,6 +472,8 @@ def main():
                 avg_launch_us=round(tsum / nl * 1e6, 2), alg_gflop_per_launch=round(fsum / nl / 1e9, 3),
                 time_frac=round(t_roof / tsum, 4) if tsum > 0 else None, hbm_bound_launches=n_hbm,
                 alg_hbm_gbs=round(bsum / tsum / 1e9, 1) if tsum > 0 else None)
+    if not args.no_stages:  # SURVEY.md §8(d) aggregate per stage (sum t_roof / sum t_meas) + per kernel family
+        roof["stages"] = stage_roofline(eng, S, tok_d, ref_d, eps_d, dur_d, seeds, n_frames)
 
     # ---- p50 latency, configs[1]: batch 1, 10-step CFG-5 ----
     lat = None

@@ -205,6 +205,7 @@ __attribute__((visibility("hidden"))) int stzs_ups_conv_launch(const stzs_conv_a
     switch (nch) {
         case 1: k = R ? ups_conv<1, true> : ups_conv<1, false>; break;
         case 2: k = R ? ups_conv<2, true> : ups_conv<2, false>; break;
+        case 3: k = R ? ups_conv<3, true> : ups_conv<3, false>; break;
         case 4: k = R ? ups_conv<4, true> : ups_conv<4, false>; break;
         default: return STZS_ESHAPE;
     }

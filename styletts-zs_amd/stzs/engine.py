@@ -48,6 +48,14 @@ DN_ROWS = {}
 LATENCY_DN_ROWS = dict(inp=1, qkv=1, o=1, q=1, co=1, ff1=1, ff2=4, out=1)
 
 
+_ES = {L.F32: 4, L.BF16: 2, L.F8: 1}
+
+
+def _ln_cost(a):
+    """(FLOP, bytes) of a row LayerNorm launch: the rows read once and written once (the FLOPs are negligible)."""
+    return 0, a.R * a.C * (_ES[a.in_dtype] + _ES[a.out_dtype])
+
+
 def _table_env(var, default):
     v = os.environ.get(var)
     if v is None:
@@ -248,8 +256,19 @@ class StyleTTSZS:
         """weight reference -> device tensor (arena name, or an already-resolved tensor)."""
         return x if isinstance(x, torch.Tensor) else self.W.t(x)
 
-    def _call(self, fn, arg, what):
+    def _call(self, fn, arg, what, cost=None):
+        """one library launch; cost = (algorithmic FLOP, algorithmic bytes) of it, recorded with HIP events when a
+        timer of every launch is running (start_timer("*"), the per-stage roofline of bench.py)."""
         self.launches += 1
+        tm = self.timer
+        if tm is not None and tm["all"] and cost is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            L.check(fn(C.byref(arg), self.stream()), what)
+            e1.record()
+            tm["rec"].append((what, e0, e1, float(cost[0]), float(cost[1]), None, self.stage))
+            return
         L.check(fn(C.byref(arg), self.stream()), what)
 
     # ------------------------------------------------------------------ ops
@@ -343,21 +362,24 @@ class StyleTTSZS:
             st = (slab, Cc, self.buf(stats_key + ".m", (y.B, Cc), torch.float32),
                   self.buf(stats_key + ".r", (y.B, Cc), torch.float32))
         tm = self.timer
-        if tm is not None and what in tm["tags"]:
+        if tm is not None and (tm["all"] or what in tm["tags"]):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
-            self._call(self.lib.stzs_conv1d, a, what)
+            self.launches += 1
+            L.check(self.lib.stzs_conv1d(C.byref(a), self.stream()), what)
             e1.record()
             flops = 2.0 * y.B * a.T_out * (cw.ups or 1) * cw.Co * cw.Ci * cw.ks
-            # algorithmic bytes: input tile once + output once (+ residual/acc reads), bf16/f32 as stored
+            # algorithmic bytes: input tile once + output once (+ residual/acc reads), bf16/f32 as stored, + the
+            # weights once (bf16; e4m3 for the fp8 linears; hi + lo for the split-operand precise form)
+            wbytes = (cw.ups or 1) * cw.Co * cw.Ci * cw.ks * (1 if cw.f8 else (4 if cw.wx3 is not None else 2))
             byt = x.B * x.T * x.C * x.t.element_size() + y.B * a.T_out * (cw.ups or 1) * cw.Co * y.t.element_size() * (
-                1 + (res is not None) + (acc_in is not None))
-            tm["rec"].append((what, e0, e1, flops, byt, (cw.ks, dil, a.T_out, cw.Co)))
+                1 + (res is not None) + (acc_in is not None)) + wbytes
+            tm["rec"].append((what, e0, e1, flops, byt, (cw.ks, dil, a.T_out, cw.Co), self.stage))
         else:
             self._call(self.lib.stzs_conv1d, a, what)
         if post_ln is not None:  # the LayerNorm that consumes this linear's output (stzs_rowln_args)
-            self._call(self.lib.stzs_row_layernorm, post_ln, what + ".ln")
+            self._call(self.lib.stzs_row_layernorm, post_ln, what + ".ln", cost=_ln_cost(post_ln))
         if st is None:
             return y
         slab, Cc, mean, rstd = st
@@ -421,16 +443,19 @@ class StyleTTSZS:
         return outs
 
     timer = None
+    stage = ""  # label of the synth() stage being enqueued (set by the caller; recorded with each timed launch)
 
     def start_timer(self, tags):
-        """record HIP events around every conv launch whose tag is in `tags` (same stream as the kernel)."""
-        self.timer = dict(tags=set(tags), rec=[])
+        """record HIP events around every conv launch whose tag is in `tags` (same stream as the kernel); tags "*":
+        every conv launch and every other launch whose algorithmic cost the engine models (attention, LSTM
+        recurrences, LayerNorm rows, statistics, harmonic source, iSTFT)."""
+        self.timer = dict(tags=set(tags) if tags != "*" else set(), all=tags == "*", rec=[])
 
     def stop_timer(self):
+        """-> [(tag, seconds, FLOP, bytes, conv shape | None, stage)] of the recorded launches, in launch order."""
         tm, self.timer = self.timer, None
         torch.cuda.synchronize(self.device)
-        out = [(w, e0.elapsed_time(e1) * 1e-3, f, b, shp) for (w, e0, e1, f, b, shp) in tm["rec"]]
-        return out
+        return [(w, e0.elapsed_time(e1) * 1e-3, f, b, shp, stg) for (w, e0, e1, f, b, shp, stg) in tm["rec"]]
 
     def stats(self, x: Act, key):
         """InstanceNorm statistics of x over time -> (mean, rstd, stat_bs)."""
@@ -441,7 +466,7 @@ class StyleTTSZS:
         a = L.StatsArgs()
         a.x, a.mean, a.rstd, a.partial = x.ptr, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr()
         a.ld, a.bs, a.stat_bs, a.B, a.T, a.C, a.dtype, a.eps = x.ld, x.bs, Cc, x.B, x.T, Cc, x.dt, 1e-5
-        self._call(self.lib.stzs_chan_stats, a, "chan_stats")
+        self._call(self.lib.stzs_chan_stats, a, "chan_stats", cost=(0, x.B * x.T * x.C * x.t.element_size()))
         return mean, rstd, Cc
 
     def rowln(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=1.0, act=L.ACT_NONE, slope=0.0,
@@ -454,7 +479,7 @@ class StyleTTSZS:
         a.C, a.gdiv, a.in_dtype, a.out_dtype, a.act = x.C, gdiv, x.dt, y.dt, act
         a.gadd, a.eps, a.slope = gadd, 1e-5, slope
         assert x.ld * x.T == x.bs and y.ld * y.T == y.bs
-        self._call(self.lib.stzs_row_layernorm, a, what)
+        self._call(self.lib.stzs_row_layernorm, a, what, cost=_ln_cost(a))
 
     def quant(self, x: Act, y: Act, scale: torch.Tensor, what="quant"):
         """bf16 rows -> e4m3fn rows + per-row scale (stzs_quant_rows)."""
@@ -462,7 +487,7 @@ class StyleTTSZS:
         a.x, a.y, a.scale, a.ldx, a.ldy = x.ptr, y.ptr, scale.data_ptr(), x.ld, y.ld
         a.R, a.C = x.B * x.T, x.C
         assert x.ld * x.T == x.bs and y.ld * y.T == y.bs
-        self._call(self.lib.stzs_quant_rows, a, what)
+        self._call(self.lib.stzs_quant_rows, a, what, cost=(0, a.R * a.C * (x.t.element_size() + 1)))
 
     def attention(self, q: Act, k: Act, v: Act, o: Act):
         S = self.spec
@@ -472,7 +497,9 @@ class StyleTTSZS:
         a.bsq, a.bsk, a.bsv, a.bso = q.bs, k.bs, v.bs, o.bs
         a.R, a.Lq, a.Lk, a.heads, a.dh = q.B, q.T, k.T, S.dn_heads, S.dn_head_dim
         a.precise = int(q.t.dtype == torch.float32)  # fp32 operands: the fp32 attention kernel
-        self._call(self.lib.stzs_attention, a, "attention")
+        self._call(self.lib.stzs_attention, a, "attention",
+                   cost=(4.0 * a.R * a.heads * a.Lq * a.Lk * a.dh,
+                         a.R * (2 * a.Lq + 2 * a.Lk) * a.heads * a.dh * q.t.element_size()))
 
     def lstm(self, lw, x: Act, y: Act, key):
         gx = self.act(key + ".gx", x.B, x.T, 8 * lw.H, torch.float32)
@@ -489,7 +516,9 @@ class StyleTTSZS:
         a.ldg, a.bsg, a.ldy, a.bsy = gx.ld, gx.bs, y.ld, y.bs
         a.B, a.T, a.H, a.ndir = x.B, x.T, lw.H, 2
         a.status, a.spin_limit = self.status.data_ptr(), self.lstm_spin_limit
-        self._call(self.lib.stzs_lstm, a, key + ".rec")
+        self._call(self.lib.stzs_lstm, a, key + ".rec",  # recurrent products + gate rows in, h rows out, W_hh once
+                   cost=(2.0 * x.B * x.T * 2 * 4 * lw.H * lw.H,
+                         x.B * x.T * (8 * lw.H * 4 + 2 * lw.H * y.t.element_size()) + 2 * 4 * lw.H * lw.H * 2))
         return y
 
     def copy2d(self, x: Act, y: Act, R, Cn, bsx=None):
@@ -748,7 +777,7 @@ class StyleTTSZS:
                                      y_scale=sin))
         fb = fmodx[0, i * R].data_ptr()
         lns.append(self._ln_args(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls))
-        self._call(self.lib.stzs_row_layernorm, lns[0], "ln1")
+        self._call(self.lib.stzs_row_layernorm, lns[0], "ln1", cost=_ln_cost(lns[0]))
         sk = {} if (f8 or self.adt == torch.float32) else self.dn_splitk
         for l, lw in enumerate(W.dn_layers):
             mb = modx[l, i * R].data_ptr()
@@ -1023,7 +1052,8 @@ class StyleTTSZS:
         a.B, a.T80, a.hop, a.n_fft, a.hop_s, a.nh = B, T80, S.hop, S.n_fft, S.istft_hop, nh
         a.sr, a.sine_amp, a.noise_std, a.voiced_thr = float(S.sr), S.sine_amp, S.noise_std, S.voiced_threshold
         a.har_dtype = har.dt
-        self._call(self.lib.stzs_harmonic_source, a, "harmonic_source")
+        self._call(self.lib.stzs_harmonic_source, a, "harmonic_source",  # F0 in, prefix, STFT rows out
+                   cost=(0, B * T80 * 4 * (1 + 2 * nh) + B * Tf * S.har_ch * har.t.element_size()))
         return har
 
     def upsample(self, x: Act, har: Act, i: int) -> Act:
@@ -1066,7 +1096,7 @@ class StyleTTSZS:
         a = L.IstftArgs()
         a.post, a.wav, a.ldp, a.bsp, a.bsw = post.ptr, wav.data_ptr(), post.ld, post.bs, Nout
         a.B, a.Tf, a.n_fft, a.hop_s = B, Tcur, S.n_fft, S.istft_hop
-        self._call(self.lib.stzs_istft, a, "istft")
+        self._call(self.lib.stzs_istft, a, "istft", cost=(0, B * Tcur * S.har_ch * 4 + B * Nout * 4))
         return wav
 
     def generator(self, x: Act, F0: torch.Tensor, seeds, gbd, trace=None, istft=True, har: Act = None):
