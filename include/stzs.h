@@ -147,7 +147,7 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * a 64/128-row block and 1/Z of K, operands loaded straight into MFMA fragments.  splitk = Z in {0, 1} (off) or any Z
  * with ci_pad / 32 = 4 Z {1, 2, 4, 8, 16}: the Z slices hand their fp32 partials to the tile's last arriver through
  * splitk_ws (stzs_conv_rows_workspace bytes) and splitk_ctr (one zeroed uint32 per tile, left zeroed).  Epilogue:
- * bias, epi_act NONE | GELU, FLAT gate, residual, alpha, beta * acc_in.  The per-element summation order depends on
+ * bias, epi_act NONE | GELU | SILU, FLAT gate, residual, alpha, beta * acc_in.  The per-element summation order depends on
  * K and Z only (batch-invariant).  Replaces gemm_glds for 100-row linears whose 8-32 tiles would stream all of K
  * through 8-32 CUs (SURVEY §8(a) a2 at B = 1). */
 #define STZS_CONV_ROWS 2048

@@ -70,7 +70,15 @@ struct ConvOpt {
     int epi_act = STZS_ACT_NONE;
     float epi_slope = 0.f;
     Stats* stats_out = nullptr;  // fused InstanceNorm statistics of the stored output
+    bool rows = false;           // per-utterance linear: the whole-chip small-M form when K allows (rows_ok)
 };
+
+// the engine's rule for its per-utterance linears (stzs/engine.py _rows_z): one K slice, every wave the same
+// K-step count
+bool rows_ok(int ci_pad) {
+    const int nk = ci_pad / 32;
+    return ci_pad % 32 == 0 && nk % 4 == 0 && (nk / 4 == 1 || nk / 4 == 2 || nk / 4 == 4 || nk / 4 == 8 || nk / 4 == 16);
+}
 
 // a packed conv / linear: weights (STZS_PACK_* form), fp32 bias (or none)
 struct CW {
@@ -78,8 +86,11 @@ struct CW {
     const stzs_tensor_t* b;
     int Co, Ci, ks, form;
 };
-// the engine's form rule for AdaIN-block convs (stzs/weights.py _lane16_ok): 128-channel chunks, Co % 16 == 0
-inline int blk_form(int Co, int Ci) { return (Ci > 64 && Co % 16 == 0) ? STZS_PACK_LANE16 : STZS_PACK_KSTEP; }
+// the engine's form rule for the k3 AdaIN-block convs (stzs/weights.py pack_blk): the register-direct form for
+// 128-channel chunks and Co % 32 == 0, the LDS-ring MRF form for Co % 16 == 0, else the general one
+inline int blk_form(int Co, int Ci) {
+    return (Ci > 64 && Co % 32 == 0) ? STZS_PACK_FRAG32 : (Ci > 64 && Co % 16 == 0) ? STZS_PACK_LANE16 : STZS_PACK_KSTEP;
+}
 
 struct Ctx {
     Carve cv;
@@ -189,6 +200,9 @@ int conv(Ctx& c, const CW& w, const Act& x, const Act& y, const ConvOpt& o = Con
     if (w.ks == 1 && o.stride == 1 && o.pad == 0 && !o.pro && o.pro_act == STZS_ACT_NONE && o.cscale == 1.f &&
         (x.dt == STZS_BF16 || x.dt == STZS_F8) && x.c0 + a.ci_pad <= x.ld && a.T_out == x.T && w.form == STZS_PACK_KSTEP)
         a.flags |= STZS_CONV_A_DMA;
+    if (o.rows && rows_ok(a.ci_pad) && w.ks == 1 && w.form == STZS_PACK_KSTEP && !o.pro && !o.stats_out &&
+        (x.dt == STZS_F32 || (x.dt == STZS_BF16 && o.cscale == 1.f)) && x.c0 + a.ci_pad <= x.ld && a.T_out == x.T)
+        a.flags = (a.flags & ~STZS_CONV_A_DMA) | STZS_CONV_ROWS;
     float* slab = nullptr;
     int Cc = 0;
     if (o.stats_out) {
@@ -366,7 +380,9 @@ int norm_gb(Ctx& c, const stzs_tensor_t& w, const stzs_tensor_t& b, const float*
     y.ld = total;
     y.bs = total;
     y.dt = STZS_F32;
-    return conv(c, CW{&w, &b, total, style, 1, STZS_PACK_KSTEP}, x, y);
+    ConvOpt o;
+    o.rows = true;
+    return conv(c, CW{&w, &b, total, style, 1, STZS_PACK_KSTEP}, x, y, o);
 }
 
 // ---------------------------------------------------------------------------------------------- a2 denoiser_fwd
@@ -449,7 +465,9 @@ int denoiser(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int 
         y.ld = d;
         y.bs = d;
         y.dt = STZS_F32;
-        CK(conv(c, W(STZS_DN_POOL_W, d, cd), x, y));
+        ConvOpt o;
+        o.rows = true;
+        CK(conv(c, W(STZS_DN_POOL_W, d, cd), x, y, o));
         if (cfg) CK(copy2d(c, in[STZS_DN_POOL_NULL].data, d, 0, STZS_F32, pool + (size_t)B * d, d, d, STZS_F32, B, 1, d));
     }
     Act kv[16];
@@ -482,8 +500,11 @@ int denoiser(Ctx& c, const stzs_tensor_t* in, int n_in, stzs_tensor_t* out, int 
     {
         ConvOpt o;
         o.epi_act = STZS_ACT_SILU;
+        o.rows = true;
         CK(conv(c, W(STZS_DN_T0_W, d, nf), four, t0, o));
-        CK(conv(c, W(STZS_DN_T1_W, d, d), t0, temb));
+        ConvOpt o1;
+        o1.rows = true;
+        CK(conv(c, W(STZS_DN_T1_W, d, d), t0, temb, o1));
     }
     Act cb, mod, fmod;
     CK(c.act(cb, R, 1, d, STZS_BF16));

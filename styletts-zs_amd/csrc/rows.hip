@@ -233,11 +233,12 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
     }
 }
 
-// epilogue activations of the denoiser linears: none, GELU (ffn1)
+// epilogue activations: none, GELU (ffn1), SiLU (the sigma-embedding MLP)
 template <typename TIn, typename TOut, int MT, int KPW, bool SPLIT>
 void* pick_act(int act) {
     switch (act) {
         case STZS_ACT_GELU: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_GELU, SPLIT>;
+        case STZS_ACT_SILU: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_SILU, SPLIT>;
         case STZS_ACT_NONE: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_NONE, SPLIT>;
         default: return nullptr;
     }

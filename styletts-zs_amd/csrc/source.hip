@@ -33,10 +33,12 @@ STZS_DEV float counter_normal(uint32_t key, uint32_t idx) {
     return (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
 }
 // the same counter pair as counter_normal, Box-Muller in fp32 hardware intrinsics (v_log_f32,
-// v_sqrt_f32, v_cos_f32 in revolutions): within ~2e-6 of the fp64 transform (tests/test_gpu_ops.py)
-STZS_DEV float counter_normal_fast(uint32_t key, uint32_t idx) {
-    const uint32_t a = hash32(key ^ hash32(idx * 2u));
-    const uint32_t b = hash32(key ^ hash32(idx * 2u + 1u));
+// v_sqrt_f32, v_cos_f32 in revolutions): within ~2e-6 of the fp64 transform (tests/test_gpu_ops.py).
+// hi0 = hash32(2 idx), hi1 = hash32(2 idx + 1): the counter hashes do not depend on the stream key, so a sample's
+// harmonics share them (the same values as counter_normal computes)
+STZS_DEV float counter_normal_fast(uint32_t key, uint32_t hi0, uint32_t hi1) {
+    const uint32_t a = hash32(key ^ hi0);
+    const uint32_t b = hash32(key ^ hi1);
     const float u1 = ((float)(a >> 8) + 1.f) * (1.f / 16777216.f);
     const float u2 = (float)(b >> 8) * (1.f / 16777216.f);
     return __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1)) * __builtin_amdgcn_cosf(u2);
@@ -78,9 +80,12 @@ __global__ __launch_bounds__(256) void phase_prefix_kernel(const stzs_source_arg
 constexpr int FB = 256;  // STFT frames per workgroup
 constexpr int KW = 8;    // 80-fps frames spanned by one workgroup's samples (checked on the host)
 
+// NFFT > 0: the transform size at compile time (twiddles and window in registers, the STFT sums fully unrolled);
+// 0: any size (runtime loops over the LDS tables).  The same products summed in the same order either way.
+template <int NFFT>
 __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args a) {
     extern __shared__ float sm[];
-    const int nfft = a.n_fft, hs = a.hop_s, nb = nfft / 2 + 1;
+    const int nfft = NFFT ? NFFT : a.n_fft, hs = a.hop_s, nb = nfft / 2 + 1;
     const int NS = hs * (FB - 1) + nfft;
     float* sbuf = sm;                 // NS samples
     float* twc = sbuf + NS;           // nfft cos
@@ -133,12 +138,13 @@ __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args
             const float namp = voiced ? a.noise_std : amp3;
             const float* fi = finc + kk * a.nh;
             const float* fp = fpre + kk * a.nh;
+            const uint32_t hi0 = hash32((uint32_t)n * 2u), hi1 = hash32((uint32_t)n * 2u + 1u);
             float acc = 0.f;
             for (int h = 0; h < a.nh; ++h) {
                 const float t = __fadd_rn(fp[h], __fmul_rn(jj, fi[h]));
                 const float th = __fsub_rn(t, floorf(t));  // wrapped phase, cycles
                 const float sine = amp * __builtin_amdgcn_sinf(th);
-                const float z = counter_normal_fast(keys[h], (uint32_t)n);
+                const float z = counter_normal_fast(keys[h], hi0, hi1);
                 acc = fmaf(mw[h], fmaf(sine, uv, namp * z), acc);
             }
             const float xx = acc + wb;
@@ -153,20 +159,57 @@ __global__ __launch_bounds__(256) void source_stft_kernel(const stzs_source_args
         const bool f32 = a.har_dtype == STZS_F32;
         bf16_t* Hh = reinterpret_cast<bf16_t*>(a.har) + (long)b * a.bsh + (long)f * a.ldh;
         float* Hf = reinterpret_cast<float*>(a.har) + (long)b * a.bsh + (long)f * a.ldh;
-        for (int kb = 0; kb < nb; ++kb) {
-            float re = 0.f, im = 0.f;
-            for (int i = 0; i < nfft; ++i) {
-                const int m = (kb * i) % nfft;
-                const float x = s[i] * win[i];
-                re += x * twc[m];
-                im -= x * tws[m];
+        if constexpr (NFFT > 0) {
+            constexpr int NB = NFFT / 2 + 1;
+            float tc[NFFT], ts[NFFT], x[NFFT];
+#pragma unroll
+            for (int i = 0; i < NFFT; ++i) {
+                tc[i] = twc[i];
+                ts[i] = tws[i];
+                x[i] = s[i] * win[i];
+            }
+            float re[NB], im[NB];
+#pragma unroll
+            for (int kb = 0; kb < NB; ++kb) {
+                float r = 0.f, q = 0.f;
+#pragma unroll
+                for (int i = 0; i < NFFT; ++i) {
+                    const int m = (kb * i) % NFFT;
+                    r += x[i] * tc[m];
+                    q -= x[i] * ts[m];
+                }
+                re[kb] = r;
+                im[kb] = q;
             }
             if (f32) {
-                Hf[kb] = re;
-                Hf[nb + kb] = im;
+#pragma unroll
+                for (int kb = 0; kb < NB; ++kb) {
+                    Hf[kb] = re[kb];
+                    Hf[NB + kb] = im[kb];
+                }
             } else {
-                Hh[kb] = f2bf(re);
-                Hh[nb + kb] = f2bf(im);
+#pragma unroll
+                for (int kb = 0; kb < NB; ++kb) {
+                    Hh[kb] = f2bf(re[kb]);
+                    Hh[NB + kb] = f2bf(im[kb]);
+                }
+            }
+        } else {
+            for (int kb = 0; kb < nb; ++kb) {
+                float re = 0.f, im = 0.f;
+                for (int i = 0; i < nfft; ++i) {
+                    const int m = (kb * i) % nfft;
+                    const float x = s[i] * win[i];
+                    re += x * twc[m];
+                    im -= x * tws[m];
+                }
+                if (f32) {
+                    Hf[kb] = re;
+                    Hf[nb + kb] = im;
+                } else {
+                    Hh[kb] = f2bf(re);
+                    Hh[nb + kb] = f2bf(im);
+                }
             }
         }
         for (int c = 2 * nb; c < a.ldh; ++c) {
@@ -193,7 +236,10 @@ extern "C" int stzs_harmonic_source(const stzs_source_args* a, void* stream) {
     const int NS = a->hop_s * (FB - 1) + a->n_fft;
     if (NS / a->hop + 2 > KW) return STZS_ESHAPE;
     const size_t lds = (size_t)(NS + 3 * a->n_fft) * 4 + (size_t)a->nh * (8 + 4 + 2 * KW * 4);
-    hipLaunchKernelGGL(source_stft_kernel, dim3((Tf + FB - 1) / FB, a->B), dim3(256), lds, s, *a);
+    if (a->n_fft == 20)
+        hipLaunchKernelGGL(source_stft_kernel<20>, dim3((Tf + FB - 1) / FB, a->B), dim3(256), lds, s, *a);
+    else
+        hipLaunchKernelGGL(source_stft_kernel<0>, dim3((Tf + FB - 1) / FB, a->B), dim3(256), lds, s, *a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

@@ -140,6 +140,7 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        if (a.flags & 4) continue;  // diagnostic (tools/ups_bench.py): no epilogue
         // epilogue: row q -> t = q ups + p - pad_up (+ refl), valid for q < T_out and t in [0, T_final)
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {

@@ -186,6 +186,11 @@ class StyleTTSZS:
         # small-M whole-chip form of the bf16 denoiser linears (csrc/rows.hip): {linear: K slices}; a per-engine
         # property of the weight like dn_splitk (batch-invariant), taking precedence over it
         self.dn_rows = _table_env("STZS_DN_ROWS", DN_ROWS) if dn_rows is None else dict(dn_rows)
+        # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
+        # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
+        # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
+        # STZS_SMALL_ROWS=0 turns it off.
+        self.small_rows = os.environ.get("STZS_SMALL_ROWS", "1") != "0"
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
@@ -335,7 +340,7 @@ class StyleTTSZS:
         if (rows > 0 and cw.ks == 1 and stride == 1 and pad == 0 and not cw.ups and pro is None and
                 pro_act == L.ACT_NONE and not cw.f8 and cw.wx3 is None and cw.w32 is None and stats_key is None and
                 (x.t.dtype == torch.float32 or (x.t.dtype == torch.bfloat16 and cscale == 1.0)) and
-                epi_act in (L.ACT_NONE, L.ACT_GELU) and
+                epi_act in (L.ACT_NONE, L.ACT_GELU, L.ACT_SILU) and
                 x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             # small-M linear on the whole chip (csrc/rows.hip): 16-column tiles x K split in `rows` slices
             a.flags = (a.flags & ~8) | L.CONV_ROWS
@@ -389,6 +394,13 @@ class StyleTTSZS:
         self.launches += 1
         L.check(self.lib.stzs_chan_stats_final(C.byref(s), L.CONV_STAT_ROWS, self.stream()), "chan_stats_final")
         return y, (mean, rstd, Cc)
+
+    def _rows_z(self, cw: ConvW) -> int:
+        """1 = the whole-chip small-M form (one K slice: no hand-off state) for a per-utterance linear whose K gives
+        every wave the same K-step count, 0 = the tiled path -- a function of the weight's shape only (the native
+        composite operators, csrc/abi_ops.hip, apply the same rule: bit-identical)."""
+        nk = cw.ci_pad // 32
+        return int(self.small_rows and nk % 4 == 0 and nk // 4 in (1, 2, 4, 8, 16))
 
     def _scratch(self, name, n):
         """fp32 scratch shared by consecutive launches of ONE branch (a conv's statistics partials, consumed by
@@ -695,7 +707,7 @@ class StyleTTSZS:
             self._call(self.lib.stzs_copy2d, a, "ctx_null")
         pm = self.mean_rows(prompt, 0, cd, "dn.pm")
         pool = self.buf("dn.pool", (R, d), torch.float32)
-        self.conv(W.dn_pool, Act(pm[:, None]), Act(pool[:B, None]), what="dn.pool")
+        self.conv(W.dn_pool, Act(pm[:, None]), Act(pool[:B, None]), rows=self._rows_z(W.dn_pool), what="dn.pool")
         if cfg:
             a = L.CopyArgs()
             a.x, a.y = W.t(W.dn_pool_null).data_ptr(), pool[B:].data_ptr()
@@ -715,8 +727,8 @@ class StyleTTSZS:
             fo = self._consts[fkey] = torch.from_numpy(four)[None].to(self.device)
         t0 = self.act("dn.t0", 1, steps, d, torch.float32)
         temb = self.act("dn.temb", 1, steps, d, torch.float32)
-        self.conv(W.dn_t0, Act(fo), t0, epi_act=L.ACT_SILU, what="dn.t0")
-        self.conv(W.dn_t1, t0, temb, what="dn.t1")
+        self.conv(W.dn_t0, Act(fo), t0, epi_act=L.ACT_SILU, rows=self._rows_z(W.dn_t0), what="dn.t0")
+        self.conv(W.dn_t1, t0, temb, rows=self._rows_z(W.dn_t1), what="dn.t1")
         cb = self.buf("dn.cb", (steps * R, d), self.adt)
         mod = self.buf("dn.mod", (steps * R, 6 * d), torch.float32)
         fmod = self.buf("dn.fmod", (steps * R, 2 * d), torch.float32)
@@ -918,7 +930,7 @@ class StyleTTSZS:
         sg = self.mean_rows(codes, S.style_ac, S.style_pr, "pr.sg")
         ng = W.pr_norm
         gbp = self.buf("pr.gbn", (B, ng.total), torch.float32)
-        self.conv(ng.lin, Act(sg[:, None]), Act(gbp[:, None]), what="pr.norms")
+        self.conv(ng.lin, Act(sg[:, None]), Act(gbp[:, None]), rows=self._rows_z(ng.lin), what="pr.norms")
         T80 = 2 * T40
         F0 = self.buf("pr.F0", (B, T80, 1), torch.float32)
         Nn = self.buf("pr.N", (B, T80, 1), torch.float32)
@@ -988,7 +1000,7 @@ class StyleTTSZS:
         sa = self.mean_rows(codes, 0, S.style_ac, "dec.sa")
         ng = W.dec_norm
         gbd = self.buf("dec.gbn", (B, ng.total), torch.float32)
-        self.conv(ng.lin, Act(sa[:, None]), Act(gbd[:, None]), what="dec.norms")
+        self.conv(ng.lin, Act(sa[:, None]), Act(gbd[:, None]), rows=self._rows_z(ng.lin), what="dec.norms")
         return gbd
 
     def decoder_pre(self, pro: dict, codes: torch.Tensor):

@@ -348,10 +348,20 @@ def _lane16_ok(w) -> bool:
     return Ci > 64 and Co % 16 == 0
 
 
+def _frag32_ok(w) -> bool:
+    """AdaIN-block conv eligible for the register-direct kernel (csrc/mrfv.hip, bit-identical to csrc/mrf.hip):
+    k3, 128-channel input chunks, Co % 32 == 0.  Faster on every decoder / predictor block shape at the bench batch
+    (tools/blk_bench.py, B = 64: dec.encode.conv1 103 -> 83 us, decode conv1 155 -> 143, conv2 135 -> 125, decode3
+    conv2 79 -> 65, predictor 45 -> 39 and 28 -> 24).  csrc/abi_ops.hip blk_form applies the same rule."""
+    Co, Ci = w.shape[0], w.shape[1]
+    return w.shape[2] == 3 and Ci > 64 and Co % 32 == 0
+
+
 def pack_blk(A: Arena, P, name, up=False, x3=False) -> BlkW:
     w1, w2 = P[name + ".conv1.w"], P[name + ".conv2.w"]
-    c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1), x3=x3)
-    c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2), x3=x3)
+    f1, f2 = _frag32_ok(w1), _frag32_ok(w2)
+    c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1) and not f1, frag32=f1, x3=x3)
+    c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2) and not f2, frag32=f2, x3=x3)
     sc = pack_conv(A, name + ".sc", P[name + ".sc.w"], x3=x3) if name + ".sc.w" in P else None
     pw = pb = None
     if up:
@@ -468,13 +478,19 @@ class PackedModel:
                 for m, dil in enumerate(S.rb_dils):
                     p = f"gen.rb{i}.{j}.{m}"
                     l16 = S.gen_ch[i] % 128 == 0 and (kr - 1) * dil <= 64  # MRF kernel (csrc/mrf.hip)
-                    # one 128-channel input chunk: the register-direct MRF kernel (csrc/mrfv.hip), 3 workgroups
-                    # per CU; bit-identical to mrf.hip, 8-18% faster on the stage-1 shapes (tools/mrfv_bench.py)
-                    fr = S.gen_ch[i] == 128 and kr in (3, 7, 11) and (kr - 1) * dil <= 64
+                    # the register-direct MRF kernel (csrc/mrfv.hip; bit-identical to mrf.hip) where it measured
+                    # faster (tools/mrfv_bench.py, B = 64, profiles/r02_mrfv_bench_s.log): every conv with one
+                    # 128-channel input chunk (stage 1: 3 workgroups per CU, 8-18%); with two chunks (stage 0) the k3
+                    # convs (155 vs 168 us, c2 185 vs 208) and every c2 (dil 1: k7 275 vs 297, k11 + accumulate 352
+                    # vs 379), while the k7 / k11 c1 convs stay on the LDS-ring kernel (266 vs 279, 366 vs 382)
+                    one = S.gen_ch[i] == 128 and kr in (3, 7, 11) and (kr - 1) * dil <= 64
+                    two = S.gen_ch[i] == 256 and kr in (3, 7, 11) and (kr - 1) * dil <= 64
+                    fr1 = one or (two and kr == 3)
+                    fr2 = one or two
                     res.append(dict(
-                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16 and not fr, frag32=fr,
+                        c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16 and not fr1, frag32=fr1,
                                      x3=xd),
-                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"], lane16=l16 and not fr, frag32=fr,
+                        c2=pack_conv(A, p + ".c2", P[p + ".c2.w"], P[p + ".c2.b"], lane16=l16 and not fr2, frag32=fr2,
                                      x3=xd),
                         a1=A.add(p + ".a1", P[p + ".alpha1"].float()), a2=A.add(p + ".a2", P[p + ".alpha2"].float()),
                         n1=p + ".n1", n2=p + ".n2", k=kr, dil=dil))

@@ -23,7 +23,12 @@ SKS = [int(v) for v in os.environ.get("SK", "0").split(",")]  # split-K counts (
 # ROWS="0,1,2,4": 0 = the LDS-DMA GEMM (gemm_glds), Z >= 1 = the small-M form (csrc/rows.hip) with K in Z slices
 ROWS = [int(v) for v in os.environ.get("ROWS", "0").split(",")]
 cases = [("ffn1 gelu", 512, 2048, torch.bfloat16, L.ACT_GELU, False), ("qkv", 512, 1536, torch.bfloat16, L.ACT_NONE, False),
-         ("out gated f32", 512, 512, torch.float32, L.ACT_NONE, True), ("ffn2 gated f32", 2048, 512, torch.float32, L.ACT_NONE, True)]
+         ("out gated f32", 512, 512, torch.float32, L.ACT_NONE, True), ("ffn2 gated f32", 2048, 512, torch.float32, L.ACT_NONE, True),
+         ("kv", 512, 1024, torch.bfloat16, L.ACT_NONE, False), ("lstm ih f32", 512, 2048, torch.float32, L.ACT_NONE, False)]
+# CASES="kv,qkv": a subset by name prefix (default: the four denoiser layer linears)
+_sel = os.environ.get("CASES")
+cases = [c for c in cases if (_sel is None and c[0] not in ("kv", "lstm ih f32")) or
+         (_sel is not None and any(c[0].startswith(n) for n in _sel.split(",")))]
 for name, K, N, odt, act, gated in cases:
     w = torch.randn(N, K) / math.sqrt(K)
     A = Arena()

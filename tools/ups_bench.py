@@ -17,6 +17,8 @@ from stzs.weights import Arena, pack_conv  # noqa: E402
 
 eng = StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, 0), device="cuda:0")
 B = int(os.environ.get("B", 64))
+FLAGS = int(os.environ.get("FLAGS", "0"), 0)  # 4: skip the epilogue (ablation)
+RES = os.environ.get("RES", "1") != "0"      # 0: no residual operand
 for (T, Ci, Co, s, refl) in [(400, 512, 256, 10, 0), (4000, 256, 128, 6, 1)]:
     w = torch.randn(Ci, Co, 2 * s) / math.sqrt(Co * 2 * s)
     x = Act(torch.randn(B, T, Ci, device="cuda:0").to(torch.bfloat16))
@@ -33,7 +35,8 @@ for (T, Ci, Co, s, refl) in [(400, 512, 256, 10, 0), (4000, 256, 128, 6, 1)]:
         cw.w, cw.b = A[cw.w], A[cw.b]
 
         def run():
-            eng.conv(cw, x, y, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=s // 2, T_final=T * s, refl=refl, res=res)
+            eng.conv(cw, x, y, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=s // 2, T_final=T * s, refl=refl,
+                     res=res if RES else None, flags=FLAGS)
         run()
         torch.cuda.synchronize()
         outs[form] = y.t.clone()
@@ -45,6 +48,6 @@ for (T, Ci, Co, s, refl) in [(400, 512, 256, 10, 0), (4000, 256, 128, 6, 1)]:
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n * 1e3
-        print(f"ups T={T} Ci={Ci} Co={Co} s={s} {form}: {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s  "
+        print(f"ups T={T} Ci={Ci} Co={Co} s={s} {form} flags={FLAGS} res={int(RES)}: {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s  "
               f"{byt / us / 1e3:7.1f} GB/s (HBM roof {byt / 8e12 * 1e6:6.1f} us)", flush=True)
     print("  bit-identical:", torch.equal(outs["lane16"], outs["frag32"]))
