@@ -151,6 +151,13 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * K and Z only (batch-invariant).  Replaces gemm_glds for 100-row linears whose 8-32 tiles would stream all of K
  * through 8-32 CUs (SURVEY §8(a) a2 at B = 1). */
 #define STZS_CONV_ROWS 2048
+/* flags bit (with STZS_CONV_W_FRAG32 and ups > 0, refl in {0, 1}, Co % 128 == 0): the polyphase ConvTranspose with
+ * the generator's 1x1 noise conv fused as ONE extra K-step per 128-column tile (stzs/weights.py pack_ups_noise):
+ * res = the harmonic-source rows [B, T_final + refl, >= 32] bf16 (ldr / bsr; channels past the noise conv's input
+ * width are zero), the weight stream holds (K-steps of the ConvTranspose + 1) per tile, bias = ConvTranspose bias +
+ * noise bias, gate = the noise conv's weights fp32 [Co][32] (the ReflectionPad(1,0) row: its ConvTranspose value is
+ * output row 2's, its noise term row 0's).  y[t] = convT(x)[t] + noise(har)[t] without the noise conv's output. */
+#define STZS_CONV_UPS_NOISE 4096
 size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 

@@ -27,10 +27,14 @@ constexpr int TILE = (ROWS * P + 15) & ~15;
 constexpr int SB = 9;                     // 16 row lanes x 9 >= 129 rows
 constexpr int RING = 4;                   // weight K-steps in flight (3 ahead); divides every NK (8 per chunk)
 
-template <int NCH, bool HR>
+// NZ (STZS_CONV_UPS_NOISE): the 1x1 noise conv fused as one more K-step per column tile whose B operand is the
+// harmonic-source rows of the tile's output rows (loaded at the tile's start, as the residual rows were) and whose
+// weights follow the tile's ConvTranspose K-steps in the stream; there is then no residual operand.
+template <int NCH, bool HR, bool NZ>
 __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_conv_args a, int ctw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NK = NCH * 8;  // K-steps per column tile: chunks x 2 taps x 4
+    constexpr int NKW = NK + (NZ ? 1 : 0);  // weight-stream K-steps per column tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tpb = (a.T_out + BT - 1) / BT;
     const int nx = gridDim.x;
@@ -42,11 +46,12 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
     const int ncol = a.ups * a.Co;
     const int nct = (ncol + 127) / 128;
     const int ct0 = gy * ctw, ct1 = min(nct, ct0 + ctw);
-    const int J = (ct1 - ct0) * NK;  // this workgroup's K-steps over all its tiles
-    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + (long)ct0 * NK * 512 + wave * 128 + lane;
+    const int J = (ct1 - ct0) * NK;  // this workgroup's ConvTranspose K-steps over all its tiles
+    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + (long)ct0 * NKW * 512 + wave * 128 + lane;
     bf16x8 wf[RING][2];
     auto wload = [&](int j, int slot) {  // j >= J: a harmless re-load of the last K-step
-        const bf16x8* p = Wf + (long)(j < J ? j : J - 1) * 512;
+        const int jj = j < J ? j : J - 1;
+        const bf16x8* p = Wf + (long)(NZ ? (jj / NK) * NKW + jj % NK : jj) * 512;
         wf[slot][0] = p[0];
         wf[slot][1] = p[64];
     };
@@ -105,7 +110,7 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
         const int ph = col0 / a.Co, cof = col0 - ph * a.Co;
         const bool col_ok = col0 < ncol;
         const int cofc = col_ok ? cof : 0;
-        uint4 rr[8];
+        uint4 rr[8];  // residual rows (HR) or, fused noise conv (NZ), the harmonic-source B fragments
         int trow[8];
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
@@ -113,7 +118,14 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
             const int t = q * a.ups + ph - a.ups_pad + a.refl;
             trow[mt] = t;
             const int tc = t < 0 ? 0 : (t > t_hi ? t_hi : t);
-            if constexpr (HR) rr[mt] = *reinterpret_cast<const uint4*>(Rb + (long)tc * a.ldr + cofc);
+            if constexpr (NZ) rr[mt] = *reinterpret_cast<const uint4*>(Rb + (long)tc * a.ldr + g * 8);
+            else if constexpr (HR) rr[mt] = *reinterpret_cast<const uint4*>(Rb + (long)tc * a.ldr + cofc);
+        }
+        bf16x8 wn[2];  // the noise conv's A fragments for this tile's 32 columns of the wave
+        if constexpr (NZ) {
+            const bf16x8* pn = Wf + (long)((ct - ct0) * NKW + NK) * 512;
+            wn[0] = pn[0];
+            wn[1] = pn[64];
         }
         float bias[8];
 #pragma unroll
@@ -140,7 +152,29 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (NZ) {  // the fused noise conv: one more K-step on the harmonic-source rows
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                const bf16x8 hf = __builtin_bit_cast(bf16x8, rr[mt]);
+                acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wn[0], hf, acc[0][mt], 0, 0, 0);
+                acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wn[1], hf, acc[1][mt], 0, 0, 0);
+            }
+        }
         if (a.flags & 4) continue;  // diagnostic (tools/ups_bench.py): no epilogue
+        // NZ, ReflectionPad(1,0): output row 0 takes row 2's ConvTranspose value (q = 0: the first row of the
+        // workgroup's first 16-row tile) and row 0's noise term: the correction W_noise (har[0] - har[2]) in fp32,
+        // computed once, outside the unrolled epilogue, by the lanes that hold q = 0
+        float corr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if constexpr (NZ) {
+            if (a.refl && q0 == 0 && n == 0 && trow[0] == 2 && col_ok) {
+#pragma unroll 1
+                for (int j = 0; j < 32; ++j) {
+                    const float d = bf2f(Rb[j]) - bf2f(Rb[2 * a.ldr + j]);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) corr[i] = fmaf(a.gate[(long)(cof + i) * 32 + j], d, corr[i]);
+                }
+            }
+        }
         // epilogue: row q -> t = q ups + p - pad_up (+ refl), valid for q < T_out and t in [0, T_final)
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
@@ -166,7 +200,10 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
             for (int i = 0; i < 8; ++i) v[i] *= a.alpha;
             if (ok) *reinterpret_cast<uint4*>(Y + (long)t * a.ldy + cof) = pack8(v);
             if (a.refl && ok && t == 2) {  // ReflectionPad(1,0): row 0 mirrors source row 1 (+ row 0's residual)
-                if constexpr (HR) {
+                if constexpr (NZ) {  // the accumulator holds row 2's noise term: + W_noise (har[0] - har[2])
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) w0[i] += corr[i];
+                } else if constexpr (HR) {
                     float f[8];
                     load8(Rb + cof, f);
 #pragma unroll
@@ -184,9 +221,13 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
 
 // internal entry (csrc/mrfv.hip routes FRAG32 weights with ups > 0 here)
 __attribute__((visibility("hidden"))) int stzs_ups_conv_launch(const stzs_conv_args& a, hipStream_t s) {
+    const bool nz = (a.flags & STZS_CONV_UPS_NOISE) != 0;
+    if (nz && (!a.res || !a.gate || a.Co % 128 || a.refl < 0 || a.refl > 1 || a.ldr < 32 || a.ldr % 8 || a.bsr % 8 ||
+               (a.refl && a.T_final + a.refl < 3)))
+        return STZS_EINVAL;  // fused noise conv: harmonic-source rows (>= 32 channels) + fp32 noise weights required
     if (a.ks != 2 || a.pad != 1 || a.dil != 1 || a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 32 ||
         a.T_out != a.T_in + 1 || a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.pro_mode != STZS_PRO_NONE ||
-        (a.pro_act != STZS_ACT_LEAKY && a.pro_act != STZS_ACT_NONE) || a.pro_cscale != 1.f || a.gate || a.acc_in ||
+        (a.pro_act != STZS_ACT_LEAKY && a.pro_act != STZS_ACT_NONE) || a.pro_cscale != 1.f || (a.gate && !nz) || a.acc_in ||
         a.stat_part || a.epi_act != STZS_ACT_NONE || a.ldy % 8 || a.bsy % 8 ||
         (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv != 1)) || a.co_pad < a.ups * a.Co)
         return STZS_ESHAPE;
@@ -204,10 +245,10 @@ __attribute__((visibility("hidden"))) int stzs_ups_conv_launch(const stzs_conv_a
     void (*k)(stzs_conv_args, int) = nullptr;
     const bool R = a.res != nullptr;
     switch (nch) {
-        case 1: k = R ? ups_conv<1, true> : ups_conv<1, false>; break;
-        case 2: k = R ? ups_conv<2, true> : ups_conv<2, false>; break;
-        case 3: k = R ? ups_conv<3, true> : ups_conv<3, false>; break;
-        case 4: k = R ? ups_conv<4, true> : ups_conv<4, false>; break;
+        case 1: k = nz ? ups_conv<1, false, true> : R ? ups_conv<1, true, false> : ups_conv<1, false, false>; break;
+        case 2: k = nz ? ups_conv<2, false, true> : R ? ups_conv<2, true, false> : ups_conv<2, false, false>; break;
+        case 3: k = nz ? ups_conv<3, false, true> : R ? ups_conv<3, true, false> : ups_conv<3, false, false>; break;
+        case 4: k = nz ? ups_conv<4, false, true> : R ? ups_conv<4, true, false> : ups_conv<4, false, false>; break;
         default: return STZS_ESHAPE;
     }
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

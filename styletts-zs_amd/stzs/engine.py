@@ -191,6 +191,8 @@ class StyleTTSZS:
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
         # STZS_SMALL_ROWS=0 turns it off.
         self.small_rows = os.environ.get("STZS_SMALL_ROWS", "1") != "0"
+        # the last generator stage's noise conv fused into its ConvTranspose (bf16 engines); STZS_UPS_NOISE=0: off
+        self.ups_noise_fused = os.environ.get("STZS_UPS_NOISE", "1") != "0"
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
@@ -378,8 +380,9 @@ class StyleTTSZS:
             # algorithmic bytes: input tile once + output once (+ residual/acc reads), bf16/f32 as stored, + the
             # weights once (bf16; e4m3 for the fp8 linears; hi + lo for the split-operand precise form)
             wbytes = (cw.ups or 1) * cw.Co * cw.Ci * cw.ks * (1 if cw.f8 else (4 if cw.wx3 is not None else 2))
-            byt = x.B * x.T * x.C * x.t.element_size() + y.B * a.T_out * (cw.ups or 1) * cw.Co * y.t.element_size() * (
-                1 + (res is not None) + (acc_in is not None)) + wbytes
+            opnd = lambda v: v.B * v.T * v.C * v.t.element_size() if v is not None else 0
+            byt = x.B * x.T * x.C * x.t.element_size() + y.B * a.T_out * (cw.ups or 1) * cw.Co * y.t.element_size() + \
+                opnd(res) + opnd(acc_in) + wbytes
             tm["rec"].append((what, e0, e1, flops, byt, (cw.ks, dil, a.T_out, cw.Co), self.stage))
         else:
             self._call(self.lib.stzs_conv1d, a, what)
@@ -1080,13 +1083,21 @@ class StyleTTSZS:
         Tcur = x.T
         Tn = Tcur * r + (1 if last else 0)
         dt = self.dec_dt
+        xu = self.act(f"gen.x{i}", B, Tn, c, dt)
+        nzw = self.W.ups_nz[i] if (self.ups_noise_fused and i < len(self.W.ups_nz)) else None
+        if nzw is not None and dt == torch.bfloat16 and har.ld >= 32:
+            # the 1x1 noise conv fused into the ConvTranspose (csrc/ups.hip STZS_CONV_UPS_NOISE): one more K-step per
+            # column tile on the harmonic-source rows; its output never goes through HBM
+            self.conv(nzw, x, xu, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=(k - r) // 2, T_final=Tcur * r,
+                      refl=1 if last else 0, res=Act(har.t, 0, har.ld), flags=L.CONV_UPS_NOISE,
+                      gate=self._t(nzw.nz32).data_ptr(), what=f"ups{i}")
+            return xu
         xsrc = self.act(f"gen.xsrc{i}", B, Tn, c, dt)
         if not last:
             sf0 = int(np.prod(S.up_rates[i + 1:]))
             self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, stride=sf0, pad=(sf0 + 1) // 2, what=f"noise_conv{i}")
         else:
             self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, what=f"noise_conv{i}")
-        xu = self.act(f"gen.x{i}", B, Tn, c, dt)
         self.conv(W.ups[i], x, xu, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=(k - r) // 2, T_final=Tcur * r,
                   refl=1 if last else 0, res=xsrc, what=f"ups{i}")
         return xu

@@ -49,6 +49,7 @@ class ConvW:
     w32: Optional[object] = None  # fp32 K-step stream (STZS_CONV_W_F32, conv_f32), unpermuted
     frag32: bool = False  # fragment-order packing of the register-direct MRF kernel (STZS_CONV_W_FRAG32)
     wx3: Optional[object] = None  # precise mode: hi | lo bf16 K-step streams (STZS_CONV_W_X3, conv_x3), unpermuted
+    nz32: Optional[object] = None  # fused noise conv (STZS_CONV_UPS_NOISE): its fp32 weights [Co][32]
 
 
 class Arena:
@@ -222,6 +223,41 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
     wn = A.add(name + ".wpk", kstep_stream(wp, cic).to(torch.bfloat16))
     bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
     return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16, w32=w32, wx3=wx3)
+
+
+def pack_ups_noise(A: Arena, name, wu, bu, wn, bn) -> ConvW:
+    """the last generator stage's polyphase ConvTranspose1d with its 1x1 noise conv fused (csrc/ups.hip,
+    STZS_CONV_UPS_NOISE): wu [Ci, Co, 2 r] / bu [Co] the ConvTranspose, wn [Co, C_har, 1] / bn [Co] the noise conv.
+    Weight stream: per 128-column tile the r-phase ConvTranspose K-steps (pack_conv(ups=r, frag32=True)) followed by
+    ONE K-step of the noise conv's weights for the tile's channels (C_har <= 32, zero-padded), fragment order; the
+    bias is bu + bn; nz32 keeps the (bf16-rounded) noise weights in fp32 [Co][32] (the ReflectionPad(1,0) row's
+    correction)."""
+    Ci, Co, k = wu.shape
+    r = k // 2
+    Ch = wn.shape[1]
+    assert Co % 128 == 0 and Ch <= 32 and wn.shape[0] == Co, (name, wu.shape, wn.shape)
+    ncol = r * Co
+    co_pad = _rup(ncol, 128)
+    wk = torch.empty(2, ncol, Ci)
+    for ph in range(r):
+        wk[0, ph * Co:(ph + 1) * Co] = wu[:, :, ph + r].t()
+        wk[1, ph * Co:(ph + 1) * Co] = wu[:, :, ph].t()
+    ci_pad = _rup(Ci, 128)
+    wp = torch.zeros(2, co_pad, ci_pad)
+    wp[:, :ncol, :Ci] = wk
+    wp = wp.view(2, co_pad // 128, 128, ci_pad)[:, :, frag32_perm()].reshape(2, co_pad, ci_pad)
+    su = frag32_stream(wp)                                       # [nct, NK * 512, 8]
+    wnp = torch.zeros(1, co_pad, 128)
+    for ph in range(r):
+        wnp[0, ph * Co:(ph + 1) * Co, :Ch] = wn[:, :, 0]
+    wnp = wnp.view(1, co_pad // 128, 128, 128)[:, :, frag32_perm()].reshape(1, co_pad, 128)
+    sn = frag32_stream(wnp)[:, :512]                             # k-step 0 (k 0..31) of every tile
+    wname = A.add(name + ".wfrn", torch.cat([su, sn], 1).to(torch.bfloat16))
+    bname = A.add(name + ".bpkn", (bu.float() + bn.float()).clone())
+    w32 = torch.zeros(Co, 32)
+    w32[:, :Ch] = wn[:, :, 0].to(torch.bfloat16).float()  # the MFMA K-step's (bf16) weights, in fp32
+    nz = A.add(name + ".nz32", w32)
+    return ConvW(wname, bname, Ci, Co, 2, ci_pad, co_pad, 128, r, False, frag32=True, nz32=nz)
 
 
 def quantize_f8_cols(w: torch.Tensor):
@@ -462,7 +498,7 @@ class PackedModel:
             self.dec_blk[nm] = pack_blk(A, P, nm, up=up, x3=xd)
             dec_norms += blk_norms(nm)
         self.src_merge = A.add("gen.src_merge", torch.cat([P["gen.src_merge.w"].reshape(-1), P["gen.src_merge.b"]]).float())
-        self.noise_conv, self.ups, self.rb = [], [], []
+        self.noise_conv, self.ups, self.rb, self.ups_nz = [], [], [], []
         for i, (r, k) in enumerate(zip(S.up_rates, S.up_kernels)):
             self.noise_conv.append(pack_conv(A, f"gen.noise_conv{i}", P[f"gen.noise_conv{i}.w"], P[f"gen.noise_conv{i}.b"],
                                              x3=xd))
@@ -472,6 +508,13 @@ class PackedModel:
                                       frag32=wu.shape[0] > 64 and wu.shape[1] % 32 == 0,
                                       lane16=wu.shape[0] > 64 and wu.shape[1] % 16 == 0 and wu.shape[1] % 32 != 0,
                                       x3=xd))
+            # the last stage's ConvTranspose with its 1x1 noise conv fused (the noise conv's 393-MB output and the
+            # residual re-read of it at batch 64 never exist): bf16 engines
+            wn = P[f"gen.noise_conv{i}.w"]
+            last = i == len(S.up_rates) - 1
+            self.ups_nz.append(pack_ups_noise(A, f"gen.ups{i}", wu, P[f"gen.ups{i}.b"], wn, P[f"gen.noise_conv{i}.b"])
+                               if last and wn.shape[2] == 1 and wn.shape[1] <= 32 and wu.shape[1] % 128 == 0 and
+                               wu.shape[0] % 128 == 0 else None)
             stage = []
             for j, kr in enumerate(S.rb_kernels):
                 res = []

@@ -173,6 +173,52 @@ def test_convtranspose_staged_once_bit_identical(eng, B, T, Ci, Co, s, refl):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("B,T,Ci,Co,s,Ch", [(2, 300, 256, 128, 6, 22), (3, 129, 256, 128, 6, 22), (1, 40, 512, 256, 4, 20)])
+def test_convtranspose_fused_noise_conv(eng, B, T, Ci, Co, s, Ch):
+    """STZS_CONV_UPS_NOISE (csrc/ups.hip): the last generator stage's ConvTranspose with its 1x1 noise conv fused as
+    one more K-step per column tile == ReflectionPad(1,0)(convT(leaky(x))) + noise_conv(har) in fp32 (the unfused
+    path rounds the noise conv's output to bf16 first), row 0 (the reflected row, which takes row 2's ConvTranspose
+    value and row 0's noise term) included; and within bf16 of the unfused two-launch path."""
+    from stzs import _lib as L
+    from stzs.weights import Arena, pack_conv, pack_ups_noise
+    g = torch.Generator().manual_seed(T + Ch)
+    k, pad = 2 * s, s // 2
+    x = bf(torch.randn(B, T, Ci, generator=g))
+    wu = torch.randn(Ci, Co, k, generator=g) / math.sqrt(Co * k)
+    bu = torch.randn(Co, generator=g) * 0.1
+    wn = torch.randn(Co, Ch, 1, generator=g) / math.sqrt(Ch)
+    bn = torch.randn(Co, generator=g) * 0.1
+    Tn = T * s + 1
+    har = bf(torch.randn(B, Tn, Ch, generator=g))
+    har_d = torch.zeros(B, Tn, 32, dtype=torch.bfloat16, device="cuda:0")
+    har_d[:, :, :Ch] = har.to(torch.bfloat16).cuda()
+    xsrc = torch.einsum("btj,cj->btc", har.double(), bf(wn)[:, :, 0].double()) + bn.double()
+    ref = convT_ref(x, wu, bu, stride=s, pad=pad, refl=1, pro_act="leaky", slope=0.1, res=xsrc.float())
+    A = Arena()
+    cw = pack_ups_noise(A, "t", wu, bu, wn, bn)
+    A.finalize("cuda:0")
+    cw.w, cw.b, cw.nz32 = A[cw.w], A[cw.b], A[cw.nz32]
+    yd = _act(torch.full((B, Tn, Co), float("nan"), dtype=torch.bfloat16, device="cuda:0"))
+    eng.conv(cw, _act(x.to(torch.bfloat16).cuda()), yd, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=pad, T_final=T * s,
+             refl=1, res=_act(har_d), flags=L.CONV_UPS_NOISE, gate=cw.nz32.data_ptr())
+    torch.cuda.synchronize()
+    y = yd.t.float().cpu()
+    e, e0 = max_rel(y, ref), max_rel(y[:, :1], ref[:, :1])
+    # the unfused path: noise conv (bf16 output) as the ConvTranspose's residual
+    cn, _An = _pack(wn, bn)
+    xs = _act(torch.zeros(B, Tn, Co, dtype=torch.bfloat16, device="cuda:0"))
+    eng.conv(cn, _act(har_d, Ch), xs)
+    cu, _Au = _pack(wu, bu, ups=s, frag32=True)
+    yu = _act(torch.zeros(B, Tn, Co, dtype=torch.bfloat16, device="cuda:0"))
+    eng.conv(cu, _act(x.to(torch.bfloat16).cuda()), yu, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=pad,
+             T_final=T * s, refl=1, res=xs)
+    torch.cuda.synchronize()
+    eu = max_rel(yu.t.float().cpu(), y)
+    print(B, T, Ci, Co, s, "fused noise conv vs fp32", e, "row 0", e0, "vs unfused", eu)
+    assert torch.isfinite(y).all()
+    assert e < 1.5e-2 and e0 < 1.5e-2 and eu < 2e-2
+
+
 def test_chan_stats(eng):
     """InstanceNorm statistics: fp32 partials + fixed-order fp64 combine; 1e-5 relative."""
     g = torch.Generator().manual_seed(3)
