@@ -22,6 +22,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=fast", "-Wall",
          "-Wno-unused-result", f"-I{INCLUDE}"]
+# per-file extra flags (the host compile ignores the gfx950 target feature with a warning).  source.hip: no packed
+# fp32 VALU ops -- its STFT tail, compiled to v_pk_fma_f32 with op_sel / neg modifiers, stored wrong imaginary bins
+# for 16-lane groups in ~1 of 3 two-shard concurrent replays (timing-dependent: never in a sequential replay);
+# without packed ops, 0 of 120 (tools/two_shard_stress.py)
+FILE_FLAGS = {"source.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]}
 
 
 def sources():
@@ -38,7 +43,7 @@ def _compile(src, force, verbose):
     obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= _deps_mtime(src):
         return obj
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -250,7 +250,28 @@ def test_two_shard_streams_match_eager(v0, c2, branch_streams):
     for s in streams:
         cur.wait_stream(s)
     conc_ok = check("concurrent")
-    assert seq_ok and conc_ok
+    # the concurrent pattern again and again (shard 0's last back phase overlaps shard 1's front): in r03 a harmonic-
+    # source kernel built with packed-fp32 FMAs wrote wrong STFT bins for 16 frames in ~1 of 3 such passes (and only
+    # under this overlap; tools/two_shard_stress.py) -- every pass must match
+    bad = []
+    for it in range(12):
+        for s in streams:
+            s.wait_stream(cur)
+        for rep in range(2):
+            for j, (s, (ga, gb)) in enumerate(zip(streams, pairs)):
+                with torch.cuda.stream(s):
+                    if rep == 0 and j == 1:
+                        s.wait_event(ev)
+                    ga.replay()
+                    if rep == 0 and j == 0:
+                        ev.record(s)
+                    gb.replay()
+        for s in streams:
+            cur.wait_stream(s)
+        torch.cuda.synchronize()
+        bad += [(it, i) for i in range(2) if not torch.equal(res[i].cpu(), g["wav"][i * nb:(i + 1) * nb])]
+    print(f"repeated concurrent passes: {len(bad)} shard mismatches in 12 x 2 {bad[:6]}")
+    assert seq_ok and conc_ok and not bad
 
 
 def test_latency_engine_batch_invariant(v0):
