@@ -158,6 +158,10 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * noise bias, gate = the noise conv's weights fp32 [Co][32] (the ReflectionPad(1,0) row: its ConvTranspose value is
  * output row 2's, its noise term row 0's).  y[t] = convT(x)[t] + noise(har)[t] without the noise conv's output. */
 #define STZS_CONV_UPS_NOISE 4096
+/* flags bit (FRAG32 weights, Snake prologue, ci_pad > 128, co_pad % 256 == 0): keep the register-direct MRF conv at
+ * 128 output channels per workgroup instead of its default wide form (256 per workgroup: every staged input row
+ * transformed once per 256 channels instead of once per 128).  Bit-identical either way; an A/B switch. */
+#define STZS_CONV_MRFV_NARROW 8192
 size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 

@@ -33,10 +33,25 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
+def _includes(path, seen):
+    """the quoted #include files of `path`, recursively (csrc/ headers and include/stzs.h)"""
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith("#include") and '"' in line:
+                name = line.split('"')[1]
+                for d in (os.path.dirname(path), CSRC, INCLUDE):
+                    q = os.path.join(d, name)
+                    if os.path.exists(q):
+                        if q not in seen:
+                            seen.add(q)
+                            _includes(q, seen)
+                        break
+    return seen
+
+
 def _deps_mtime(src):
-    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
-    hdrs.append(os.path.join(INCLUDE, "stzs.h"))
-    return max(os.path.getmtime(p) for p in [src] + hdrs)
+    return max(os.path.getmtime(p) for p in [src] + sorted(_includes(src, set())))
 
 
 def _compile(src, force, verbose):

@@ -1,158 +1,17 @@
 // Denoiser multi-head attention: self-attention over the L_s = 50 style codes
 // and cross-attention to [text ; prompt] context (T_txt + 50 keys), head dim 64.
 //
-// Flash-style on v_mfma_f32_16x16x32_bf16: one workgroup (4 waves) per (row, head, 64 queries), one
-// wave per 16 queries.  Keys stream through LDS in 64-key chunks: K as rows (B operand of S = Q K^T),
-// V transposed (B operand of O = P V), both 16-B padded.  Online softmax in fp32 on the accumulator
-// layout (row max / sum by in-register max + 16-lane xor shuffles); P goes C-layout -> A-layout through
-// a per-wave bf16 LDS tile.  Q fragments come straight from global memory (read once).
-#include "common.hpp"
+// bf16: the flash unit of csrc/attn_body.hpp, one workgroup per (row, head, 64 queries).
+#include "attn_body.hpp"
 
 namespace {
 
-constexpr int KC = 64;  // keys per chunk
+constexpr int KC = stzs_attn::KC;  // keys per chunk
 
 template <int DH>
 __global__ __launch_bounds__(256) void attn_mfma(const stzs_attn_args a) {
-    constexpr int NKS = DH / 32;   // k-steps of S
-    constexpr int NDT = DH / 16;   // d tiles of O
-    constexpr int KP = DH + 8;     // K row pitch (bf16)
-    constexpr int VP = KC + 8;     // V^T row pitch
-    constexpr int PP = KC + 8;     // P row pitch
-    __shared__ __attribute__((aligned(16))) bf16_t Ks[KC * KP];
-    __shared__ __attribute__((aligned(16))) bf16_t Vt[DH * VP];
-    __shared__ __attribute__((aligned(16))) bf16_t Ps[4][16 * PP];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const long r = blockIdx.x;
-    const int h = blockIdx.y;
-    const int qb = blockIdx.z * 64 + wave * 16;
-    const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + r * a.bsq + h * DH;
-    const bf16_t* K = reinterpret_cast<const bf16_t*>(a.k) + r * a.bsk + h * DH;
-    const bf16_t* V = reinterpret_cast<const bf16_t*>(a.v) + r * a.bsv + h * DH;
-    const float scale = 1.f / sqrtf((float)DH);
-
-    bf16x8 qf[NKS];
-    {
-        const int qr = min(qb + (lane & 15), a.Lq - 1);
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks)
-            qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (long)qr * a.ldq + ks * 32 + 8 * (lane >> 4));
-    }
-    f32x4 o[NDT];
-#pragma unroll
-    for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m[4], l[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        m[i] = -INFINITY;
-        l[i] = 0.f;
-    }
-    bf16_t* P = Ps[wave];
-
-    // K / V chunk loads run one chunk ahead in registers: chunk c + 1's global loads are in flight while chunk c
-    // is computed (cross-attention: 3 chunks of 64 keys), the LDS images are written from the registers
-    constexpr int NLD = KC * (DH / 8) / 256;  // 16-B K (and V) words per thread per chunk
-    static_assert(KC * (DH / 8) % 256 == 0, "whole chunk per pass");
-    uint4 pk[NLD], pv[NLD];
-    auto load_chunk = [&](int c0) {
-#pragma unroll
-        for (int j = 0; j < NLD; ++j) {
-            const int i = tid + j * 256;
-            const int kr = i / (DH / 8), cv = i - kr * (DH / 8);
-            const bool ok = c0 + kr < a.Lk;
-            const int kk = ok ? c0 + kr : 0;
-            pk[j] = *reinterpret_cast<const uint4*>(K + (long)kk * a.ldk + cv * 8);
-            pv[j] = *reinterpret_cast<const uint4*>(V + (long)kk * a.ldv + cv * 8);
-            if (!ok) pk[j] = pv[j] = make_uint4(0, 0, 0, 0);
-        }
-    };
-    load_chunk(0);
-    for (int c0 = 0; c0 < a.Lk; c0 += KC) {
-        __syncthreads();
-        // stage K rows and V^T for keys [c0, c0 + KC) from the registers, then start the next chunk's loads
-#pragma unroll
-        for (int j = 0; j < NLD; ++j) {
-            const int i = tid + j * 256;
-            const int kr = i / (DH / 8), cv = i - kr * (DH / 8);
-            const uint4 kv = pk[j], vv = pv[j];
-            *reinterpret_cast<uint4*>(Ks + kr * KP + cv * 8) = kv;
-            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                Vt[(cv * 8 + 2 * q) * VP + kr] = (bf16_t)(w[q] & 0xFFFF);
-                Vt[(cv * 8 + 2 * q + 1) * VP + kr] = (bf16_t)(w[q] >> 16);
-            }
-        }
-        if (c0 + KC < a.Lk) load_chunk(c0 + KC);
-        __syncthreads();
-        // S = Q K^T for 16 queries x 64 keys
-        f32x4 s[4];
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (nt * 16 + (lane & 15)) * KP + ks * 32 + 8 * (lane >> 4));
-                s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, s[nt], 0, 0, 0);
-            }
-        }
-        // online softmax; element (row = (lane>>4)*4 + i, key = nt*16 + (lane & 15))
-        float alpha[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float mx = -INFINITY;
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const bool ok = c0 + nt * 16 + (lane & 15) < a.Lk;
-                s[nt][i] = ok ? s[nt][i] * scale : -INFINITY;
-                mx = fmaxf(mx, s[nt][i]);
-            }
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-            const float mn = fmaxf(m[i], mx);
-            alpha[i] = __expf(m[i] - mn);
-            float sum = 0.f;
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const float pv = __expf(s[nt][i] - mn);
-                s[nt][i] = pv;
-                sum += pv;
-            }
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
-            l[i] = l[i] * alpha[i] + sum;
-            m[i] = mn;
-        }
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[dt][i] *= alpha[i];
-        // P -> LDS (C layout) -> A fragments
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) P[((lane >> 4) * 4 + i) * PP + nt * 16 + (lane & 15)] = f2bf(s[nt][i]);
-        __syncthreads();
-#pragma unroll
-        for (int ks = 0; ks < KC / 32; ++ks) {
-            const bf16x8 pf = *reinterpret_cast<const bf16x8*>(P + (lane & 15) * PP + ks * 32 + 8 * (lane >> 4));
-#pragma unroll
-            for (int dt = 0; dt < NDT; ++dt) {
-                const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vt + (dt * 16 + (lane & 15)) * VP + ks * 32 + 8 * (lane >> 4));
-                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[dt], 0, 0, 0);
-            }
-        }
-    }
-    bf16_t* O = reinterpret_cast<bf16_t*>(a.o) + r * a.bso + h * DH;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int q = qb + (lane >> 4) * 4 + i;
-        if (q < a.Lq) {
-            const float inv = 1.f / l[i];
-#pragma unroll
-            for (int dt = 0; dt < NDT; ++dt) O[(long)q * a.ldo + dt * 16 + (lane & 15)] = f2bf(o[dt][i] * inv);
-        }
-    }
+    __shared__ __attribute__((aligned(16))) unsigned char lds[stzs_attn::Lds<DH>::BYTES];
+    stzs_attn::attn_unit<DH, stzs_attn::LdPlain>(a, blockIdx.x, blockIdx.y, blockIdx.z * 64, lds);
 }
 
 // PRECISE mode (stzs_attn_args.precise = 1): fp32 q / k / v / o.  The same flash structure on the same MFMAs

@@ -59,8 +59,14 @@ STZS_DEV void row_sum16_n(float* x) {
 // during the staging, so the kernel fits 3 workgroups per CU; NCH = 0: any number of chunks, 2 per CU.
 // AL: the epilogue scales by a.alpha (alpha != 1; a uniform runtime test was if-converted into a multiply + select
 // per element)
-template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL>
+// WPW: 32-channel weight groups per wave.  1: a workgroup owns 128 output channels; 2 (the wide form, multi-chunk
+// inputs with co_pad % 256 == 0): 256, so a 256-channel layer stages (loads + AdaIN + Snake) each input row ONCE
+// instead of once per 128-channel tile, and every B fragment read from LDS feeds 4 MFMAs instead of 2.  Same K
+// order per output element either way (bit-identical).
+template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1>
 __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
+    static_assert(WPW == 1 || (WPW == 2 && NCH != 1), "the wide form is for multi-chunk inputs");
+    constexpr int NA = 2 * WPW;  // A fragments (16 output channels each) per wave and K-step
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NKC = KS * 4;  // 32-wide K-steps per 128-channel chunk
     const int dil = a.dil;
@@ -76,14 +82,17 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     const int t0 = (bx - bq * tpb) * BT;
     const int nchunk = NCH ? NCH : a.ci_pad >> 7;
     constexpr int SB = sb_rows(KS);
-    // weights: [co tile][chunk][tap][kq][wave][nt][lane][8] bf16 -> 512 bf16x8 per K-step
-    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + ((long)by * nchunk * NKC) * 512 + wave * 128 + lane;
-    auto wload = [&](bf16x8 (&w)[2], int kk) {
+    // weights: [co tile][chunk][tap][kq][wave][nt][lane][8] bf16 -> 512 bf16x8 per K-step.  Wide form: wave w takes
+    // the packed waves 2 (w & 1) and 2 (w & 1) + 1 of 128-channel tile 2 by + (w >> 1) -- consecutive in the stream
+    const int ct = WPW == 1 ? by : by * 2 + (wave >> 1);
+    const int ow0 = WPW == 1 ? wave : (wave & 1) * 2;
+    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + ((long)ct * nchunk * NKC) * 512 + ow0 * 128 + lane;
+    auto wload = [&](bf16x8 (&w)[NA], int kk) {
         const bf16x8* p = Wf + (long)kk * 512;
-        w[0] = p[0];
-        w[1] = p[64];
+#pragma unroll
+        for (int j = 0; j < NA; ++j) w[j] = p[64 * j];
     };
-    f32x4 acc[2][8];
+    f32x4 acc[NA][8];
 
     const int xoff0 = (lane & 15) * P + (lane >> 4) * 16;
     const int dP = dil * P;
@@ -92,8 +101,10 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 #ifndef STZS_MRFV_PD
 #define STZS_MRFV_PD 2
 #endif
-    constexpr int PD = STZS_MRFV_PD;  // weight K-steps in flight ahead of the MFMAs
-    bf16x8 wf[PD + 1][2];
+    // weight K-steps in flight ahead of the MFMAs (the wide form's K-step is twice as long: one is as far ahead in
+    // time, and two spill its 256 VGPRs)
+    constexpr int PD = WPW == 2 ? 1 : STZS_MRFV_PD;
+    bf16x8 wf[PD + 1][NA];
     bf16x8 xf[8];
 
     for (int cc = 0; cc < nchunk; ++cc) {
@@ -220,16 +231,17 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
                     const bool z = FIRST && s == 0;
-                    acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % (PD + 1)][0], xf[mt], z ? zero : acc[0][mt], 0, 0, 0);
-                    acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % (PD + 1)][1], xf[mt], z ? zero : acc[1][mt], 0, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < NA; ++j)
+                        acc[j][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % (PD + 1)][j], xf[mt], z ? zero : acc[j][mt], 0, 0, 0);
                     if (sn < NKC) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + offn + mt * 16 * P);
                 }
                 if (s + 2 < NKC) {
-                    __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // the two weight loads first
+                    __builtin_amdgcn_sched_group_barrier(0x020, NA, 0);  // the weight loads first
                 }
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
                     if (sn < NKC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -240,7 +252,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
         } else {  // (two K-loop bodies spill the multi-chunk forms: zero the accumulators once instead)
             if (cc == 0) {
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < NA; ++i)
 #pragma unroll
                     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
@@ -251,12 +263,6 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 
     // ---------------- epilogue: lane (g, n): time t = t0 + mt*16 + n, channels co0 .. co0 + 7
     const int g = lane >> 4, n = lane & 15;
-    const int co0 = by * BCO + wave * 32 + g * 8;
-    const bool col_ok = co0 < a.Co;
-    const int coc = col_ok ? co0 : 0;
-    float bias[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
     const bool stat = a.stat_part != nullptr;
     // residual rows at t / res_tdiv; the Snake (MRF) forms always have res_tdiv 1 (checked by the launcher)
     constexpr bool TD1 = PACT == STZS_ACT_SNAKE;
@@ -264,6 +270,14 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     const char* Aq = reinterpret_cast<const char*>(a.acc_in) + (long)bq * a.bsa * 2;
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
     const int nch = (a.T_out + 63) / 64;
+#pragma unroll
+    for (int sw = 0; sw < WPW; ++sw) {  // (wide form: the wave's two 32-channel groups one after the other)
+    const int co0 = ct * BCO + (ow0 + sw) * 32 + g * 8;
+    const bool col_ok = co0 < a.Co;
+    const int coc = col_ok ? co0 : 0;
+    float bias[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
     // the residual / accumulate rows of BOTH halves in flight at once (the second half's HBM latency hides
     // behind the first half's epilogue); uniform utterance bases + 32-bit per-lane offsets
     uint4 rr[8], aa[8];
@@ -291,7 +305,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[nt][mt][r] + bias[nt * 4 + r];
+                for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[sw * 2 + nt][mt][r] + bias[nt * 4 + r];
             if constexpr (HR) {
                 float f[8];
                 unpack8(rr[mt], f);
@@ -334,19 +348,21 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
             }
         }
     }
+    }
 }
 
-template <int PACT, bool HR, bool HA, int NCH, bool AL>
+template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1>
 void (*pick_ks(int ks))(stzs_conv_args) {
     switch (ks) {
-        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL>;
-        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL>;
-        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH, AL>;
+        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL, WPW>;
+        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL, WPW>;
+        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH, AL, WPW>;
         default: return nullptr;
     }
 }
 template <int PACT, bool HR, bool HA>
-void (*pick(int ks, bool one, bool al))(stzs_conv_args) {
+void (*pick(int ks, bool one, bool al, bool wide))(stzs_conv_args) {
+    if (wide) return al ? pick_ks<PACT, HR, HA, 0, true, 2>(ks) : pick_ks<PACT, HR, HA, 0, false, 2>(ks);
     if (al) return one ? pick_ks<PACT, HR, HA, 1, true>(ks) : pick_ks<PACT, HR, HA, 0, true>(ks);
     return one ? pick_ks<PACT, HR, HA, 1, false>(ks) : pick_ks<PACT, HR, HA, 0, false>(ks);
 }
@@ -374,11 +390,14 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + CS_BYTES;
     void (*k)(stzs_conv_args) = nullptr;
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
+    // the wide form (256 output channels per workgroup) for multi-chunk Snake convs, unless STZS_CONV_MRFV_NARROW
+    const bool wide = a.pro_act == STZS_ACT_SNAKE && a.ci_pad > 128 && a.co_pad % (2 * BCO) == 0 &&
+                      !(a.flags & STZS_CONV_MRFV_NARROW);
     if (a.pro_act == STZS_ACT_SNAKE) {
         const bool one = a.ci_pad == 128;
         const bool al = a.alpha != 1.f;
-        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al))
-              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al));
+        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide))
+              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide));
     } else if (!A && a.ks == 3) {  // the AdaIN residual blocks of the decoder / prosody predictor
         if (a.pro_act == STZS_ACT_LEAKY)
             k = R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true>;
@@ -387,7 +406,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     }
     if (!k) return STZS_ESHAPE;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / BCO);
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / (wide ? 2 * BCO : BCO));
     hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;

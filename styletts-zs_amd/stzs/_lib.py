@@ -26,6 +26,7 @@ CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD
 CONV_MRF_PIPE = 512  # include/stzs.h STZS_CONV_MRF_PIPE (k3 residual MRF convs on csrc/mrfp.hip, opt-in)
 CONV_ROWS = 2048  # include/stzs.h STZS_CONV_ROWS (small-M linear on the whole chip, csrc/rows.hip)
 CONV_UPS_NOISE = 4096  # include/stzs.h STZS_CONV_UPS_NOISE (ConvTranspose + fused 1x1 noise conv, csrc/ups.hip)
+CONV_MRFV_NARROW = 8192  # include/stzs.h STZS_CONV_MRFV_NARROW (register-direct MRF conv at 128 channels per workgroup)
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -67,6 +68,14 @@ class AttnArgs(C.Structure):
     _fields_ = [("q", vp), ("k", vp), ("v", vp), ("o", vp)] + \
                [(n, i64) for n in ("ldq", "ldk", "ldv", "ldo", "bsq", "bsk", "bsv", "bso")] + \
                [(n, i32) for n in ("R", "Lq", "Lk", "heads", "dh", "precise")]
+
+
+class RowsFuse(C.Structure):
+    """stzs_rows_fuse (include/stzs_fused.h): the consumer fused into a small-M linear's launch"""
+    _fields_ = [("mode", i32), ("pad0", i32), ("ctr", vp), ("ln", RowLNArgs), ("attn", AttnArgs)]
+
+
+FUSE_LN, FUSE_ATTN = 1, 2  # include/stzs_fused.h
 
 
 class LstmArgs(C.Structure):
@@ -211,6 +220,8 @@ EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_co
            "stzs_dn_cond", "stzs_dn_cond_steps", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed", "stzs_embed_f32", "stzs_dn_cond_steps_f32", "stzs_pack_conv_size", "stzs_pack_conv",
            "stzs_pack_lstm", "stzs_pack_lstm_x3"] + [f"stzs_{o}{sfx}" for o in GENERIC_OPS for sfx in ("", "_workspace")]
+# include/stzs_fused.h
+EXPORTS_FUSED = ["stzs_rows_fuse_counters", "stzs_conv_rows_fused"]
 
 _lib = None
 
@@ -236,6 +247,8 @@ def load():
         "stzs_conv1d": ([P(ConvArgs), vp], i32),
         "stzs_conv_splitk_workspace": ([i64, i32, i32], C.c_size_t),
         "stzs_conv_rows_workspace": ([i64, i32, i32], C.c_size_t),
+        "stzs_rows_fuse_counters": ([P(ConvArgs), P(RowsFuse)], C.c_size_t),
+        "stzs_conv_rows_fused": ([P(ConvArgs), P(RowsFuse), vp], i32),
         "stzs_chan_stats_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
         "stzs_chan_stats_final": ([P(StatsArgs), i32, vp], i32),

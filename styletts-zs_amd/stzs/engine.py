@@ -140,7 +140,8 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
-                 packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None, dn_rows=None):
+                 packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None, dn_rows=None,
+                 fuse_rows=False):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
@@ -186,6 +187,11 @@ class StyleTTSZS:
         # small-M whole-chip form of the bf16 denoiser linears (csrc/rows.hip): {linear: K slices}; a per-engine
         # property of the weight like dn_splitk (batch-invariant), taking precedence over it
         self.dn_rows = _table_env("STZS_DN_ROWS", DN_ROWS) if dn_rows is None else dict(dn_rows)
+        # the consumers of the small-M denoiser linears fused into their launches (include/stzs_fused.h: the
+        # LayerNorm after the residual linears, the attention after the q / qkv linears; bit-identical, 31 launches
+        # fewer per NFE); STZS_FUSE_ROWS=0 / 1 overrides the constructor
+        fz = os.environ.get("STZS_FUSE_ROWS")
+        self.fuse_rows = bool(fuse_rows) if fz is None else fz != "0"
         # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
         # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
@@ -282,9 +288,12 @@ class StyleTTSZS:
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
-             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, splitk=0, rows=0, what="conv"):
+             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, splitk=0, rows=0, attn=None,
+             what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
-        output fused into the conv epilogue (per-tile partials) + one small finalize launch."""
+        output fused into the conv epilogue (per-tile partials) + one small finalize launch.
+        post_ln (stzs_rowln_args) / attn ((q, k, v, o) Acts): the LayerNorm / attention that consumes y, launched
+        behind the linear, or folded into its launch on the fused small-M form (fuse_rows, include/stzs_fused.h)."""
         W = self.W
         a = L.ConvArgs()
         a.x, a.w, a.y = x.ptr, self._t(cw.w).data_ptr(), y.ptr
@@ -360,6 +369,16 @@ class StyleTTSZS:
             assert nb > 0, (what, splitk)
             a.splitk, a.splitk_ws = splitk, self._scratch("sk_ws", nb // 4).data_ptr()
             a.splitk_ctr = self._counters("sk_ctr", nb // (splitk * 32768)).data_ptr()
+        fz = None
+        if (a.flags & L.CONV_ROWS) and self.fuse_rows and (post_ln is not None or attn is not None):
+            fz = L.RowsFuse()
+            if post_ln is not None:
+                fz.mode, fz.ln = L.FUSE_LN, post_ln
+            else:
+                fz.mode, fz.attn = L.FUSE_ATTN, self._attn_args(*attn)
+            n = self.lib.stzs_rows_fuse_counters(C.byref(a), C.byref(fz))
+            assert n > 0, what
+            fz.ctr = self._counters("fuse_ctr", n).data_ptr()
         st = None
         if stats_key is not None:
             Cc = _rup(cw.Co, 8)
@@ -369,12 +388,14 @@ class StyleTTSZS:
             st = (slab, Cc, self.buf(stats_key + ".m", (y.B, Cc), torch.float32),
                   self.buf(stats_key + ".r", (y.B, Cc), torch.float32))
         tm = self.timer
+        launch = (lambda: self.lib.stzs_conv1d(C.byref(a), self.stream())) if fz is None else \
+            (lambda: self.lib.stzs_conv_rows_fused(C.byref(a), C.byref(fz), self.stream()))
         if tm is not None and (tm["all"] or what in tm["tags"]):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
             self.launches += 1
-            L.check(self.lib.stzs_conv1d(C.byref(a), self.stream()), what)
+            L.check(launch(), what)
             e1.record()
             flops = 2.0 * y.B * a.T_out * (cw.ups or 1) * cw.Co * cw.Ci * cw.ks
             # algorithmic bytes: input tile once + output once (+ residual/acc reads), bf16/f32 as stored, + the
@@ -384,10 +405,15 @@ class StyleTTSZS:
             byt = x.B * x.T * x.C * x.t.element_size() + y.B * a.T_out * (cw.ups or 1) * cw.Co * y.t.element_size() + \
                 opnd(res) + opnd(acc_in) + wbytes
             tm["rec"].append((what, e0, e1, flops, byt, (cw.ks, dil, a.T_out, cw.Co), self.stage))
-        else:
+        elif fz is None:
             self._call(self.lib.stzs_conv1d, a, what)
-        if post_ln is not None:  # the LayerNorm that consumes this linear's output (stzs_rowln_args)
+        else:
+            self.launches += 1
+            L.check(launch(), what + ".fused")
+        if post_ln is not None and fz is None:  # the LayerNorm that consumes this linear's output (stzs_rowln_args)
             self._call(self.lib.stzs_row_layernorm, post_ln, what + ".ln", cost=_ln_cost(post_ln))
+        if attn is not None and fz is None:  # the attention whose q (k, v) this linear produced
+            self.attention(*attn)
         if st is None:
             return y
         slab, Cc, mean, rstd = st
@@ -504,7 +530,7 @@ class StyleTTSZS:
         assert x.ld * x.T == x.bs and y.ld * y.T == y.bs
         self._call(self.lib.stzs_quant_rows, a, what, cost=(0, a.R * a.C * (x.t.element_size() + 1)))
 
-    def attention(self, q: Act, k: Act, v: Act, o: Act):
+    def _attn_args(self, q: Act, k: Act, v: Act, o: Act):
         S = self.spec
         a = L.AttnArgs()
         a.q, a.k, a.v, a.o = q.ptr, k.ptr, v.ptr, o.ptr
@@ -512,6 +538,10 @@ class StyleTTSZS:
         a.bsq, a.bsk, a.bsv, a.bso = q.bs, k.bs, v.bs, o.bs
         a.R, a.Lq, a.Lk, a.heads, a.dh = q.B, q.T, k.T, S.dn_heads, S.dn_head_dim
         a.precise = int(q.t.dtype == torch.float32)  # fp32 operands: the fp32 attention kernel
+        return a
+
+    def attention(self, q: Act, k: Act, v: Act, o: Act):
+        a = self._attn_args(q, k, v, o)
         self._call(self.lib.stzs_attention, a, "attention",
                    cost=(4.0 * a.R * a.heads * a.Lq * a.Lk * a.dh,
                          a.R * (2 * a.Lq + 2 * a.Lk) * a.heads * a.dh * q.t.element_size()))
@@ -773,7 +803,6 @@ class StyleTTSZS:
             s_ff = self.buf("dn.ff8s", (R * Ls,), torch.float32)
         co = edm_coeffs(S, st["sig"][i])
         rk = {} if (f8 or self.adt == torch.float32) else self.dn_rows
-        self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, rows=rk.get("inp", 0), what="dn.in")
         if f8:
             ain, sin, sfx = an8, s_an, "8"
         else:
@@ -792,20 +821,19 @@ class StyleTTSZS:
                                      y_scale=sin))
         fb = fmodx[0, i * R].data_ptr()
         lns.append(self._ln_args(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls))
-        self._call(self.lib.stzs_row_layernorm, lns[0], "ln1", cost=_ln_cost(lns[0]))
+        self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, rows=rk.get("inp", 0), post_ln=lns[0], what="dn.in")
         sk = {} if (f8 or self.adt == torch.float32) else self.dn_splitk
         for l, lw in enumerate(W.dn_layers):
             mb = modx[l, i * R].data_ptr()
             self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, splitk=sk.get("qkv", 0), rows=rk.get("qkv", 0),
-                      what="qkv")
-            self.attention(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o)
+                      attn=(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o), what="qkv")
             xo, so = (o8, s_o) if f8 else (o, None)
             if f8:
                 self.quant(o, o8, s_o)
             self.conv(lw["o" + sfx], xo, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=so,
                       post_ln=lns[3 * l + 1], splitk=sk.get("o", 0), rows=rk.get("o", 0), what="sa_o")
-            self.conv(lw["q" + sfx], ain, q, x_scale=sin, splitk=sk.get("q", 0), rows=rk.get("q", 0), what="ca_q")
-            self.attention(q, kv[l].sl(0, d), kv[l].sl(d, d), o)
+            self.conv(lw["q" + sfx], ain, q, x_scale=sin, splitk=sk.get("q", 0), rows=rk.get("q", 0),
+                      attn=(q, kv[l].sl(0, d), kv[l].sl(d, d), o), what="ca_q")
             if f8:
                 self.quant(o, o8, s_o)
             self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=lns[3 * l + 2], splitk=sk.get("co", 0),
@@ -1372,7 +1400,8 @@ def latency_engine(spec: Spec, packed: PackedModel, device="cuda:0") -> "StyleTT
     """the batch-1 serving engine bench.py times for the configs[1] p50 (and tests/test_gpu_configs.py checks against
     the oracle): the same packed weights, the denoiser layer linears on the whole-chip small-M form
     (LATENCY_DN_ROWS, csrc/rows.hip) and split-K ffn2 wherever the rows form does not apply (LATENCY_DN_SPLITK)."""
-    return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS)
+    return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS,
+                      fuse_rows=True)
 
 
 class CheckedGraph:

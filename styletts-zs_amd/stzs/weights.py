@@ -521,15 +521,15 @@ class PackedModel:
                 for m, dil in enumerate(S.rb_dils):
                     p = f"gen.rb{i}.{j}.{m}"
                     l16 = S.gen_ch[i] % 128 == 0 and (kr - 1) * dil <= 64  # MRF kernel (csrc/mrf.hip)
-                    # the register-direct MRF kernel (csrc/mrfv.hip; bit-identical to mrf.hip) where it measured
-                    # faster (tools/mrfv_bench.py, B = 64, profiles/r02_mrfv_bench_s.log): every conv with one
-                    # 128-channel input chunk (stage 1: 3 workgroups per CU, 8-18%); with two chunks (stage 0) the k3
-                    # convs (155 vs 168 us, c2 185 vs 208) and every c2 (dil 1: k7 275 vs 297, k11 + accumulate 352
-                    # vs 379), while the k7 / k11 c1 convs stay on the LDS-ring kernel (266 vs 279, 366 vs 382)
+                    # the register-direct MRF kernel (csrc/mrfv.hip; bit-identical to mrf.hip) for every generator
+                    # conv: with one 128-channel input chunk (stage 1: 3 workgroups per CU, 8-18% faster than the
+                    # LDS-ring kernel, profiles/r02_mrfv_bench_s.log) and, in its wide form (256 output channels per
+                    # workgroup, each staged input row transformed once), with two (stage 0, B = 64,
+                    # profiles/r03_r_mrfv_wide.log: k3 c1 131 vs 175 us on the LDS ring, k7 d3 c1 255 vs 279,
+                    # k11 d5 c1 352 vs 401, c2 / c2 + accumulate 7-17% faster, k11 c2 level)
                     one = S.gen_ch[i] == 128 and kr in (3, 7, 11) and (kr - 1) * dil <= 64
                     two = S.gen_ch[i] == 256 and kr in (3, 7, 11) and (kr - 1) * dil <= 64
-                    fr1 = one or (two and kr == 3)
-                    fr2 = one or two
+                    fr1 = fr2 = one or two
                     res.append(dict(
                         c1=pack_conv(A, p + ".c1", P[p + ".c1.w"], P[p + ".c1.b"], lane16=l16 and not fr1, frag32=fr1,
                                      x3=xd),

@@ -266,6 +266,8 @@ MRF_CASES = [
     (9, 4000, 128, 128, 7, 3, "snake", True, False, True, 1),    # c2 form + stats (288 tiles)
     (2, 777, 256, 256, 7, 1, "snake", True, True, True, 1),      # stage-0 width: 2 input chunks x 2 column tiles
     (1, 129, 256, 256, 3, 5, "snake", False, False, True, 1),    # ragged: the second row tile has 1 valid row
+    (2, 500, 384, 256, 11, 3, "snake", True, False, True, 1),    # 3 input chunks, wide (256-channel) register-direct form
+    (2, 300, 256, 176, 3, 1, "snake", True, False, True, 1),     # wide form with Co < co_pad (masked column groups)
     (3, 400, 1090, 256, 3, 1, "leaky", True, False, True, 2),    # decoder block conv2: Ci 1090 (9 chunks), x2 shortcut
     (4, 200, 200, 96, 3, 1, "leaky", False, False, True, 1),     # predictor block conv1 (2 chunks, 1 column tile)
     (2, 300, 130, 64, 3, 1, "none", False, False, True, 1),      # up-block conv1 after the dw-ConvT: no prologue
@@ -345,6 +347,22 @@ def test_mrf_frag32_bit_identical(eng, case):
     """the register-direct kernel accumulates every output in the same K order from the same staged bf16
     operands as the LDS-ring kernel: outputs and fused statistics are bit-identical (tolerance 0)."""
     a, sa, _ = _run_mrf(eng, case, "lane16")
+    b, sb, _ = _run_mrf(eng, case, "frag32")
+    assert torch.equal(a, b)
+    if sa is not None:
+        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
+
+
+WIDE_CASES = [c for c in MRF_CASES if c[2] > 128 and c[6] == "snake"]  # multi-chunk Snake: the wide mrfv form
+
+
+@pytest.mark.parametrize("case", WIDE_CASES)
+def test_mrf_wide_bit_identical(eng, case):
+    """the wide register-direct form (256 output channels per workgroup, the default for multi-chunk Snake convs) vs
+    the narrow one (STZS_CONV_MRFV_NARROW: 128 per workgroup): same staged operands, same K order per output ->
+    outputs and fused statistics bit-identical (tolerance 0)."""
+    from stzs import _lib as L
+    a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_NARROW)
     b, sb, _ = _run_mrf(eng, case, "frag32")
     assert torch.equal(a, b)
     if sa is not None:

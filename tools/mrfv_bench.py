@@ -46,7 +46,10 @@ for (T, C, k, dil) in cases:
     byt = 2.0 * B * T * C * 2
     for variant in ("c1", "c2", "c2acc"):
         outs = {}
-        for name, cw, fl in (("lane16", c16, 0), ("mrfv", cfr, 0), ("mrfp", cfr, L.CONV_MRF_PIPE)):
+        forms = [("lane16", c16, 0), ("mrfv", cfr, 0)]
+        # single-chunk: the persistent form; two chunks: the narrow (128 channels per workgroup) register-direct form
+        forms.append(("mrfp", cfr, L.CONV_MRF_PIPE) if C == 128 else ("mrfvN", cfr, L.CONV_MRFV_NARROW))
+        for name, cw, fl in forms:
             y = Act(torch.zeros(B, T, C, device=dev, dtype=torch.bfloat16))
             kw = dict(pad=dil * (k - 1) // 2, dil=dil, pro=(mean, rstd, C, gb.data_ptr(), 2 * C, C),
                       pro_act=L.ACT_SNAKE, pro_alpha=al, flags=flags | fl)
@@ -74,7 +77,7 @@ for (T, C, k, dil) in cases:
             print(f"T={T} C={C} k={k:2d} d={dil} {variant:6s} {name:7s}: {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s  "
                   f"{nb / us / 1e3:7.1f} GB/s", flush=True)
         a = outs["lane16"]
-        for other in ("mrfv", "mrfp"):
+        for other in [f[0] for f in forms[1:]]:
             bb = outs[other]
             same = torch.equal(a[0], bb[0]) and (a[1] is None or (torch.equal(a[1][0], bb[1][0]) and
                                                                    torch.equal(a[1][1], bb[1][1])))
