@@ -16,6 +16,10 @@
  *                   flash unit of that head (sc1 loads) and writes attn.o.  Replaces stzs_conv1d +
  *                   stzs_attention: the qkv linear + self-attention, the cross-attention query linear +
  *                   cross-attention.
+ *   STZS_FUSE_CFG   the classifier-free-guidance combine + Euler step of the sampler state (stzs_cfg_euler
+ *                   semantics, `cfg_*`) on the denoiser output D = y: every 16-column tile has a counter over the row
+ *                   blocks, its last arriver updates the state x for its columns (D by sc1 loads).  Replaces
+ *                   stzs_conv1d + stzs_cfg_euler for the denoiser's output projection.
  *
  * Results are bit-identical to the unfused pair (same per-element arithmetic: the linear's K order depends on K
  * and the split only, the LayerNorm / attention code is the same device code).  Counters: `ctr` holds
@@ -30,6 +34,7 @@ extern "C" {
 
 #define STZS_FUSE_LN 1
 #define STZS_FUSE_ATTN 2
+#define STZS_FUSE_CFG 3
 
 typedef struct stzs_rows_fuse {
     int32_t mode;           /* STZS_FUSE_LN | STZS_FUSE_ATTN */
@@ -41,6 +46,12 @@ typedef struct stzs_rows_fuse {
     /* STZS_FUSE_ATTN: bf16, precise 0, dh 64, q == y (+ 0), R == B, Lq == T_in, Co % (heads * dh) == 0;
      * k / v may point into y (the qkv linear) or at tensors written by earlier launches */
     stzs_attn_args attn;
+    /* STZS_FUSE_CFG: y = D fp32 [R, T_in, Co] flat (ldy == Co, bsy == T_in * Co), R == 2 cfg_B (cfg_on) or cfg_B;
+     * cfg_x = the state [R, T_in * Co] fp32 (x of stzs_cfg_euler), updated in place for rows < cfg_B and copied to
+     * rows cfg_B + b when cfg_on; scale / sigma / dsig as stzs_cfg_euler's s / s0 / dsig */
+    float* cfg_x;
+    int32_t cfg_B, cfg_on;
+    float cfg_scale, cfg_sigma, cfg_dsig, cfg_pad;
 } stzs_rows_fuse;
 
 /* counter words a fused launch of `a` needs (0 for a bad argument) */

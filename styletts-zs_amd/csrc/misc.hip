@@ -7,6 +7,7 @@
 //   stzs_copy2d       strided row copy with dtype conversion (buffer assembly, no torch ops)
 //   stzs_embed        token embedding rows (text front end)
 #include "common.hpp"
+#include "cfg.hpp"
 
 namespace {
 
@@ -41,13 +42,7 @@ __global__ void adaln_expand_kernel(const float* mod, const float* table, float*
 __global__ void cfg_euler_kernel(float* x, const float* D, int B, int N, int cfg, float s, float s0, float dsig) {
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     if (i >= (long)B * N) return;
-    const float xv = x[i];
-    float d = D[i];
-    if (cfg) {
-        const float du = D[(long)B * N + i];
-        d = du + s * (d - du);
-    }
-    const float xn = xv + dsig * (xv - d) / s0;
+    const float xn = stzs_cfg_euler_elem(x[i], D[i], cfg ? D[(long)B * N + i] : 0.f, cfg, s, s0, dsig);
     x[i] = xn;
     if (cfg) x[(long)B * N + i] = xn;
 }

@@ -390,9 +390,12 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + CS_BYTES;
     void (*k)(stzs_conv_args) = nullptr;
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
-    // the wide form (256 output channels per workgroup) for multi-chunk Snake convs, unless STZS_CONV_MRFV_NARROW
+    // the wide form (256 output channels per workgroup) for multi-chunk Snake convs whose wide grid still gives every
+    // CU two workgroups (at batch 1 a stage-0 conv has 32 row tiles: the narrow form's 64 workgroups finish sooner),
+    // unless STZS_CONV_MRFV_NARROW.  Both forms are bit-identical, so the choice never changes a result.
+    const long wide_tiles = (long)a.B * ((a.T_out + BT - 1) / BT) * (a.co_pad / (2 * BCO));
     const bool wide = a.pro_act == STZS_ACT_SNAKE && a.ci_pad > 128 && a.co_pad % (2 * BCO) == 0 &&
-                      !(a.flags & STZS_CONV_MRFV_NARROW);
+                      wide_tiles >= 512 && !(a.flags & STZS_CONV_MRFV_NARROW);
     if (a.pro_act == STZS_ACT_SNAKE) {
         const bool one = a.ci_pad == 128;
         const bool al = a.alpha != 1.f;

@@ -26,6 +26,7 @@
 // device code as stzs_row_layernorm / stzs_attention, so results are bit-identical to the unfused pair.
 #include "common.hpp"
 #include "attn_body.hpp"
+#include "cfg.hpp"
 #include "rowln.hpp"
 #include "stzs_fused.h"
 
@@ -55,7 +56,7 @@ STZS_DEV float epi_act(float x, float slope) {
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((address_space(1))) unsigned int gu32;
 
-constexpr int FUSE_NONE = 0, FUSE_LN = STZS_FUSE_LN, FUSE_ATTN = STZS_FUSE_ATTN;
+constexpr int FUSE_NONE = 0, FUSE_LN = STZS_FUSE_LN, FUSE_ATTN = STZS_FUSE_ATTN, FUSE_CFG = STZS_FUSE_CFG;
 
 struct RowsArgs {
     stzs_conv_args c;
@@ -313,6 +314,25 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const RowsArgs ra) {
                 }
                 stzs_ln::ln_row_finish<bf16_t, 4>(f.ln, r, lane, v);
             }
+        } else if constexpr (FUSE == FUSE_CFG) {
+            // this tile's 16 columns of every state row, complete once every row block has arrived
+            if (!ticket(f.ctr + ct, gridDim.y, &s_last)) return;
+            const int Bc = f.cfg_B, on = f.cfg_on;
+            const long N = (long)T * a.Co;  // state elements per utterance row
+            const float* D = reinterpret_cast<const float*>(a.y);
+            const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(D), 0, 0x7FFFFFFF, 0x00020000);
+            const int ncol = min(16, a.Co - ct * 16);
+            const int per = T * ncol;  // elements of one utterance row in this tile
+            for (int e = tid; e < Bc * per; e += NTHR) {
+                const int b = e / per, q = e - b * per;
+                const int t = q / ncol, c = ct * 16 + (q - t * ncol);
+                const long i = (long)b * N + (long)t * a.Co + c;
+                const float dc = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dr, (int)(i * 4), 0, 16));
+                const float du = on ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dr, (int)((i + Bc * N) * 4), 0, 16)) : 0.f;
+                const float xn = stzs_cfg_euler_elem(f.cfg_x[i], dc, du, on, f.cfg_scale, f.cfg_sigma, f.cfg_dsig);
+                f.cfg_x[i] = xn;
+                if (on) f.cfg_x[i + Bc * N] = xn;
+            }
         } else {
             // the (utterance, head) units this block's rows and this tile's head complete
             const int dm = f.attn.heads * 64;
@@ -422,6 +442,11 @@ static int rows_launch(const stzs_conv_args& a, const stzs_rows_fuse* f, hipStre
                 !l.y || l.gdiv <= 0 || (l.G && (l.gs % 8 || !stzs_aligned(l.G, 32))) ||
                 (l.Bt && (l.bs % 8 || !stzs_aligned(l.Bt, 32))) || l.ldy % 8 || l.ldx % 8)
                 return STZS_ESHAPE;
+        } else if (f->mode == STZS_FUSE_CFG) {
+            const int R = f->cfg_on ? 2 * f->cfg_B : f->cfg_B;
+            if (a.out_dtype != STZS_F32 || !f->cfg_x || f->cfg_B <= 0 || a.B != R || a.ldy != a.Co ||
+                (a.B > 1 && a.bsy != (long)a.T_in * a.Co) || (long)a.B * a.T_in * a.Co >= 0x1FFFFFFF)
+                return STZS_ESHAPE;
         } else if (f->mode == STZS_FUSE_ATTN) {
             const stzs_attn_args& t = f->attn;
             const int dm = t.heads * t.dh;
@@ -441,6 +466,9 @@ static int rows_launch(const stzs_conv_args& a, const stzs_rows_fuse* f, hipStre
         if (a.in_dtype == STZS_BF16) k = pick_fused<bf16_t, float, FUSE_LN>(kpw, split);
         else if (a.in_dtype == STZS_F32) k = pick_fused<float, float, FUSE_LN>(kpw, split);
         else return STZS_EDTYPE;
+    } else if (f && f->mode == STZS_FUSE_CFG) {
+        if (a.in_dtype != STZS_BF16) return STZS_EDTYPE;
+        k = pick_fused<bf16_t, float, FUSE_CFG>(kpw, split);
     } else if (f) {
         if (a.in_dtype != STZS_BF16) return STZS_EDTYPE;
         k = pick_fused<bf16_t, bf16_t, FUSE_ATTN>(kpw, split);
@@ -464,6 +492,7 @@ extern "C" size_t stzs_rows_fuse_counters(const stzs_conv_args* a, const stzs_ro
     if (!a || !f || a->B <= 0 || a->T_in <= 0) return 0;
     if (f->mode == STZS_FUSE_LN) return (size_t)(((long)a->B * a->T_in + 15) / 16);
     if (f->mode == STZS_FUSE_ATTN) return f->attn.heads > 0 ? (size_t)a->B * f->attn.heads : 0;
+    if (f->mode == STZS_FUSE_CFG) return a->Co > 0 ? (size_t)((a->Co + 15) / 16) : 0;
     return 0;
 }
 

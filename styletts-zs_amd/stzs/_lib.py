@@ -72,10 +72,12 @@ class AttnArgs(C.Structure):
 
 class RowsFuse(C.Structure):
     """stzs_rows_fuse (include/stzs_fused.h): the consumer fused into a small-M linear's launch"""
-    _fields_ = [("mode", i32), ("pad0", i32), ("ctr", vp), ("ln", RowLNArgs), ("attn", AttnArgs)]
+    _fields_ = [("mode", i32), ("pad0", i32), ("ctr", vp), ("ln", RowLNArgs), ("attn", AttnArgs), ("cfg_x", vp),
+                ("cfg_B", i32), ("cfg_on", i32), ("cfg_scale", f32), ("cfg_sigma", f32), ("cfg_dsig", f32),
+                ("cfg_pad", f32)]
 
 
-FUSE_LN, FUSE_ATTN = 1, 2  # include/stzs_fused.h
+FUSE_LN, FUSE_ATTN, FUSE_CFG = 1, 2, 3  # include/stzs_fused.h
 
 
 class LstmArgs(C.Structure):

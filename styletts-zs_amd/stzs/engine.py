@@ -73,6 +73,9 @@ def _rup(x, m):
     return (x + m - 1) // m * m
 
 
+_FUSED = object()  # conv(): the CFG + Euler step ran inside the linear's launch
+
+
 @dataclass
 class Act:
     """channels-last activation view: buffer [B, T, ld], logical channels [c0, c0 + C)."""
@@ -188,7 +191,8 @@ class StyleTTSZS:
         # property of the weight like dn_splitk (batch-invariant), taking precedence over it
         self.dn_rows = _table_env("STZS_DN_ROWS", DN_ROWS) if dn_rows is None else dict(dn_rows)
         # the consumers of the small-M denoiser linears fused into their launches (include/stzs_fused.h: the
-        # LayerNorm after the residual linears, the attention after the q / qkv linears; bit-identical, 31 launches
+        # LayerNorm after the residual linears, the attention after the q / qkv linears, the CFG + Euler step after the
+        # output projection; bit-identical, 32 launches
         # fewer per NFE); STZS_FUSE_ROWS=0 / 1 overrides the constructor
         fz = os.environ.get("STZS_FUSE_ROWS")
         self.fuse_rows = bool(fuse_rows) if fz is None else fz != "0"
@@ -289,11 +293,13 @@ class StyleTTSZS:
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
              T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, splitk=0, rows=0, attn=None,
-             what="conv"):
+             cfg=None, what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
         output fused into the conv epilogue (per-tile partials) + one small finalize launch.
         post_ln (stzs_rowln_args) / attn ((q, k, v, o) Acts): the LayerNorm / attention that consumes y, launched
-        behind the linear, or folded into its launch on the fused small-M form (fuse_rows, include/stzs_fused.h)."""
+        behind the linear, or folded into its launch on the fused small-M form (fuse_rows, include/stzs_fused.h).
+        cfg = (B, cfg_on, scale, sigma, dsig): the sampler's CFG + Euler step on y = D of the state acc_in, folded
+        in the same way (returns _FUSED then: the caller skips its stzs_cfg_euler launch); ignored otherwise."""
         W = self.W
         a = L.ConvArgs()
         a.x, a.w, a.y = x.ptr, self._t(cw.w).data_ptr(), y.ptr
@@ -370,12 +376,15 @@ class StyleTTSZS:
             a.splitk, a.splitk_ws = splitk, self._scratch("sk_ws", nb // 4).data_ptr()
             a.splitk_ctr = self._counters("sk_ctr", nb // (splitk * 32768)).data_ptr()
         fz = None
-        if (a.flags & L.CONV_ROWS) and self.fuse_rows and (post_ln is not None or attn is not None):
+        if (a.flags & L.CONV_ROWS) and self.fuse_rows and (post_ln is not None or attn is not None or cfg is not None):
             fz = L.RowsFuse()
             if post_ln is not None:
                 fz.mode, fz.ln = L.FUSE_LN, post_ln
-            else:
+            elif attn is not None:
                 fz.mode, fz.attn = L.FUSE_ATTN, self._attn_args(*attn)
+            else:
+                fz.mode, fz.cfg_x = L.FUSE_CFG, acc_in.ptr
+                fz.cfg_B, fz.cfg_on, fz.cfg_scale, fz.cfg_sigma, fz.cfg_dsig = cfg
             n = self.lib.stzs_rows_fuse_counters(C.byref(a), C.byref(fz))
             assert n > 0, what
             fz.ctr = self._counters("fuse_ctr", n).data_ptr()
@@ -414,6 +423,8 @@ class StyleTTSZS:
             self._call(self.lib.stzs_row_layernorm, post_ln, what + ".ln", cost=_ln_cost(post_ln))
         if attn is not None and fz is None:  # the attention whose q (k, v) this linear produced
             self.attention(*attn)
+        if fz is not None and cfg is not None and post_ln is None and attn is None:
+            return _FUSED
         if st is None:
             return y
         slab, Cc, mean, rstd = st
@@ -697,7 +708,9 @@ class StyleTTSZS:
                 "state_init")
         D = self.act("dn.D", R, S.L_s, S.code_dim, torch.float32)
         for i in range(steps):
-            self.denoiser_step(st, i, Act(x), D)
+            eu = (B, int(cfg), float(cfg_scale), float(sig[i]), float(sig[i + 1] - sig[i]))
+            if self.denoiser_step(st, i, Act(x), D, euler=eu):
+                continue  # the CFG + Euler update ran inside the output projection's launch
             self.launches += 1
             L.check(self.lib.stzs_cfg_euler(x.data_ptr(), D.t.data_ptr(), B, N, int(cfg), float(cfg_scale),
                                             float(sig[i]), float(sig[i + 1] - sig[i]), self.stream()), "cfg_euler")
@@ -779,9 +792,11 @@ class StyleTTSZS:
                                            self.stream()), "adaln_expand.f")
         return dict(R=R, sig=list(sigmas), kv=kv, modx=modx, fmodx=fmodx)
 
-    def denoiser_step(self, st: dict, i: int, xa: Act, D: Act):
+    def denoiser_step(self, st: dict, i: int, xa: Act, D: Act, euler=None) -> bool:
         """one NFE: D = c_skip x + c_out F(c_in x, sigma_i) for the R rows of xa, with the conditioning prepared
-        by denoiser_prepare (6 layers: adaLN-modulated self-attention, cross-attention, GELU FFN)."""
+        by denoiser_prepare (6 layers: adaLN-modulated self-attention, cross-attention, GELU FFN).
+        euler = (B, cfg, scale, sigma, dsig): the sampler's CFG + Euler update of xa that follows; True when it
+        ran inside the output projection's launch (fuse_rows), False when the caller still has to launch it."""
         S, W = self.spec, self.W
         R, kv, modx, fmodx = st["R"], st["kv"], st["modx"], st["fmodx"]
         Ls, d = S.L_s, S.dn_d
@@ -845,8 +860,8 @@ class StyleTTSZS:
                 self.quant(ff, ff8, s_ff)
             self.conv(lw["ff2" + sfx], xf, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=sf,
                       post_ln=lns[3 * l + 3], splitk=sk.get("ff2", 0), rows=rk.get("ff2", 0), what="ff2")
-        self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], rows=rk.get("out", 0),
-                  what="dn.out")
+        return self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], rows=rk.get("out", 0),
+                         cfg=euler, what="dn.out") is _FUSED
 
     def _ln_args(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=0.0, y_scale=None):
         """stzs_rowln_args of a modulated LayerNorm x -> y (launched by stzs_row_layernorm, or fused into a

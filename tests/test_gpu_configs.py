@@ -293,8 +293,8 @@ def test_latency_engine_batch_invariant(v0):
 
 def test_latency_engine_fused_linears_bit_identical(v0):
     """the latency engine's fused small-M linears (include/stzs_fused.h: the LayerNorm after dn.in / sa_o / ca_o /
-    ff2 and the self / cross attention after qkv / ca_q inside the linear's launch) vs the same engine launching them
-    separately: codes, F0 and waveform bit-identical at batch 1 and 2, and 31 launches fewer per NFE."""
+    ff2, the self / cross attention after qkv / ca_q and the CFG + Euler step after dn.out inside the linear's launch) vs the same engine launching them
+    separately: codes, F0 and waveform bit-identical at batch 1 and 2, and 32 launches fewer per NFE."""
     from stzs.engine import latency_engine
     S, P, eng = v0
     e = latency_engine(S, eng.W, eng.device)
@@ -312,4 +312,4 @@ def test_latency_engine_fused_linears_bit_identical(v0):
         e.fuse_rows = True
         for k in ("codes", "F0", "wav"):
             assert torch.equal(outs[0][k], outs[1][k]), (nb, k)
-        assert nl[1] - nl[0] == 31 * bench.STEPS_LATENCY, nl
+        assert nl[1] - nl[0] == 32 * bench.STEPS_LATENCY, nl

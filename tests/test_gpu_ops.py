@@ -266,8 +266,8 @@ MRF_CASES = [
     (9, 4000, 128, 128, 7, 3, "snake", True, False, True, 1),    # c2 form + stats (288 tiles)
     (2, 777, 256, 256, 7, 1, "snake", True, True, True, 1),      # stage-0 width: 2 input chunks x 2 column tiles
     (1, 129, 256, 256, 3, 5, "snake", False, False, True, 1),    # ragged: the second row tile has 1 valid row
-    (2, 500, 384, 256, 11, 3, "snake", True, False, True, 1),    # 3 input chunks, wide (256-channel) register-direct form
-    (2, 300, 256, 176, 3, 1, "snake", True, False, True, 1),     # wide form with Co < co_pad (masked column groups)
+    (2, 500, 384, 256, 11, 3, "snake", True, False, True, 1),    # 3 input chunks
+    (2, 300, 256, 176, 3, 1, "snake", True, False, True, 1),     # Co < co_pad (masked column groups)
     (3, 400, 1090, 256, 3, 1, "leaky", True, False, True, 2),    # decoder block conv2: Ci 1090 (9 chunks), x2 shortcut
     (4, 200, 200, 96, 3, 1, "leaky", False, False, True, 1),     # predictor block conv1 (2 chunks, 1 column tile)
     (2, 300, 130, 64, 3, 1, "none", False, False, True, 1),      # up-block conv1 after the dw-ConvT: no prologue
@@ -282,7 +282,7 @@ MRF_CASES = [
 PIPE_CASES = [c for c in MRF_CASES if c[2] == 128 and c[4] == 3 and c[7]]  # residual forms (csrc/mrfp.hip)
 
 
-def _run_mrf(eng, case, form, flags=0):
+def _run_mrf(eng, case, form, flags=0, ref=True):
     B, T, Ci, Co, k, dil, act, hr, ha, st, tdiv = case
     g = torch.Generator().manual_seed(B * T + Ci + k)
     pad = dil * (k - 1) // 2
@@ -301,7 +301,7 @@ def _run_mrf(eng, case, form, flags=0):
         sc, sh = torch.ones(B, Ci), torch.zeros(B, Ci)
     osc = 1 / 3 if ha else (0.7071 if hr else 1.0)
     ref = conv_ref(x, w, b, pad=pad, dil=dil, stride=1, sc=sc, sh=sh, pro_act=None if act == "none" else act,
-                   slope=0.2, alpha=alpha, res=res, res_tdiv=tdiv, out_scale=osc, acc_in=acc, beta=1.0)
+                   slope=0.2, alpha=alpha, res=res, res_tdiv=tdiv, out_scale=osc, acc_in=acc, beta=1.0) if ref else None
     from stzs.weights import Arena, pack_conv
     A = Arena()
     cw = pack_conv(A, "t", w, b, lane16=form == "lane16", frag32=form == "frag32")
@@ -353,17 +353,22 @@ def test_mrf_frag32_bit_identical(eng, case):
         assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
 
 
-WIDE_CASES = [c for c in MRF_CASES if c[2] > 128 and c[6] == "snake"]  # multi-chunk Snake: the wide mrfv form
+# multi-chunk Snake convs with >= 512 wide tiles (batch x row tiles x 256-channel tiles): the wide mrfv form
+WIDE_CASES = [
+    (20, 3300, 256, 256, 7, 3, "snake", True, True, True, 1),    # stage-0 width, residual + accumulate + stats
+    (18, 3700, 384, 256, 11, 5, "snake", True, False, True, 1),  # 3 input chunks, ragged last row tile
+    (20, 3300, 256, 176, 3, 1, "snake", False, False, True, 1),  # Co < co_pad: masked column groups
+]
 
 
 @pytest.mark.parametrize("case", WIDE_CASES)
 def test_mrf_wide_bit_identical(eng, case):
-    """the wide register-direct form (256 output channels per workgroup, the default for multi-chunk Snake convs) vs
-    the narrow one (STZS_CONV_MRFV_NARROW: 128 per workgroup): same staged operands, same K order per output ->
-    outputs and fused statistics bit-identical (tolerance 0)."""
+    """the wide register-direct form (256 output channels per workgroup, the default for multi-chunk Snake convs whose
+    wide grid has >= 512 workgroups) vs the narrow one (STZS_CONV_MRFV_NARROW: 128 per workgroup): same staged
+    operands, same K order per output -> outputs and fused statistics bit-identical (tolerance 0)."""
     from stzs import _lib as L
-    a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_NARROW)
-    b, sb, _ = _run_mrf(eng, case, "frag32")
+    a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_NARROW, ref=False)
+    b, sb, _ = _run_mrf(eng, case, "frag32", ref=False)
     assert torch.equal(a, b)
     if sa is not None:
         assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])

@@ -196,3 +196,45 @@ def test_rows_fused_attention_bit_identical(eng, kind, B):
     assert torch.equal(o1, o2)
     assert int(eng._counters("fuse_ctr", 1).abs().sum()) == 0
     assert float(o0.float().abs().max()) > 0
+
+
+@pytest.mark.parametrize("B,cfg", [(1, 1), (2, 1), (3, 0)])
+def test_rows_fused_cfg_euler_bit_identical(eng, B, cfg):
+    """STZS_FUSE_CFG: the denoiser output projection D = c_out F + c_skip x and the sampler's CFG + Euler update of x
+    from ONE launch equal the linear + stzs_cfg_euler bit for bit (state and D; tolerance 0), counters left zero."""
+    from stzs import _lib as L
+    from stzs.engine import Act
+    dev = eng.device
+    R = 2 * B if cfg else B
+    K, N = 512, 256
+    g = torch.Generator().manual_seed(R)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    from stzs.weights import Arena, pack_conv
+    A = Arena()
+    cw = pack_conv(A, "g", w, torch.randn(N, generator=g) * 0.1)
+    A.finalize(dev)
+    cw.w, cw.b = A[cw.w], A[cw.b]
+    an = Act(torch.randn(R, 50, K, generator=g).to(dev, torch.bfloat16))
+    x0 = torch.randn(R, 50, N, generator=g).to(dev)
+    eu = (B, cfg, 5.0, 0.8, -0.3)
+
+    def run(on):
+        x = x0.clone()
+        D = Act(torch.zeros(R, 50, N, device=dev))
+        old, eng.fuse_rows = eng.fuse_rows, on
+        try:
+            fused = eng.conv(cw, an, D, alpha=0.6, acc_in=Act(x), beta=0.4, rows=1, cfg=eu, what="fz") is not D
+        finally:
+            eng.fuse_rows = old
+        if not fused:
+            L.check(eng.lib.stzs_cfg_euler(x.data_ptr(), D.t.data_ptr(), B, 50 * N, cfg, 5.0, 0.8, -0.3,
+                                           eng.stream()), "cfg_euler")
+        torch.cuda.synchronize()
+        return fused, x.cpu(), D.t.cpu()
+
+    f0, xa, Da = run(False)
+    f1, xb, Db = run(True)
+    assert (f0, f1) == (False, True)
+    assert torch.equal(Da, Db) and torch.equal(xa, xb)
+    assert not torch.equal(xa, x0.cpu())
+    assert int(eng._counters("fuse_ctr", 1).abs().sum()) == 0

@@ -54,6 +54,13 @@ def main(path):
     print(f"\n{'kernel family':30s} {'calls':>6s} {'total us':>9s} {'avg us':>8s}")
     for n, _ in t.most_common(20):
         print(f"{n:30s} {c[n]:6d} {t[n]:9.1f} {t[n] / c[n]:8.2f}")
+    if "--list" in sys.argv:  # every kernel of the replay in order: duration and the gap before it
+        print(f"\n{'#':>4s} {'kernel':34s} {'us':>7s} {'gap us':>7s}")
+        prev = None
+        for k, (r, n) in enumerate(zip(last, names)):
+            gap = (t0(r) - t1(prev)) / 1e3 if prev is not None else 0.0
+            print(f"{k:4d} {n[:34]:34s} {(t1(r) - t0(r)) / 1e3:7.2f} {gap:7.2f}")
+            prev = r
 
 
 if __name__ == "__main__":
