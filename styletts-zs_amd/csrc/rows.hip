@@ -295,6 +295,31 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const RowsArgs ra) {
             const int nv = f.ln.C >> 3;
             const float* X = reinterpret_cast<const float*>(f.ln.x);
             const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X), 0, 0x7FFFFFFF, 0x00020000);
+            // the wave's 4 rows (r0 + wave + 4 j) loaded at once -- one sc1 round trip instead of four -- from
+            // clamped addresses (rows past the end are loaded, never stored); C <= 512 here (one vector per lane)
+            if (nv <= 64) {
+                f32x4 raw[4][2];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = min(r0 + wave + 4 * j, nR - 1);
+                    const int off = (int)(((long)r * f.ln.ldx + min(lane, nv - 1) * 8) * 4);
+                    raw[j][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 16));
+                    raw[j][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 16));
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = r0 + wave + 4 * j;
+                    if (r >= nR) break;
+                    float v[1][8];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        v[0][q] = raw[j][0][q];
+                        v[0][4 + q] = raw[j][1][q];
+                    }
+                    stzs_ln::ln_row_finish<bf16_t, 1>(f.ln, r, lane, v);
+                }
+                return;
+            }
             for (int j = 0; j < 4; ++j) {
                 const int r = r0 + wave + 4 * j;
                 if (r >= nR) break;

@@ -192,10 +192,13 @@ class StyleTTSZS:
         self.dn_rows = _table_env("STZS_DN_ROWS", DN_ROWS) if dn_rows is None else dict(dn_rows)
         # the consumers of the small-M denoiser linears fused into their launches (include/stzs_fused.h: the
         # LayerNorm after the residual linears, the attention after the q / qkv linears, the CFG + Euler step after the
-        # output projection; bit-identical, 32 launches
-        # fewer per NFE); STZS_FUSE_ROWS=0 / 1 overrides the constructor
+        # output projection; bit-identical, 32 launches fewer per NFE).  OFF by default: measured SLOWER at batch 1
+        # (configs[1] p50 8.56 -> 10.1 ms, each in-launch hand-off ~5 us dearer than the launch it removes,
+        # profiles/r03_t_fused_latency_ab.log); STZS_FUSE_ROWS=0 / 1 overrides the constructor
         fz = os.environ.get("STZS_FUSE_ROWS")
         self.fuse_rows = bool(fuse_rows) if fz is None else fz != "0"
+        # which consumers fuse (STZS_FUSE_MODES, e.g. "ln,attn,cfg")
+        self.fuse_modes = set(os.environ.get("STZS_FUSE_MODES", "ln,attn,cfg").split(","))
         # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
         # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
@@ -376,7 +379,11 @@ class StyleTTSZS:
             a.splitk, a.splitk_ws = splitk, self._scratch("sk_ws", nb // 4).data_ptr()
             a.splitk_ctr = self._counters("sk_ctr", nb // (splitk * 32768)).data_ptr()
         fz = None
-        if (a.flags & L.CONV_ROWS) and self.fuse_rows and (post_ln is not None or attn is not None or cfg is not None):
+        fm = self.fuse_modes
+        if (a.flags & L.CONV_ROWS) and self.fuse_rows and ((post_ln is not None and "ln" in fm) or
+                                                          (attn is not None and "attn" in fm) or
+                                                          (cfg is not None and post_ln is None and attn is None and
+                                                           "cfg" in fm)):
             fz = L.RowsFuse()
             if post_ln is not None:
                 fz.mode, fz.ln = L.FUSE_LN, post_ln
@@ -1415,8 +1422,7 @@ def latency_engine(spec: Spec, packed: PackedModel, device="cuda:0") -> "StyleTT
     """the batch-1 serving engine bench.py times for the configs[1] p50 (and tests/test_gpu_configs.py checks against
     the oracle): the same packed weights, the denoiser layer linears on the whole-chip small-M form
     (LATENCY_DN_ROWS, csrc/rows.hip) and split-K ffn2 wherever the rows form does not apply (LATENCY_DN_SPLITK)."""
-    return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS,
-                      fuse_rows=True)
+    return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS)
 
 
 class CheckedGraph:
