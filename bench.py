@@ -484,7 +484,7 @@ def main():
     roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                 frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=traffic, traffic_src=tsrc,
                 alg_bytes_per_launch=round(bsum / nl),
-                kernel="generator MRF convs: mrfv_conv (stage 1, csrc/mrfv.hip) + mrf_conv (stage 0, csrc/mrf.hip)",
+                kernel="generator MRF convs: mrfv_conv (csrc/mrfv.hip; stage 1 narrow, stage 0 the wide 256-channel form)",
                 launches=len(rec),
                 avg_launch_us=round(tsum / nl * 1e6, 2), alg_gflop_per_launch=round(fsum / nl / 1e9, 3),
                 time_frac=round(t_roof / tsum, 4) if tsum > 0 else None, hbm_bound_launches=n_hbm,
