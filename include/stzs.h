@@ -121,8 +121,9 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * conv feature except the fp8 path.  Used by StyleTTSZS(precise_decoder=True) to meet the north-star
  * mel-L1 <= 1e-3 on the decoder (bf16 weight rounding alone costs ~1.3e-2). */
 #define STZS_CONV_W_F32 64
-/* flags bit (diagnostic): keep the dispatcher's linear workgroup order on the LANE16 / NARROW32 kernels
- * instead of the XCD-aware remap (neighbouring time tiles on one L2); results are identical either way. */
+/* flags bit (diagnostic): keep the dispatcher's linear workgroup order on the LANE16 / NARROW32 kernels and the
+ * LDS-DMA linear GEMM instead of the XCD-aware remap (neighbouring tiles on one L2); results are identical
+ * either way. */
 #define STZS_CONV_LINEAR_IDS 128
 /* flags bit: weights packed in MFMA fragment order for the register-direct MRF conv (csrc/mrfv.hip,
  * stzs/weights.py pack_conv(frag32=True)): [co_pad/128][ci_pad/128][ks][4 k-steps][4 waves][2][64 lanes][8]

@@ -101,7 +101,7 @@ STZS_DEV float epi_act(float x, float slope) {
 
 template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA, int EACT, int BTM>
 STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_bias, const float* c_gate, int bq,
-                       int t0, long row0, int tid) {
+                       int t0, long row0, int tid, int by) {
     const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
     const TOut* AI = reinterpret_cast<const TOut*>(a.acc_in);
     TOut* Y = reinterpret_cast<TOut*>(a.y);
@@ -109,7 +109,7 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
     const long nrows_flat = (long)a.B * a.T_out;
     const long t_hi = a.ups > 0 ? (long)a.T_final + a.refl - 1 : (long)a.T_out - 1;
     const int cv = tid & 15;
-    const int n = blockIdx.y * BCO + cv * 8;
+    const int n = by * BCO + cv * 8;
     const bool col_ok = n < ncol;
     int co = n, p = 0;
     if (a.ups > 0) {
@@ -271,7 +271,7 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
         __syncthreads();
         // one deterministic fp32 partial per (utterance, 64-row chunk, channel)
         const int half = tid >> 7, cl = tid & (BCO - 1);
-        const int c = blockIdx.y * BCO + cl;
+        const int c = by * BCO + cl;
         const int r0 = t0 + half * 64;
         if (c < a.Co && r0 < a.T_out) {
             float ss = 0.f, qq = 0.f;
@@ -291,17 +291,18 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
 
 template <typename TOut, bool FLAT, bool VEC, bool HR, bool HA, int BTM>
 STZS_DEV void epilogue_act(const stzs_conv_args& a, const float* ep, const float* c_bias, const float* c_gate, int bq,
-                           int t0, long row0, int tid) {
+                           int t0, long row0, int tid, int by) {
     switch (a.epi_act) {
-        case STZS_ACT_GELU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_GELU, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
-        case STZS_ACT_SILU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_SILU, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
-        case STZS_ACT_LEAKY: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_LEAKY, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
-        default: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_NONE, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid); break;
+        case STZS_ACT_GELU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_GELU, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by); break;
+        case STZS_ACT_SILU: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_SILU, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by); break;
+        case STZS_ACT_LEAKY: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_LEAKY, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by); break;
+        default: epilogue<TOut, FLAT, VEC, HR, HA, STZS_ACT_NONE, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by); break;
     }
 }
 
 template <typename TOut, bool FLAT, int BTM = BT>
-STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0);
+STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0,
+                     int by);
 
 // 8-wide vector epilogue legal (every output / residual / accumulate row 16-B aligned)
 __host__ __device__ inline bool epi_vec(const stzs_conv_args& a) {
@@ -325,19 +326,27 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
+    // XCD-aware tile order (as gemm_glds): each XCD runs a contiguous range of tiles, output-channel tile fastest,
+    // so the workgroups one XCD holds at a time share their staged input rows (one fabric fetch per XCD instead
+    // of one per channel tile).  Same tiles, same K order: bit-identical to the linear order.
+    const int gy = gridDim.y;
+    const bool lin_ids = (a.flags & STZS_CONV_LINEAR_IDS) != 0;
+    const int lin = lin_ids ? 0 : xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gy);
+    const int by = lin_ids ? (int)blockIdx.y : lin % gy;
+    const int bx = lin_ids ? (int)blockIdx.x : lin / gy;
     int bq = 0, t0 = 0;
     long row0 = 0;
     if (FLAT) {
-        row0 = (long)blockIdx.x * BT;
+        row0 = (long)bx * BT;
     } else {
         const int tpb = (a.T_out + BT - 1) / BT;
-        bq = blockIdx.x / tpb;
-        t0 = (blockIdx.x - bq * tpb) * BT;
+        bq = bx / tpb;
+        t0 = (bx - bq * tpb) * BT;
     }
     const int nchunk = a.ci_pad / cic;
     const int kpc = cic >> 5;
     const int NK = nchunk * ks * kpc;
-    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
+    const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)by * NK * (BCO * 32);
 
     auto fill = [&](int k) {
         const bf16_t* src = Wt + (long)k * (BCO * 32) + wave * 1024 + lane * 8;
@@ -485,12 +494,13 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         }
     }
 
-    finish<TOut, FLAT>(a, acc, smem, bq, t0, row0);
+    finish<TOut, FLAT>(a, acc, smem, bq, t0, row0, by);
 }
 
 // Accumulators -> LDS (fp32, padded rows) -> vectorised fused epilogue.
 template <typename TOut, bool FLAT, int BTM>
-STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0) {
+STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0,
+                     int by) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
     __syncthreads();
@@ -506,19 +516,19 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigne
     float* c_bias = ep + BT * EP_PITCH;       // [BCO] bias, [BCO] gate (conv mode: one utterance)
     float* c_gate = c_bias + BCO;
     if (tid < BCO) {
-        const int n = blockIdx.y * BCO + tid;
+        const int n = by * BCO + tid;
         const int co = a.ups > 0 ? n % a.Co : min(n, a.Co - 1);
         c_bias[tid] = a.bias ? a.bias[co] : 0.f;
         c_gate[tid] = (!FLAT && a.gate) ? a.gate[(long)bq * a.gate_bs + co] : 1.f;
     }
     __syncthreads();
     if (epi_vec(a)) {
-        if (a.res && a.acc_in) epilogue_act<TOut, FLAT, true, true, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else if (a.res) epilogue_act<TOut, FLAT, true, true, false, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else if (a.acc_in) epilogue_act<TOut, FLAT, true, false, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
-        else epilogue_act<TOut, FLAT, true, false, false, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        if (a.res && a.acc_in) epilogue_act<TOut, FLAT, true, true, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
+        else if (a.res) epilogue_act<TOut, FLAT, true, true, false, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
+        else if (a.acc_in) epilogue_act<TOut, FLAT, true, false, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
+        else epilogue_act<TOut, FLAT, true, false, false, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
     } else {
-        epilogue_act<TOut, FLAT, false, true, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid);
+        epilogue_act<TOut, FLAT, false, true, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
     }
 }
 
@@ -555,12 +565,21 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = wave >> 1, wc = wave & 1;
-    const long row0 = (long)blockIdx.x * BTM;
+    // XCD-aware tile order (the dispatcher deals workgroup ids round-robin over the 8 XCDs): every XCD gets a
+    // contiguous range of tiles, column tile fastest, so the tiles one XCD runs at a time share their A rows and
+    // the whole weight matrix (<= 2 MB for every linear) stays resident in that XCD's 4-MB L2 instead of being
+    // re-fetched from the fabric by each XCD for every row tile.  Same tiles, same K order: bit-identical.
+    const int gy = gridDim.y;
+    const int lin = (a.flags & STZS_CONV_LINEAR_IDS) ? blockIdx.y * gridDim.x + blockIdx.x
+                                                      : xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gy);
+    const int by = (a.flags & STZS_CONV_LINEAR_IDS) ? (int)blockIdx.y : lin % gy;
+    const int bx = (a.flags & STZS_CONV_LINEAR_IDS) ? (int)blockIdx.x : lin / gy;
+    const long row0 = (long)bx * BTM;
     const long nR = (long)a.B * a.T_in;
     const int NK = a.ci_pad / (64 / ESZ);
     const int NKS = NK / SK;                                  // K-steps of this workgroup's slice
     const int kb = SK > 1 ? (int)blockIdx.z * NKS : 0;
-    const unsigned char* Wt = reinterpret_cast<const unsigned char*>(a.w) + (long)blockIdx.y * NK * SLOT_BYTES;
+    const unsigned char* Wt = reinterpret_cast<const unsigned char*>(a.w) + (long)by * NK * SLOT_BYTES;
     const unsigned char* X = reinterpret_cast<const unsigned char*>(a.x);
     long asrc[AP];  // byte offsets
 #pragma unroll
@@ -656,7 +675,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     if constexpr (F8) {  // dequantise: row scale (flat row, clamped like the A rows) x column scale
         float sw[4];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) sw[nt] = a.w_scale[blockIdx.y * BCO + wc * 64 + nt * 16 + (lane & 15)];
+        for (int nt = 0; nt < 4; ++nt) sw[nt] = a.w_scale[by * BCO + wc * 64 + nt * 16 + (lane & 15)];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -671,7 +690,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     if constexpr (SK > 1) {
         if (!splitk_combine<BTM, SK>(a, acc, smem)) return;
     }
-    finish<TOut, true, BTM>(a, acc, smem, 0, 0, row0);
+    finish<TOut, true, BTM>(a, acc, smem, 0, 0, row0, by);
 }
 
 // In-launch split-K hand-off (MI355X guide: cdna_hip_programming.md, "In-launch split-K reduction", the sc1
@@ -813,7 +832,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_f32(const stzs_conv_args a) {
                         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt][j], bv[nt][j], acc[mt][nt], 0, 0, 0);
         }
     }
-    finish<TOut, false, BT>(a, acc, smem, bq, t0, 0);
+    finish<TOut, false, BT>(a, acc, smem, bq, t0, 0, blockIdx.y);
 }
 
 // PRECISE mode on the bf16 matrix cores, STZS_CONV_W_X3: split-operand ("bf16x3") products.  Every fp32
@@ -986,7 +1005,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3(const stzs_conv_args a) {
                 }
         }
     }
-    finish<TOut, FLAT, BT>(a, acc, smem, bq, t0, row0);
+    finish<TOut, FLAT, BT>(a, acc, smem, bq, t0, row0, blockIdx.y);
 }
 
 size_t x3_lds_bytes(int rows_in) {
