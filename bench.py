@@ -327,7 +327,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from stzs.engine import LATENCY_DN_ROWS, LATENCY_DN_SPLITK, StyleTTSZS, latency_engine
+    from stzs.engine import LATENCY_DN_ROWS, LATENCY_DN_SPLITK, LATENCY_TE_SPLITK, StyleTTSZS, latency_engine
     from stzs.params import init_params
     from stzs.spec import SPEC_V0
     S = SPEC_V0
@@ -522,7 +522,8 @@ def main():
         lstm_timeouts += int(int(elat.status.item()) != 0)
         lat = dict(p50_ms=round(float(np.percentile(ts, 50)), 3), p90_ms=round(float(np.percentile(ts, 90)), 3),
                    config="batch 1, 10-step sampling, CFG 5, 5-s target, 3-s reference",
-                   dn_splitk=dict(LATENCY_DN_SPLITK), dn_rows=dict(LATENCY_DN_ROWS))
+                   dn_splitk=dict(LATENCY_DN_SPLITK), dn_rows=dict(LATENCY_DN_ROWS),
+                   te_splitk=LATENCY_TE_SPLITK)
 
     # ---- configs[4]: 30-s target, batch 1, fp8 denoiser linears, streaming iSTFT (1-s chunks) ----
     lf = None

@@ -300,6 +300,8 @@ STZS_DEV void epilogue_act(const stzs_conv_args& a, const float* ep, const float
     }
 }
 
+template <int BTM>
+STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK);
 template <typename TOut, bool FLAT, int BTM = BT>
 STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0,
                      int by);
@@ -347,6 +349,14 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     const int kpc = cic >> 5;
     const int NK = nchunk * ks * kpc;
     const bf16_t* Wt = reinterpret_cast<const bf16_t*>(a.w) + (long)by * NK * (BCO * 32);
+    // in-launch split-K over input-channel chunks (stzs_conv_args.splitk, grid.z slices): slice z stages and runs
+    // chunks [cc_lo, cc_hi) -- K-steps [k_lo, k_hi) of the chunk-major weight stream -- and hands its fp32 partial
+    // to the tile's last arriver (splitk_combine_rt), which runs the fused epilogue.  For the small grids of the
+    // batch-1 front end (text-encoder k5 convs: 4 workgroups x 80 K-steps at batch 1).
+    const int SKr = a.splitk > 1 ? a.splitk : 1;
+    const int cc_lo = SKr > 1 ? (int)blockIdx.z * (nchunk / SKr) : 0;
+    const int cc_hi = SKr > 1 ? cc_lo + nchunk / SKr : nchunk;
+    const int k_lo = cc_lo * ks * kpc, k_hi = cc_hi * ks * kpc;
 
     auto fill = [&](int k) {
         const bf16_t* src = Wt + (long)k * (BCO * 32) + wave * 1024 + lane * 8;
@@ -374,10 +384,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         boff[nt] = rr * 64 + (((lane >> 4) ^ gswz(rr)) << 4);
     }
 
-    fill(0);
-    if (NK > 1) fill(1);
-    int k = 0;
-    for (int cc = 0; cc < nchunk; ++cc) {
+    fill(k_lo);
+    if (k_lo + 1 < k_hi) fill(k_lo + 1);
+    int k = k_lo;
+    for (int cc = cc_lo; cc < cc_hi; ++cc) {
         __syncthreads();
         const int nv = (a.flags & 1) ? 0 : rows_in * vpr;
         // Staging: ONE batch of SB independent 16-B loads per thread (every MRF tile fits), issued
@@ -471,9 +481,9 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         for (int tap = 0; tap < ((a.flags & 2) ? 0 : ks); ++tap) {
             const int roff = FLAT ? 0 : tap * a.dil;
             for (int kq = 0; kq < kpc; ++kq, ++k) {
-                waitcnt_vm(k + 1 < NK ? 2 : 0);
+                waitcnt_vm(k + 1 < k_hi ? 2 : 0);
                 __builtin_amdgcn_s_barrier();
-                if (k + 2 < NK) fill(k + 2);
+                if (k + 2 < k_hi) fill(k + 2);
                 const unsigned char* wl = ring + (k % NSLOT) * SLOT_BYTES;
                 const int kb = (kq * 32 + 8 * (lane >> 4)) * 2;
                 bf16x8 af[4], bw[4];
@@ -494,6 +504,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         }
     }
 
+    if (SKr > 1 && !splitk_combine_rt<BT>(a, acc, smem, SKr)) return;
     finish<TOut, FLAT>(a, acc, smem, bq, t0, row0, by);
 }
 
@@ -738,6 +749,48 @@ STZS_DEV bool splitk_combine(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4],
 #pragma unroll
         for (int s = 1; s < SK; ++s) t += __builtin_bit_cast(f32x4, v[s][i]);
         acc[i >> 2][i & 3] = t;
+    }
+    return true;
+}
+
+// splitk_combine with the slice count at run time (conv_mfma): the same slabs, ticket and slice-order sum, the
+// slices loaded one at a time (no [SK][NV] register block).
+template <int BTM>
+STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK) {
+    constexpr int NV = BTM / 32 * 4;
+    constexpr int SLAB = NV * NTHR * 16;
+    const int tid = threadIdx.x;
+    const long tile = blockIdx.x + (long)gridDim.x * blockIdx.y;
+    unsigned char* base = reinterpret_cast<unsigned char*>(a.splitk_ws) + tile * (long)SK * SLAB;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(base, 0, SK * SLAB, 0x00020000);
+    const int z = blockIdx.z;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i >> 2][i & 3]), wr,
+                                               (z * NV + i) * (NTHR * 16) + tid * 16, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    volatile int* flag = reinterpret_cast<volatile int*>(smem);  // staging / ring idle: every wave is past its K loop
+    if (tid == 0) {
+        typedef __attribute__((address_space(1))) unsigned int gu32;
+        gu32* ctr = (gu32*)(a.splitk_ctr + tile);
+        const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (unsigned)(SK - 1);
+        if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return false;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+        acc[i >> 2][i & 3] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, i * (NTHR * 16) + tid * 16, 0, 16));
+    for (int sl = 1; sl < SK; ++sl) {
+        u32x4 v[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            v[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, (sl * NV + i) * (NTHR * 16) + tid * 16, 0, 16);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) acc[i >> 2][i & 3] += __builtin_bit_cast(f32x4, v[i]);
     }
     return true;
 }
@@ -1057,7 +1110,12 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
         STZS_LAUNCH_CHECK();
         return STZS_OK;
     }
-    if (a.splitk > 1) return STZS_EINVAL;  // split-K exists on the LDS-DMA GEMM path only
+    if (a.splitk > 1) {  // conv_mfma: split over input-channel chunks (the chunk count must divide)
+        if (F8 || (a.splitk != 2 && a.splitk != 4) || (a.ci_pad / a.cic) % a.splitk || !a.splitk_ws || !a.splitk_ctr ||
+            !stzs_aligned(a.splitk_ws, 16) || !stzs_aligned(a.splitk_ctr, 4))
+            return STZS_EINVAL;
+        grid.z = (unsigned)a.splitk;
+    }
     if constexpr (F8) {
         return STZS_EDTYPE;  // (unreachable: fp8 is a pure linear)
     } else {

@@ -46,6 +46,11 @@ LATENCY_DN_SPLITK = dict(ff2=4)
 # ({}): "0" = off, or e.g. "qkv=1,ff2=4".
 DN_ROWS = {}
 LATENCY_DN_ROWS = dict(inp=1, qkv=1, o=1, q=1, co=1, ff1=1, ff2=4, out=1)
+# in-launch split-K (input-channel chunks, csrc/conv.hip conv_mfma) of the text-encoder k5 convs: at batch 1 their
+# grid is 4 workgroups of 80 K-steps each.  A per-engine property of the weight (batch-invariant); the batch-1
+# latency engine's value.  STZS_TE_SPLITK overrides an engine built without te_splitk.
+TE_SPLITK = 0
+LATENCY_TE_SPLITK = 4
 
 
 _ES = {L.F32: 4, L.BF16: 2, L.F8: 1}
@@ -144,7 +149,7 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
                  packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None, dn_rows=None,
-                 fuse_rows=False):
+                 fuse_rows=False, te_splitk=None):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
@@ -190,6 +195,8 @@ class StyleTTSZS:
         # small-M whole-chip form of the bf16 denoiser linears (csrc/rows.hip): {linear: K slices}; a per-engine
         # property of the weight like dn_splitk (batch-invariant), taking precedence over it
         self.dn_rows = _table_env("STZS_DN_ROWS", DN_ROWS) if dn_rows is None else dict(dn_rows)
+        # split-K slices of the text-encoder convs (LATENCY_TE_SPLITK); 0 = off
+        self.te_splitk = int(os.environ.get("STZS_TE_SPLITK", TE_SPLITK)) if te_splitk is None else int(te_splitk)
         # the consumers of the small-M denoiser linears fused into their launches (include/stzs_fused.h: the
         # LayerNorm after the residual linears, the attention after the q / qkv linears, the CFG + Euler step after the
         # output projection; bit-identical, 32 launches fewer per NFE).  OFF by default: measured SLOWER at batch 1
@@ -378,6 +385,15 @@ class StyleTTSZS:
             assert nb > 0, (what, splitk)
             a.splitk, a.splitk_ws = splitk, self._scratch("sk_ws", nb // 4).data_ptr()
             a.splitk_ctr = self._counters("sk_ctr", nb // (splitk * 32768)).data_ptr()
+        elif (splitk > 1 and not (a.flags & (8 | L.CONV_ROWS | L.CONV_W_X3 | L.CONV_W_F32 | L.CONV_W_FRAG32 |
+                                             L.CONV_W_LANE16 | L.CONV_W_NARROW32)) and not cw.f8 and
+              (cw.ci_pad // cw.cic) % splitk == 0):
+            # conv_mfma split over input-channel chunks: one 64-KB fp32 slab per (128-row tile, slice) + a ticket
+            # per tile (grid.x is at most B x ceil(T_out / 128))
+            tiles = x.B * ((a.T_out + 127) // 128) * (cw.co_pad // 128)
+            a.splitk = splitk
+            a.splitk_ws = self._scratch("csk_ws", tiles * splitk * 16384).data_ptr()
+            a.splitk_ctr = self._counters("csk_ctr", tiles).data_ptr()
         fz = None
         fm = self.fuse_modes
         if (a.flags & L.CONV_ROWS) and self.fuse_rows and ((post_ln is not None and "ln" in fm) or
@@ -610,7 +626,8 @@ class StyleTTSZS:
         emb = self.lib.stzs_embed_f32 if self.adt == torch.float32 else self.lib.stzs_embed
         L.check(emb(tokens.data_ptr(), W.t(W.te_emb).data_ptr(), e.ptr, B, T, S.d_txt, e.ld, self.stream()), "embed")
         for i in range(S.te_layers):
-            self.conv(W.te_conv[i], e, c, pad=S.te_kernel // 2, what=f"te.conv{i}")
+            self.conv(W.te_conv[i], e, c, pad=S.te_kernel // 2, splitk=0 if self.adt == torch.float32 else self.te_splitk,
+                      what=f"te.conv{i}")
             g, b = W.te_ln[i]
             self.rowln(c, e, G=W.t(g).data_ptr(), gs=0, Bt=W.t(b).data_ptr(), bs=0, gadd=0.0,
                        act=L.ACT_LEAKY, slope=0.2, what=f"te.ln{i}")
@@ -1422,7 +1439,8 @@ def latency_engine(spec: Spec, packed: PackedModel, device="cuda:0") -> "StyleTT
     """the batch-1 serving engine bench.py times for the configs[1] p50 (and tests/test_gpu_configs.py checks against
     the oracle): the same packed weights, the denoiser layer linears on the whole-chip small-M form
     (LATENCY_DN_ROWS, csrc/rows.hip) and split-K ffn2 wherever the rows form does not apply (LATENCY_DN_SPLITK)."""
-    return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS)
+    return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS,
+                      te_splitk=LATENCY_TE_SPLITK)
 
 
 class CheckedGraph:

@@ -91,3 +91,42 @@ def test_conv_mfma_xcd_order_bit_identical(eng, R, T, Ci, Co, k):
     e = max_rel(ys[0].float().cpu(), ref)
     print("xcd conv", R, T, Ci, Co, k, e)
     assert e < 1e-2
+
+
+@pytest.mark.parametrize("splitk", [2, 4])
+def test_conv_mfma_splitk(eng, splitk):
+    """conv_mfma in-launch split-K over input-channel chunks (the latency engine's text-encoder k5 convs,
+    LATENCY_TE_SPLITK): matches F.conv1d on the same bf16 operands, utterance 0 of a 3-utterance launch is
+    bit-identical to the 1-utterance launch (per-utterance tiles: batch-invariant), a re-run is bit-identical (the
+    self-resetting tile tickets), and the result is within fp32 re-association of the unsplit conv."""
+    from stzs import _lib as L
+    from stzs.engine import Act
+    from stzs.weights import Arena, pack_conv
+    T, Ci, Co, k = 80, 512, 512, 5
+    g = torch.Generator().manual_seed(100 + splitk)
+    x = bf(torch.randn(3, T, Ci, generator=g))
+    w = torch.randn(Co, Ci, k, generator=g) / math.sqrt(Ci * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    A = Arena()
+    cw = pack_conv(A, "t", w, b)
+    A.finalize("cuda:0")
+    cw.w, cw.b = A[cw.w], A[cw.b]
+    xd = x.to(torch.bfloat16).cuda()
+
+    def run(xb, sk):
+        y = torch.zeros(xb.shape[0], T, Co, dtype=torch.bfloat16, device="cuda:0")
+        eng.conv(cw, Act(xb, 0, Ci), _act(y), pad=k // 2, splitk=sk)
+        torch.cuda.synchronize()
+        return y
+
+    y3 = run(xd, splitk)
+    y3b = run(xd, splitk)
+    y1 = run(xd[:1].contiguous(), splitk)
+    y0 = run(xd, 0)
+    assert torch.equal(y3, y3b)
+    assert torch.equal(y3[:1], y1)
+    ref = F.conv1d(x.transpose(1, 2), bf(w), b, padding=k // 2).transpose(1, 2)
+    e = max_rel(y3.float().cpu(), ref)
+    e0 = max_rel(y3.float().cpu(), y0.float().cpu())
+    print("conv split-K", splitk, e, "vs unsplit", e0)
+    assert e < 1e-2 and e0 < 1e-2
