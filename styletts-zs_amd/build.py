@@ -22,11 +22,15 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=fast", "-Wall",
          "-Wno-unused-result", f"-I{INCLUDE}"]
-# per-file extra flags (the host compile ignores the gfx950 target feature with a warning).  source.hip: no packed
-# fp32 VALU ops -- its STFT tail, compiled to v_pk_fma_f32 with op_sel / neg modifiers, stored wrong imaginary bins
-# for 16-lane groups in ~1 of 3 two-shard concurrent replays (timing-dependent: never in a sequential replay);
-# without packed ops, 0 of 120 (tools/two_shard_stress.py)
-FILE_FLAGS = {"source.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]}
+# per-file extra flags (the host compile ignores the gfx950 target feature with a warning): no packed-fp32 VALU ops
+# where hipcc emits packed ops that SWAP a source's 32-bit halves (op_sel 1 + op_sel_hi 0 on one operand).  On MI355X
+# such an op intermittently writes wrong values for lanes 48-63 of a wave while other kernels share the CU: the
+# harmonic-source STFT built with them failed 104 of 512 swept two-shard passes, the same code with only its 7 swapped
+# operands pre-swapped by two v_mov_b32 (everything else still packed) 0 of 512 (tools/pk_bisect.py,
+# profiles/r04_*_pk_bisect*.log).  tests/test_isa_audit.py fails the build if any kernel of the
+# library contains the pattern; conv.hip's epilogues / prologues and source.hip's STFT sums are where hipcc made it.
+NO_PK = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+FILE_FLAGS = {"source.hip": NO_PK, "conv.hip": NO_PK}
 
 
 def sources():
@@ -55,10 +59,17 @@ def _deps_mtime(src):
 
 
 def _compile(src, force, verbose):
+    """compile one source unless its object is newer than every dependency AND was built by the same command:
+    the exact command line is kept in a stamp file beside the object, so a change of FLAGS / FILE_FLAGS / HIPCC
+    (or of build.py itself) rebuilds it (an object from before a codegen flag existed is never reused)"""
     obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
-    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= _deps_mtime(src):
-        return obj
+    stamp = obj + ".cmd"
     cmd = [HIPCC] + FLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
+    key = " ".join(cmd)
+    fresh = (os.path.exists(obj) and os.path.getmtime(obj) >= max(_deps_mtime(src), os.path.getmtime(__file__))
+             and os.path.exists(stamp) and open(stamp).read() == key)
+    if not force and fresh:
+        return obj
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -66,6 +77,8 @@ def _compile(src, force, verbose):
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
     if verbose and r.stderr.strip():
         print(r.stderr, file=sys.stderr)
+    with open(stamp, "w") as f:
+        f.write(key)
     return obj
 
 

@@ -29,6 +29,7 @@ extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
         if (a->ci_pad < a->Ci || a->co_pad < a->Co || a->co_pad % 128) return STZS_ESHAPE;
         if (a->ldx % 8 || a->bsx % 8) return STZS_ESHAPE;
         if (!stzs_aligned(a->x, 16) || !stzs_aligned(a->w, 16)) return STZS_EINVAL;
+        if (a->res && a->res_tdiv != 1) return STZS_EINVAL;  // the residual row is the output row (rows.hip)
         return stzs_rows_gemm_launch(*a, reinterpret_cast<hipStream_t>(stream));
     }
     return stzs_conv1d_core(a, stream);

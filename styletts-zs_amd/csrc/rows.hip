@@ -446,6 +446,7 @@ static int rows_launch(const stzs_conv_args& a, const stzs_rows_fuse* f, hipStre
         return STZS_EINVAL;
     if (a.in_dtype == STZS_F8) return STZS_EDTYPE;
     if (a.in_dtype == STZS_BF16 ? a.pro_cscale != 1.f : false) return STZS_EINVAL;
+    if (a.res && a.res_tdiv != 1) return STZS_EINVAL;  // gemm_rows reads the residual at the output row itself
     const int NK = a.ci_pad / 32;
     const int Z = a.splitk > 1 ? a.splitk : 1;
     if (a.ci_pad % 32 || NK % (4 * Z) || Z > 16) return STZS_ESHAPE;  // every wave of every slice runs the same K-step count

@@ -213,6 +213,9 @@ class StyleTTSZS:
         self.small_rows = os.environ.get("STZS_SMALL_ROWS", "1") != "0"
         # the last generator stage's noise conv fused into its ConvTranspose (bf16 engines); STZS_UPS_NOISE=0: off
         self.ups_noise_fused = os.environ.get("STZS_UPS_NOISE", "1") != "0"
+        # the first stage's strided noise conv on super-rows of the harmonic source (register-direct kernel, bf16
+        # engines); STZS_NOISE_SUPER=0: the stride-6 conv_mfma form
+        self.noise_super = os.environ.get("STZS_NOISE_SUPER", "1") != "0"
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
@@ -377,8 +380,13 @@ class StyleTTSZS:
                 a.splitk_ws = self._scratch("rows_ws", nb // 4 + 1).data_ptr()
                 a.splitk_ctr = self._counters("rows_ctr", nb // (rows * 16)).data_ptr()
             splitk = 0
-        while splitk > 1 and (cw.ci_pad // 32) % splitk:  # a function of K only: batch invariance holds
-            splitk //= 2
+        if a.flags & 8:  # LDS-DMA GEMM: the slices split the K-steps (a function of K only: batch invariance holds)
+            while splitk > 1 and (cw.ci_pad // 32) % splitk:
+                splitk //= 2
+        elif splitk > 1:  # conv_mfma: the slices split the input-channel chunks, 2 or 4 of them
+            splitk = min(splitk, 4)
+            while splitk > 1 and (cw.ci_pad // cw.cic) % splitk:
+                splitk //= 2
         if splitk > 1 and (a.flags & 8) and not cw.f8 and cw.wx3 is None and cw.w32 is None:
             # in-launch split-K (stzs_conv_args.splitk): per-branch fp32 slabs + self-resetting tile counters
             nb = self.lib.stzs_conv_splitk_workspace(x.B * x.T, cw.co_pad, splitk)
@@ -430,6 +438,8 @@ class StyleTTSZS:
             L.check(launch(), what)
             e1.record()
             flops = 2.0 * y.B * a.T_out * (cw.ups or 1) * cw.Co * cw.Ci * cw.ks
+            if cw.wx3 is not None:  # precise mode: 3 bf16 MFMA products per fp32 product (bf16x3-equivalent FLOP)
+                flops *= 3.0
             # algorithmic bytes: input tile once + output once (+ residual/acc reads), bf16/f32 as stored, + the
             # weights once (bf16; e4m3 for the fp8 linears; hi + lo for the split-operand precise form)
             wbytes = (cw.ups or 1) * cw.Co * cw.Ci * cw.ks * (1 if cw.f8 else (4 if cw.wx3 is not None else 2))
@@ -1126,7 +1136,9 @@ class StyleTTSZS:
         pref = self.buf("gen.pref", (B, nh, T80), torch.float32)
         # row pitch = the noise convs' padded K (32): the 1x1 noise conv then takes the LDS-DMA GEMM path
         dt = self.dec_dt
-        har = Act(self.buf("gen.har", (B, Tf, _rup(S.har_ch, 32)), dt, zero=True), 0, S.har_ch)
+        # rows rounded up to a multiple of the first stage's noise-conv stride (zero past Tf): the buffer then reads as
+        # whole super-rows (engine.upsample's super-row noise conv)
+        har = Act(self.buf("gen.har", (B, self._har_rows(Tf), _rup(S.har_ch, 32)), dt, zero=True), 0, S.har_ch)
         a = L.SourceArgs()
         a.f0, a.seeds, a.merge_w, a.prefix, a.har = F0.data_ptr(), sd.data_ptr(), W.t(W.src_merge).data_ptr(), \
             pref.data_ptr(), har.ptr
@@ -1137,6 +1149,11 @@ class StyleTTSZS:
         self._call(self.lib.stzs_harmonic_source, a, "harmonic_source",  # F0 in, prefix, STFT rows out
                    cost=(0, B * T80 * 4 * (1 + 2 * nh) + B * Tf * S.har_ch * har.t.element_size()))
         return har
+
+    def _har_rows(self, Tf: int) -> int:
+        """rows allocated for Tf harmonic-source frames: a multiple of the stage-0 noise-conv stride"""
+        s = math.prod(self.spec.up_rates[1:]) if len(self.spec.up_rates) > 1 else 1
+        return _rup(Tf, s)
 
     def upsample(self, x: Act, har: Act, i: int) -> Act:
         """a11: generator stage i's noise conv of the harmonic features + LeakyReLU(0.1) -> polyphase
@@ -1160,8 +1177,16 @@ class StyleTTSZS:
                       gate=self._t(nzw.nz32).data_ptr(), what=f"ups{i}")
             return xu
         xsrc = self.act(f"gen.xsrc{i}", B, Tn, c, dt)
-        if not last:
-            sf0 = int(np.prod(S.up_rates[i + 1:]))
+        sup = W.noise_sup[i] if (not last and i < len(W.noise_sup)) else None
+        sf0 = int(np.prod(S.up_rates[i + 1:])) if not last else 1
+        if (sup is not None and self.noise_super and har.dt == L.BF16 and har.t.shape[1] % sf0 == 0 and
+                har.t.shape[1] // sf0 >= Tn + 1 and sf0 * har.ld == sup.Ci):
+            # the strided noise conv on SUPER-ROWS (weights.noise_super_weights): the harmonic-source buffer read as
+            # [B, rows / s, s * 32] is a k3 stride-1 conv over 192 channels -> the register-direct kernel (mrfv.hip)
+            # instead of a stride-6 conv staging 6 rows of 64 B per output row
+            hs = har.t.view(B, har.t.shape[1] // sf0, sf0 * har.ld)
+            self.conv(sup, Act(hs), xsrc, pad=1, T_out=Tn, what=f"noise_conv{i}")
+        elif not last:
             self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, stride=sf0, pad=(sf0 + 1) // 2, what=f"noise_conv{i}")
         else:
             self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, what=f"noise_conv{i}")
@@ -1230,13 +1255,35 @@ class StyleTTSZS:
         self._call(self.lib.stzs_istft_stream, a, "istft_stream")
         return n0.value, n1.value
 
-    def decode_chunked(self, pro: dict, codes: torch.Tensor, seeds, chunk: int, halo: int):
+    @staticmethod
+    def chunk_windows(T40: int, chunk: int, halo: int):
+        """the chunked decoder's schedule (oracle/stzs_ref.py chunk_windows): chunk i owns aligned frames
+        [i chunk, min((i + 1) chunk, T40)) and is decoded over a window of fixed length W = min(chunk + 2 halo, T40)
+        starting at clamp(a - halo, 0, T40 - W).  -> [(a, b, wa, wb)]"""
+        W = min(chunk + 2 * halo, T40)
+        out = []
+        for a in range(0, T40, chunk):
+            wa = min(max(0, a - halo), T40 - W)
+            out.append((a, min(a + chunk, T40), wa, wa + W))
+        return out
+
+    def _copy_rows(self, x: int, ldx: int, bsx: int, y: int, ldy: int, bsy: int, nb: int, R: int, Cn: int, dti, dto):
+        """stzs_copy2d on raw byte addresses: nb blocks of R rows x Cn columns (source block stride bsx elements)"""
+        a = L.CopyArgs()
+        a.x, a.y, a.ldx, a.bsx, a.ldy, a.bsy = x, y, ldx, bsx, ldy, bsy
+        a.B, a.R, a.C, a.in_dtype, a.out_dtype = nb, R, Cn, dti, dto
+        self._call(self.lib.stzs_copy2d, a, "copy_windows")
+
+    def decode_chunked(self, pro: dict, codes: torch.Tensor, seeds, chunk: int, halo: int, batch_windows=True):
         """configs[4] CHUNKED streaming decoder (oracle/stzs_ref.py decode_chunked): each chunk of `chunk` aligned
-        frames is decoded over its window of +-`halo` frames -- pre-blocks and generator on the window alone, AdaIN with
-        WINDOW-local InstanceNorm statistics -- on the slice of the whole utterance's harmonic-source features (global
-        phase prefix and noise counters); its own conv_post frames go through the streaming iSTFT with the carried
-        tail.  The first chunk's audio is ready after one window's decode instead of the whole utterance's.
-        Yields (first_sample, wav chunk [B, n]) views of one [B, 600 T40] buffer."""
+        frames is decoded over its fixed-length window (chunk_windows) -- pre-blocks and generator on the window alone,
+        AdaIN with WINDOW-local InstanceNorm statistics -- on the slice of the whole utterance's harmonic-source
+        features (global phase prefix and noise counters); its own conv_post frames go through the streaming iSTFT with
+        the carried tail.  The first chunk's window is decoded alone (its audio is ready after one window's decode);
+        with batch_windows every later window is then decoded in ONE pass, the windows as the rows of one batch
+        (window-major, [window][utterance]): every decoder kernel is batch-invariant (per-utterance tiles and
+        statistics), so this is bit-identical to decoding them one by one (batch_windows=False), in 3 passes' worth of
+        launches instead of one per chunk.  Yields (first_sample, wav chunk [B, n]) views of one [B, 600 T40] buffer."""
         S = self.spec
         enc_in, F0, Nn, T40 = pro["asr_buf"], pro["F0"], pro["N"], pro["T40"]
         B = enc_in.B
@@ -1247,23 +1294,56 @@ class StyleTTSZS:
         ncol = _rup(S.n_fft + 2, 4)
         tails = [self.buf("gen.ctail0", (B, 8, ncol), torch.float32), self.buf("gen.ctail1", (B, 8, ncol), torch.float32)]
         dt = self.dec_dt
-        for i, a0 in enumerate(range(0, T40, chunk)):
-            b0 = min(a0 + chunk, T40)
-            wa, wb = max(0, a0 - halo), min(T40, b0 + halo)
-            n = wb - wa
-            enc_w = self.act("dec.enc_in_w", B, n, S.d_txt + 2, dt)
-            self.copy2d(Act(enc_in.t[:, wa:wb], 0, S.d_txt), enc_w, n, S.d_txt, bsx=enc_in.bs)
-            Tfw = fpf * n + 1
-            har_w = Act(self.buf("gen.har_w", (B, Tfw, har.ld), dt, zero=True), 0, S.har_ch)
-            self.copy2d(Act(har.t[:, fpf * wa:fpf * wb + 1], 0, S.har_ch), har_w, Tfw, S.har_ch, bsx=har.bs)
-            F0w, Nw = F0[:, 2 * wa:2 * wb], Nn[:, 2 * wa:2 * wb]
-            gen_in, gbd = self.decoder_pre(dict(asr_buf=enc_w, F0=F0w, N=Nw, T40=n), codes)
+        wins = self.chunk_windows(T40, chunk, halo)
+        Wn = wins[0][3] - wins[0][2]
+        Tfw = fpf * Wn + 1
+        groups = ([[0], list(range(1, len(wins)))] if batch_windows else [[k] for k in range(len(wins))])
+        groups = [g for g in groups if g]
+        F0c, Nc = F0.contiguous(), Nn.contiguous()
+        cdt = L.F32 if codes.dtype == torch.float32 else L.BF16
+        for ks in groups:
+            nw = len(ks)
+            Bw = nw * B
+            enc_w = self.act("dec.enc_in_w", Bw, Wn, S.d_txt + 2, dt)
+            har_w = Act(self.buf("gen.har_w", (Bw, self._har_rows(Tfw), har.ld), dt, zero=True), 0, S.har_ch)
+            F0w = self.buf("dec.F0w", (Bw, 2 * Wn), torch.float32)
+            Nw = self.buf("dec.Nw", (Bw, 2 * Wn), torch.float32)
+            cw_ = codes if nw == 1 else self.buf("dec.codes_w", (Bw,) + tuple(codes.shape[1:]), codes.dtype)
+            esz, hsz = enc_in.t.element_size(), har.t.element_size()
+            for b in range(B):
+                # runs of windows whose starts are `chunk` apart: one strided copy per run and tensor
+                i = 0
+                while i < nw:
+                    j = i + 1
+                    while j < nw and wins[ks[j]][2] - wins[ks[j - 1]][2] == chunk:
+                        j += 1
+                    wa, cnt = wins[ks[i]][2], j - i
+                    row = i * B + b  # window-major rows of the batch
+                    self._copy_rows(enc_in.t.data_ptr() + (b * enc_in.bs + wa * enc_in.ld) * esz, enc_in.ld,
+                                    chunk * enc_in.ld, enc_w.t.data_ptr() + row * enc_w.bs * esz, enc_w.ld,
+                                    B * enc_w.bs, cnt, Wn, S.d_txt, enc_in.dt, enc_w.dt)
+                    self._copy_rows(har.t.data_ptr() + (b * har.bs + fpf * wa * har.ld) * hsz, har.ld,
+                                    fpf * chunk * har.ld, har_w.t.data_ptr() + row * har_w.bs * hsz, har_w.ld,
+                                    B * har_w.bs, cnt, Tfw, S.har_ch, har.dt, har_w.dt)
+                    for src, dst in ((F0c, F0w), (Nc, Nw)):
+                        self._copy_rows(src.data_ptr() + (b * src.stride(0) + 2 * wa) * 4, 2 * Wn, 2 * chunk,
+                                        dst.data_ptr() + row * 2 * Wn * 4, 2 * Wn, B * 2 * Wn, cnt, 1, 2 * Wn,
+                                        L.F32, L.F32)
+                    i = j
+                if nw > 1:  # every window of utterance b takes its codes (source block stride 0)
+                    Lc, Dc = codes.shape[1], codes.shape[2]
+                    self._copy_rows(codes.data_ptr() + b * codes.stride(0) * codes.element_size(), Dc, 0,
+                                    cw_.data_ptr() + b * Lc * Dc * cw_.element_size(), Dc, B * Lc * Dc, nw, Lc, Dc,
+                                    cdt, cdt)
+            gen_in, gbd = self.decoder_pre(dict(asr_buf=enc_w, F0=F0w, N=Nw, T40=Wn), cw_)
             post = self.generator(gen_in, F0w, seeds, gbd, istft=False, har=har_w)
-            fin = int(b0 == T40)
-            r0 = fpf * (a0 - wa)
-            n0, n1 = self._istft_chunk(post.ptr + r0 * post.ld * 4, post.ld, post.bs, B, fpf * a0,
-                                       fpf * (b0 - a0) + fin, fin, wav, tails, i)
-            yield n0, wav[:, n0:n1]
+            for i, k in enumerate(ks):
+                a0, b0, wa, _ = wins[k]
+                fin = int(b0 == T40)
+                r0 = fpf * (a0 - wa)
+                n0, n1 = self._istft_chunk(post.ptr + (i * B * post.bs + r0 * post.ld) * 4, post.ld, post.bs, B,
+                                           fpf * a0, fpf * (b0 - a0) + fin, fin, wav, tails, k)
+                yield n0, wav[:, n0:n1]
 
     def istft_stream(self, post: Act, chunk_frames: int):
         """iSTFT of conv_post frames [B, Tf, 22] in chunks of `chunk_frames` frames,

@@ -225,6 +225,24 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
     return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16, w32=w32, wx3=wx3)
 
 
+def noise_super_weights(wn: torch.Tensor, s: int, ld: int) -> torch.Tensor:
+    """the strided noise conv of a non-last generator stage -- Conv1d(C_har -> Co, k = 2 s, stride s, pad (s + 1) // 2)
+    over the harmonic-source rows -- restated on SUPER-ROWS of s consecutive rows (s ld channels: row pos*ld + c) as a
+    k3 stride-1 conv with padding 1: out[t] = sum_tap W'[tap] . super[t + tap - 1], where tap's position pos holds
+    the original tap j = s (tap - 1) + pos + pad (zero where j falls outside [0, 2 s), and for c >= C_har).
+    -> W' [Co, s ld, 3]"""
+    Co, Ch, k = wn.shape
+    assert k == 2 * s and Ch <= ld
+    pad = (s + 1) // 2
+    w = torch.zeros(Co, s * ld, 3)
+    for tap in range(3):
+        for pos in range(s):
+            j = s * (tap - 1) + pos + pad
+            if 0 <= j < k:
+                w[:, pos * ld:pos * ld + Ch, tap] = wn[:, :, j]
+    return w
+
+
 def pack_ups_noise(A: Arena, name, wu, bu, wn, bn) -> ConvW:
     """the last generator stage's polyphase ConvTranspose1d with its 1x1 noise conv fused (csrc/ups.hip,
     STZS_CONV_UPS_NOISE): wu [Ci, Co, 2 r] / bu [Co] the ConvTranspose, wn [Co, C_har, 1] / bn [Co] the noise conv.
@@ -498,10 +516,19 @@ class PackedModel:
             self.dec_blk[nm] = pack_blk(A, P, nm, up=up, x3=xd)
             dec_norms += blk_norms(nm)
         self.src_merge = A.add("gen.src_merge", torch.cat([P["gen.src_merge.w"].reshape(-1), P["gen.src_merge.b"]]).float())
-        self.noise_conv, self.ups, self.rb, self.ups_nz = [], [], [], []
+        self.noise_conv, self.ups, self.rb, self.ups_nz, self.noise_sup = [], [], [], [], []
         for i, (r, k) in enumerate(zip(S.up_rates, S.up_kernels)):
             self.noise_conv.append(pack_conv(A, f"gen.noise_conv{i}", P[f"gen.noise_conv{i}.w"], P[f"gen.noise_conv{i}.b"],
                                              x3=xd))
+            # a strided noise conv restated on super-rows of the harmonic source (k3 stride 1 over s*32 channels, the
+            # register-direct kernel; engine.upsample): bf16 engines
+            sf0 = math.prod(S.up_rates[i + 1:])
+            wn0 = P[f"gen.noise_conv{i}.w"]
+            self.noise_sup.append(
+                pack_conv(A, f"gen.noise_sup{i}", noise_super_weights(wn0, sf0, 32), P[f"gen.noise_conv{i}.b"],
+                          frag32=True)
+                if (i < len(S.up_rates) - 1 and not xd and wn0.shape[2] == 2 * sf0 and wn0.shape[1] <= 32 and
+                    sf0 * 32 > 128 and wn0.shape[0] % 8 == 0) else None)
             wu = P[f"gen.ups{i}.w"]  # ConvTranspose1d [Ci, Co, 2r]
             # 128-channel input chunks, Co % 32 == 0: the input-staged-once polyphase kernel (csrc/ups.hip)
             self.ups.append(pack_conv(A, f"gen.ups{i}", wu, P[f"gen.ups{i}.b"], ups=r,

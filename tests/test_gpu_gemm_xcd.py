@@ -93,40 +93,90 @@ def test_conv_mfma_xcd_order_bit_identical(eng, R, T, Ci, Co, k):
     assert e < 1e-2
 
 
+SPLITK_CASES = [  # (B, T, Ci, Co, k, epilogue): the text-encoder shape, then T_out > 128 (several row tiles per
+    # utterance) with a residual, fused statistics, accumulate into a separate buffer and in place, a 1x1 conv
+    (3, 80, 512, 512, 5, "plain"),
+    (3, 300, 512, 256, 3, "res"),
+    (3, 300, 512, 256, 3, "stats"),
+    (3, 300, 512, 256, 3, "acc"),
+    (3, 300, 512, 256, 3, "acc_inplace"),
+    (2, 200, 512, 384, 1, "leaky"),  # 1x1 with a prologue: conv_mfma, not the LDS-DMA GEMM
+]
+
+
 @pytest.mark.parametrize("splitk", [2, 4])
-def test_conv_mfma_splitk(eng, splitk):
+@pytest.mark.parametrize("case", SPLITK_CASES, ids=lambda c: f"B{c[0]}-T{c[1]}-k{c[4]}-{c[5]}")
+def test_conv_mfma_splitk(eng, splitk, case):
     """conv_mfma in-launch split-K over input-channel chunks (the latency engine's text-encoder k5 convs,
-    LATENCY_TE_SPLITK): matches F.conv1d on the same bf16 operands, utterance 0 of a 3-utterance launch is
-    bit-identical to the 1-utterance launch (per-utterance tiles: batch-invariant), a re-run is bit-identical (the
-    self-resetting tile tickets), and the result is within fp32 re-association of the unsplit conv."""
+    LATENCY_TE_SPLITK) through the last arriver's full epilogue (residual, alpha / beta accumulate incl. y == acc_in,
+    fused InstanceNorm statistics partials), T_out > 128 and a 1x1 conv: matches F.conv1d on the same bf16 operands,
+    utterance 0 of a B-utterance launch is bit-identical to the 1-utterance launch (per-utterance tiles:
+    batch-invariant), a re-run is bit-identical (the self-resetting tile tickets), and the result is within fp32
+    re-association of the unsplit conv (statistics included)."""
     from stzs import _lib as L
     from stzs.engine import Act
     from stzs.weights import Arena, pack_conv
-    T, Ci, Co, k = 80, 512, 512, 5
-    g = torch.Generator().manual_seed(100 + splitk)
-    x = bf(torch.randn(3, T, Ci, generator=g))
+    B, T, Ci, Co, k, epi = case
+    g = torch.Generator().manual_seed(100 + splitk + T + k)
+    x = bf(torch.randn(B, T, Ci, generator=g))
     w = torch.randn(Co, Ci, k, generator=g) / math.sqrt(Ci * k)
     b = torch.randn(Co, generator=g) * 0.1
+    r = bf(torch.randn(B, T, Co, generator=g))
+    acc = bf(torch.randn(B, T, Co, generator=g))
     A = Arena()
     cw = pack_conv(A, "t", w, b)
     A.finalize("cuda:0")
     cw.w, cw.b = A[cw.w], A[cw.b]
     xd = x.to(torch.bfloat16).cuda()
+    rd = r.to(torch.bfloat16).cuda()
+    accd = acc.to(torch.bfloat16).cuda()
+    alpha, beta = (0.7, 0.5) if epi.startswith("acc") else (1.0, 0.0)
 
-    def run(xb, sk):
-        y = torch.zeros(xb.shape[0], T, Co, dtype=torch.bfloat16, device="cuda:0")
-        eng.conv(cw, Act(xb, 0, Ci), _act(y), pad=k // 2, splitk=sk)
+    def run(n, sk):
+        xb = xd[:n].contiguous()
+        a0 = accd[:n].clone()
+        y = a0 if epi == "acc_inplace" else torch.zeros(n, T, Co, dtype=torch.bfloat16, device="cuda:0")
+        kw = dict(pad=k // 2, splitk=sk)
+        if epi == "leaky":
+            kw.update(pro_act=L.ACT_LEAKY, pro_slope=0.2)
+        if epi == "res":
+            kw["res"] = _act(rd[:n].contiguous())
+        if epi.startswith("acc"):
+            kw.update(acc_in=_act(a0), alpha=alpha, beta=beta)
+        if epi == "stats":
+            kw["stats_key"] = f"t.sk{sk}.{n}"
+        out = eng.conv(cw, Act(xb, 0, Ci), _act(y), **kw)
         torch.cuda.synchronize()
-        return y
+        st = None
+        if epi == "stats":
+            st = (out[1][0].clone(), out[1][1].clone())
+        return y.clone(), st
 
-    y3 = run(xd, splitk)
-    y3b = run(xd, splitk)
-    y1 = run(xd[:1].contiguous(), splitk)
-    y0 = run(xd, 0)
+    y3, s3 = run(B, splitk)
+    y3b, s3b = run(B, splitk)
+    y1, s1 = run(1, splitk)
+    y0, s0 = run(B, 0)
     assert torch.equal(y3, y3b)
     assert torch.equal(y3[:1], y1)
-    ref = F.conv1d(x.transpose(1, 2), bf(w), b, padding=k // 2).transpose(1, 2)
+    xin = bf(F.leaky_relu(x, 0.2)) if epi == "leaky" else x
+    ref = F.conv1d(xin.transpose(1, 2), bf(w), b, padding=k // 2).transpose(1, 2)
+    if epi == "res":
+        ref = ref + r
+    if epi.startswith("acc"):
+        ref = ref * alpha + beta * acc
     e = max_rel(y3.float().cpu(), ref)
     e0 = max_rel(y3.float().cpu(), y0.float().cpu())
-    print("conv split-K", splitk, e, "vs unsplit", e0)
+    print("conv split-K", case, splitk, e, "vs unsplit", e0)
     assert e < 1e-2 and e0 < 1e-2
+    if epi == "stats":
+        assert torch.equal(s3[0], s3b[0]) and torch.equal(s3[1], s3b[1])
+        assert torch.equal(s3[0][:1], s1[0]) and torch.equal(s3[1][:1], s1[1])
+        yf = y3.double().cpu()  # the statistics of the STORED bf16 output, in fp64
+        m_ref = yf.mean(1)
+        r_ref = 1.0 / torch.sqrt(yf.var(1, unbiased=False) + 1e-5)
+        em = (s3[0].cpu().double() - m_ref).abs().max().item()
+        er = max_rel(s3[1].cpu().double(), r_ref)
+        eu = (s3[0] - s0[0]).abs().max().item(), max_rel(s3[1].cpu(), s0[1].cpu())
+        print("   stats: mean abs err", em, "rstd rel err", er, "vs unsplit", eu)
+        assert em < 1e-4 and er < 3e-4
+        assert eu[0] < 1e-4 and eu[1] < 3e-4  # the unsplit conv's bf16 output differs by re-association roundings

@@ -219,6 +219,38 @@ def test_convtranspose_fused_noise_conv(eng, B, T, Ci, Co, s, Ch):
     assert e < 1.5e-2 and e0 < 1.5e-2 and eu < 2e-2
 
 
+@pytest.mark.parametrize("B,T80", [(2, 20), (3, 57)])
+def test_noise_conv_super_rows(gpu_device, B, T80):
+    """generator stage 0 with its stride-6 noise conv restated on super-rows of the harmonic source (engine.upsample,
+    weights.noise_super_weights: a k3 stride-1 conv over 192 channels on the register-direct kernel) vs the oracle's
+    upsample_stage (fp32: LeakyReLU, strided noise conv, ConvTranspose1d, sum) on the same bf16 inputs, and vs the
+    stride-6 conv_mfma path (STZS_NOISE_SUPER=0): within bf16 rounding of each (v0 dims)."""
+    from oracle import stzs_ref as R
+    from stzs.engine import Act, StyleTTSZS
+    from stzs.params import init_params
+    from stzs.spec import SPEC_V0
+    S = SPEC_V0
+    P = init_params(S, seed=0)
+    e = StyleTTSZS(S, P, device=gpu_device)
+    assert e.W.noise_sup[0] is not None
+    g = torch.Generator().manual_seed(B * 100 + T80)
+    F0 = (100 + 150 * torch.rand(B, T80, generator=g)).to(gpu_device)
+    har = e.sine_gen(F0, list(range(B)))
+    x = bf(torch.randn(B, T80, S.dec_out, generator=g))
+    ys = []
+    for sup in (True, False):
+        e.noise_super = sup
+        ys.append(e.upsample(Act(x.to(torch.bfloat16).to(gpu_device)), har, 0).t.float().cpu().clone())
+    torch.cuda.synchronize()
+    Tf = T80 * S.hop // S.istft_hop + 1
+    hn = har.t[:, :Tf, :S.har_ch].float().cpu().transpose(1, 2)
+    ref = R.upsample_stage(P, S, x.transpose(1, 2), hn, 0).transpose(1, 2)
+    e_ref, e_alt = max_rel(ys[0], ref), max_rel(ys[0], ys[1])
+    print("noise conv on super-rows: vs oracle", e_ref, "vs stride-6 path", e_alt, "| stride-6 vs oracle", max_rel(ys[1], ref))
+    assert ys[0].shape == ref.shape
+    assert e_ref < 1.5e-2 and e_alt < 1.5e-2
+
+
 def test_chan_stats(eng):
     """InstanceNorm statistics: fp32 partials + fixed-order fp64 combine; 1e-5 relative."""
     g = torch.Generator().manual_seed(3)

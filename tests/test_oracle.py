@@ -273,4 +273,5 @@ def test_decode_chunked_reduces_to_decode(tiny, tiny_params):
     w3, _ = R.decode_chunked(P, S, asr, F0, N, codes, [3, 4], chunk=8, halo=3)
     assert w3.shape == full.shape and torch.isfinite(w3).all()
     assert ((w3 - full).norm() / full.norm()).item() > 1e-3
-    assert R.chunk_windows(23, 8, 3) == [(0, 8, 0, 11), (8, 16, 5, 19), (16, 23, 13, 23)]
+    # fixed-length windows (W = chunk + 2 halo = 14), the first and last shifted inward
+    assert R.chunk_windows(23, 8, 3) == [(0, 8, 0, 14), (8, 16, 5, 19), (16, 23, 9, 23)]

@@ -2,7 +2,7 @@
 many times in one process and say WHICH output of which shard diverges from the sequential replay (codes, F0, N,
 decoder wav), to localise a timing-dependent mismatch.
 
-    python tools/two_shard_stress.py      (env: ITERS=40, BRANCH=1 (branch_streams), NB=8)
+    python tools/two_shard_stress.py      (env: ITERS=40, BRANCH=1 (branch_streams), NB=8, SWEEP_US=0, BUFS=1)
 """
 import os
 import sys
@@ -20,6 +20,7 @@ dev = "cuda:0"
 iters = int(os.environ.get("ITERS", 40))
 branch = os.environ.get("BRANCH", "1") == "1"
 nb = int(os.environ.get("NB", 8))
+sweep = float(os.environ.get("SWEEP_US", 0))  # shard-1 start offset step per iteration (us, 32 steps; tools/pk_bisect.py)
 S = SPEC_V0
 eng = StyleTTSZS(S, init_params(S, seed=0), device=dev)
 tok, ref, eps, dur, seeds = bench.rank_inputs(S, 2 * nb, 0)
@@ -81,6 +82,8 @@ for it in range(iters):
             with torch.cuda.stream(s):
                 if rep == 0 and j == 1:
                     s.wait_event(ev)
+                    if sweep:
+                        torch.cuda._sleep(int((it % 32) * sweep * 1e-6 * 2.4e9))
                 ga.replay()
                 if rep == 0 and j == 0:
                     ev.record(s)
