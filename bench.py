@@ -272,18 +272,22 @@ def stage_roofline(eng, S, tok_d, ref_d, eps_d, dur_d, seeds, n_frames):
                 stages=out, families=fams, top_tags=top)
 
 
-def precise_mode(S, P, dev, B=64, steps=5):
+def precise_mode(S, P, dev, B=64, steps=5, nstream=2):
     """throughput of the PRECISE mode -- the whole pipeline (text encoder, style diffusion, predictor, decoder) on
     fp32 activations and split-operand bf16x3 products, the mode that meets the north-star log-mel L1 <= 1e-3
     END TO END (tests/test_gpu_precise.py: 4.2e-4 at configs[1]) -- on the throughput workload (batch 64, 5-s
-    targets, 2-step CFG 5), one graph-replayed stream."""
+    targets, 2-step CFG 5): replayed as the main leg is, two shards on two streams (shard_runner), and as one graph
+    on one stream beside it."""
     from stzs.engine import StyleTTSZS
     ep = StyleTTSZS(S, P, device=dev, precise=True)
-    tok, ref, eps, dur = (t.to(dev) for t in make_inputs(S, B, 7))
+    host_src = make_inputs(S, B, 7)
+    tok, ref, eps, dur = (t.to(dev) for t in host_src)
     nf = int(dur[0].sum())
+    seeds = list(range(B))
     fn = lambda: ep.synth(tok, ref, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps, durations=dur,
-                          seeds=list(range(B)), n_frames=nf, check=False)
-    fn()
+                          seeds=seeds, n_frames=nf, check=False)
+    o = fn()
+    nwav = o["wav"].shape[1]
     g, _ = ep.capture(fn)
     g.replay()
     torch.cuda.synchronize()
@@ -291,17 +295,112 @@ def precise_mode(S, P, dev, B=64, steps=5):
     for _ in range(steps):
         g.replay()
     torch.cuda.synchronize()
+    el1 = (time.perf_counter() - t0) / steps
+    del g
+    run_steps, twins, _ = shard_runner(ep, S, dev, tok, ref, eps, dur, seeds, nf, nstream, True, None, host_src, nwav)
+    run_steps(1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_steps(steps)
+    torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps
-    lstm_to = int(ep.status.item())
+    lstm_to = int(ep.status.item()) + sum(int(t.status.item()) for t in twins)
     # where the precise step goes: the per-stage / per-family roofline of one eager pass, conv / linear FLOP counted
     # bf16x3-equivalent (3 bf16 MFMA products per fp32 product), so frac is against the bf16 MFMA peak
-    st = stage_roofline(ep, S, tok, ref, eps, dur, list(range(B)), nf)
-    del g, ep
+    st = stage_roofline(ep, S, tok, ref, eps, dur, seeds, nf)
+    del run_steps, twins, ep
     torch.cuda.empty_cache()
     return dict(config=f"batch {B}, 5-s targets, 2-step CFG-5, precise mode (fp32 activations, split-operand "
-                       f"bf16x3 convs / linears / LSTM / attention in every stage)",
-                audio_s_per_s=round(B * TARGET_S / el, 1), ms_per_step=round(el * 1e3, 2), lstm_status=lstm_to,
-                stages=st)
+                       f"bf16x3 convs / linears / LSTM / attention in every stage); {nstream} shards on {nstream} "
+                       f"streams as the main leg",
+                audio_s_per_s=round(B * TARGET_S / el, 1), ms_per_step=round(el * 1e3, 2),
+                single_stream_audio_s_per_s=round(B * TARGET_S / el1, 1), lstm_status=lstm_to, stages=st)
+
+
+def shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstream, stagger, pidx, host_src, nwav,
+                 steps=STEPS_THROUGHPUT, cfg=CFG):
+    """the per-GPU batch as `nstream` (near-)equal shards on engine twins (shared weights, own buffers), each captured
+    as two graphs -- front (text, prompt, style diffusion, prosody) and back (decoder) -- replayed on its own stream;
+    shard j > 0 starts one front phase behind shard 0 (stagger), so one shard's latency-bound front (LSTM recurrences,
+    small GEMMs) runs beside another's decoder convs.  A step is one front + one back of every shard; steps are not
+    joined, the timed region ends with a synchronize after the last one.
+    Host-to-host steps (h2h=True): per shard one H2D and one D2H copy stream, ordered by events so the copies overlap
+    the shard's other phase -- step i+1's inputs go in once step i's front graph has read them (during its back graph),
+    step i's waveform comes out during step i+1's front graph, and back graph i+1 waits for that D2H.
+    -> (run_steps(k, h2h=False), twins, host buffers {tok, ref, eps, dur, wav} (pinned))"""
+    B = tok_d.shape[0]
+    sizes = [B // nstream + (1 if i < B % nstream else 0) for i in range(nstream)]
+    pairs, twins = [], []
+    for i in range(nstream):
+        tw = eng.twin()
+        twins.append(tw)
+        sl = slice(sum(sizes[:i]), sum(sizes[:i + 1]))
+        st_ = {}
+
+        def front(tw=tw, sl=sl, st_=st_):
+            h, pr = tw.encode_inputs(tok_d[sl], ref_d[sl], pidx)
+            if pr.shape[0] == 1 and sl.stop - sl.start > 1:  # shared speaker: one prompt for the shard
+                pe = tw.buf("prompt.bc", (sl.stop - sl.start, S.L_s, S.code_dim), pr.dtype)
+                pe.copy_(pr.expand(pe.shape[0], -1, -1))
+                pr = pe
+            codes = tw.sample_style(h, pr, eps_d[sl], steps, cfg)
+            st_["codes"], st_["pro"] = codes, tw.predict_prosody(h, codes, dur_d[sl], n_frames)
+
+        def back(tw=tw, sl=sl, st_=st_):
+            return tw.decode(st_["pro"], st_["codes"], seeds[sl])
+        front()
+        back()
+        ga = tw.capture(front)[0]
+        gb, wv = tw.capture(back)
+        pairs.append((ga, gb, sl, wv))
+    streams = [torch.cuda.Stream(dev) for _ in range(nstream)]
+    h2d_streams = [torch.cuda.Stream(dev) for _ in range(nstream)]
+    d2h_streams = [torch.cuda.Stream(dev) for _ in range(nstream)]
+    host = dict(zip(("tok", "ref", "eps", "dur"), (t.pin_memory() for t in host_src)))
+    host["wav"] = torch.empty(B, nwav, dtype=torch.float32).pin_memory()
+
+    def run_steps(k, h2h=False):
+        cur = torch.cuda.current_stream(dev)
+        for st in streams + (h2d_streams + d2h_streams if h2h else []):
+            st.wait_stream(cur)
+        ev = torch.cuda.Event()
+        front_done = [torch.cuda.Event() for _ in range(nstream)]
+        back_done = [torch.cuda.Event() for _ in range(nstream)]
+        in_ready = [torch.cuda.Event() for _ in range(nstream)]
+        out_done = [torch.cuda.Event() for _ in range(nstream)]
+        for i in range(k):
+            for j, (st, (ga, gb, sl, wv)) in enumerate(zip(streams, pairs)):
+                if h2h:  # this shard's inputs in from pinned host memory
+                    with torch.cuda.stream(h2d_streams[j]):
+                        if i > 0:
+                            h2d_streams[j].wait_event(front_done[j])
+                        for d_, h_ in ((tok_d, host["tok"]), (ref_d, host["ref"]), (eps_d, host["eps"]),
+                                       (dur_d, host["dur"])):
+                            d_[sl].copy_(h_[sl], non_blocking=True)
+                        in_ready[j].record(h2d_streams[j])
+                with torch.cuda.stream(st):
+                    if i == 0 and j > 0 and stagger:
+                        st.wait_event(ev)
+                    if h2h:
+                        st.wait_event(in_ready[j])
+                    ga.replay()
+                    if h2h:
+                        front_done[j].record(st)
+                    if i == 0 and j == 0:
+                        ev.record(st)
+                    if h2h and i > 0:
+                        st.wait_event(out_done[j])
+                    gb.replay()
+                    if h2h:
+                        back_done[j].record(st)
+                if h2h:  # and its waveform back
+                    with torch.cuda.stream(d2h_streams[j]):
+                        d2h_streams[j].wait_event(back_done[j])
+                        host["wav"][sl].copy_(wv, non_blocking=True)
+                        out_done[j].record(d2h_streams[j])
+        for st in streams + (h2d_streams + d2h_streams if h2h else []):
+            cur.wait_stream(st)
+    return run_steps, twins, host
 
 
 def main():
@@ -377,92 +476,21 @@ def main():
     nstream = min(args.streams, B) if (graph is not None and args.streams > 1) else 1
     twins = [eng]
     if nstream > 1:
-        # the batch as `nstream` (near-)equal shards on engine twins (shared weights, own buffers), each captured as
-        # two graphs -- front (text, prompt, style diffusion, prosody) and back (decoder) -- replayed on its
-        # own stream; shard j > 0 starts one front phase behind shard 0, so one shard's latency-bound front
-        # (LSTM recurrences, small GEMMs) runs beside another's decoder convs.  A step is still one front +
-        # one back of every shard (64 utterances per GPU); steps are not joined, the timed region ends with
-        # a synchronize after the last one.
-        sizes = [B // nstream + (1 if i < B % nstream else 0) for i in range(nstream)]
-        pairs = []
-        for i in range(nstream):
-            tw = eng.twin()
-            twins.append(tw)
-            sl = slice(sum(sizes[:i]), sum(sizes[:i + 1]))
-            st_ = {}
-
-            def front(tw=tw, sl=sl, st_=st_):
-                h, pr = tw.encode_inputs(tok_d[sl], ref_d[sl], pidx)
-                if pr.shape[0] == 1 and sl.stop - sl.start > 1:  # shared speaker: one prompt for the shard
-                    pe = tw.buf("prompt.bc", (sl.stop - sl.start, S.L_s, S.code_dim), torch.float32)
-                    pe.copy_(pr.expand(pe.shape[0], -1, -1))
-                    pr = pe
-                codes = tw.sample_style(h, pr, eps_d[sl], STEPS_THROUGHPUT, CFG)
-                st_["codes"], st_["pro"] = codes, tw.predict_prosody(h, codes, dur_d[sl], n_frames)
-
-            def back(tw=tw, sl=sl, st_=st_):
-                return tw.decode(st_["pro"], st_["codes"], seeds[sl])
-            front()
-            back()
-            ga = tw.capture(front)[0]
-            gb, wv = tw.capture(back)
-            pairs.append((ga, gb, sl, wv))
-        streams = [torch.cuda.Stream(dev) for _ in range(nstream)]
-        # host-to-host steps: per shard one H2D and one D2H copy stream, ordered by events so the copies overlap the
-        # shard's other phase -- step i+1's inputs go in once step i's front graph has read them (during its back
-        # graph), step i's waveform comes out during step i+1's front graph, and back graph i+1 waits for that D2H
-        h2d_streams = [torch.cuda.Stream(dev) for _ in range(nstream)]
-        d2h_streams = [torch.cuda.Stream(dev) for _ in range(nstream)]
-
-        def run_steps(k, h2h=False):
-            cur = torch.cuda.current_stream(dev)
-            for st in streams + (h2d_streams + d2h_streams if h2h else []):
-                st.wait_stream(cur)
-            ev = torch.cuda.Event()
-            front_done = [torch.cuda.Event() for _ in range(nstream)]
-            back_done = [torch.cuda.Event() for _ in range(nstream)]
-            in_ready = [torch.cuda.Event() for _ in range(nstream)]
-            out_done = [torch.cuda.Event() for _ in range(nstream)]
-            for i in range(k):
-                for j, (st, (ga, gb, sl, wv)) in enumerate(zip(streams, pairs)):
-                    if h2h:  # this shard's inputs in from pinned host memory
-                        with torch.cuda.stream(h2d_streams[j]):
-                            if i > 0:
-                                h2d_streams[j].wait_event(front_done[j])
-                            for d_, h_ in ((tok_d, tok_h), (ref_d, ref_h), (eps_d, eps_h), (dur_d, dur_h)):
-                                d_[sl].copy_(h_[sl], non_blocking=True)
-                            in_ready[j].record(h2d_streams[j])
-                    with torch.cuda.stream(st):
-                        if i == 0 and j > 0 and args.stagger:
-                            st.wait_event(ev)
-                        if h2h:
-                            st.wait_event(in_ready[j])
-                        ga.replay()
-                        if h2h:
-                            front_done[j].record(st)
-                        if i == 0 and j == 0:
-                            ev.record(st)
-                        if h2h and i > 0:
-                            st.wait_event(out_done[j])
-                        gb.replay()
-                        if h2h:
-                            back_done[j].record(st)
-                    if h2h:  # and its waveform back
-                        with torch.cuda.stream(d2h_streams[j]):
-                            d2h_streams[j].wait_event(back_done[j])
-                            wav_h[sl].copy_(wv, non_blocking=True)
-                            out_done[j].record(d2h_streams[j])
-            for st in streams + (h2d_streams + d2h_streams if h2h else []):
-                cur.wait_stream(st)
+        run_steps, tws, host = shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstream,
+                                            bool(args.stagger), pidx, (tok, ref, eps, dur), out["wav"].shape[1])
+        twins += tws
     else:
+        host = {}
+
         def run_steps(k, h2h=False):
             for _ in range(k):
                 if h2h:
-                    for d_, h_ in ((tok_d, tok_h), (ref_d, ref_h), (eps_d, eps_h), (dur_d, dur_h)):
+                    for d_, h_ in ((tok_d, host["tok"]), (ref_d, host["ref"]), (eps_d, host["eps"]),
+                                   (dur_d, host["dur"])):
                         d_.copy_(h_, non_blocking=True)
                 run()
                 if h2h:
-                    wav_h.copy_(out["wav"], non_blocking=True)
+                    host["wav"].copy_(out["wav"], non_blocking=True)
     run_steps(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
@@ -475,8 +503,9 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     # the same steps host to host (inputs from pinned host memory, waveform back): reported beside `value`
-    tok_h, ref_h, eps_h, dur_h = (t.pin_memory() for t in (tok, ref, eps, dur))
-    wav_h = torch.empty(B, out["wav"].shape[1], dtype=torch.float32).pin_memory()
+    if not host:
+        host.update(zip(("tok", "ref", "eps", "dur"), (t.pin_memory() for t in (tok, ref, eps, dur))))
+        host["wav"] = torch.empty(B, out["wav"].shape[1], dtype=torch.float32).pin_memory()
     run_steps(1, h2h=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -616,7 +645,7 @@ def main():
             "lstm_timeouts": lstm_timeouts,
             "host_to_host": {"value": round(world * B * audio_s * args.steps / el_h2h, 2), "unit": "audio-s/s",
                              "ms_per_step": round(el_h2h / args.steps * 1e3, 3), "h2d_bytes_per_step": h2d_bytes,
-                             "d2h_bytes_per_step": int(wav_h.numel() * 4),
+                             "d2h_bytes_per_step": int(host["wav"].numel() * 4),
                              "note": "inputs copied in from pinned host memory and the waveform copied back inside "
                                      "every step, on the shard streams"},
             "longform": lf,

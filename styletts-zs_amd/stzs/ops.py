@@ -250,19 +250,29 @@ def _(post, tail, f0, final, n_fft, hop):
 
 
 # ------------------------------------------------------------------ per-row operators (SURVEY §8(b) list)
-# Activations cross this boundary channels-last, [B, T, C] (the kernels' layout; a torch Conv1d NCT tensor is
-# x.transpose(1, 2)); outputs are fp32 copies.
+# Activations cross this boundary channels-last, [B, T, C] (the kernels' layout) by default; with nct=True they
+# cross as torch Conv1d tensors, [B, C, T] (SURVEY §8(b) "NCT at the boundary"): the transpose is folded into the
+# copy each operator already makes into / out of the engine's buffers (no extra pass).  Outputs are fp32 copies.
 
-def _out(view: torch.Tensor) -> torch.Tensor:
-    """an fp32 COPY of an engine buffer view: never the view itself (in fp32 engines `.float()` would return the
-    cached buffer, which the next call of the op overwrites), so outputs never alias engine storage."""
+def _out(view: torch.Tensor, nct: bool = False) -> torch.Tensor:
+    """an fp32 COPY of an engine buffer view [B, T, C] ([B, C, T] with nct): never the view itself (in fp32 engines
+    `.float()` would return the cached buffer, which the next call of the op overwrites), so outputs never alias
+    engine storage."""
+    if nct:
+        return view.transpose(1, 2).to(torch.float32, memory_format=torch.contiguous_format, copy=True)
     return view.to(torch.float32, copy=True)
 
 
-def _act_in(eng, key, x: torch.Tensor, dtype=None):
-    """x [B, T, C] -> an engine Act (row pitch padded to 8) holding x in `dtype` (default: the engine's
-    activation dtype, fp32 in precise mode)."""
+def _ntc(x: torch.Tensor, nct: bool) -> torch.Tensor:
+    """the channels-last view of an operand given as [B, T, C], or as [B, C, T] with nct (a view, no copy)"""
+    return x.transpose(1, 2) if nct else x
+
+
+def _act_in(eng, key, x: torch.Tensor, dtype=None, nct: bool = False):
+    """x [B, T, C] ([B, C, T] with nct) -> an engine Act (row pitch padded to 8) holding x in `dtype` (default: the
+    engine's activation dtype, fp32 in precise mode); the copy into the buffer does the transpose."""
     from .engine import Act
+    x = _ntc(x, nct)
     dtype = eng.adt if dtype is None else dtype
     B, T, Cn = x.shape
     t = eng.buf("op." + key, (B, T, (Cn + 7) // 8 * 8), dtype, zero=True)
@@ -322,100 +332,113 @@ def _(handle, h_txt, prompt, x, sigma, cfg):
 
 
 @custom_op("stzs::f0n_predictor", mutates_args=(), device_types="cuda")
-def f0n_predictor(handle: int, en: torch.Tensor, codes: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """a8: aligned predictor features en [B, T40, pr_in], codes [B, L_s, code] -> (F0, N) fp32 [B, 2 T40]."""
+def f0n_predictor(handle: int, en: torch.Tensor, codes: torch.Tensor, nct: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """a8: aligned predictor features en [B, T40, pr_in] ([B, pr_in, T40] with nct), codes [B, L_s, code] -> (F0, N)
+    fp32 [B, 2 T40]."""
     eng = _eng(handle, en, codes)
-    F0, Nn = eng.f0n_predictor(_act_in(eng, "en", en), codes.float().contiguous())
+    F0, Nn = eng.f0n_predictor(_act_in(eng, "en", en, nct=nct), codes.float().contiguous())
     eng.check_status()
     return F0.contiguous().clone(), Nn.contiguous().clone()
 
 
 @register_fake("stzs::f0n_predictor")
-def _(handle, en, codes):
-    B, T40 = en.shape[0], en.shape[1]
+def _(handle, en, codes, nct=False):
+    B, T40 = en.shape[0], en.shape[2 if nct else 1]
     return en.new_empty((B, 2 * T40), dtype=torch.float32), en.new_empty((B, 2 * T40), dtype=torch.float32)
 
 
 @custom_op("stzs::decoder_pre", mutates_args=(), device_types="cuda")
-def decoder_pre(handle: int, asr: torch.Tensor, F0: torch.Tensor, N: torch.Tensor, codes: torch.Tensor) -> torch.Tensor:
-    """a9: asr [B, T40, d_txt], F0 / N [B, 2 T40], codes [B, L_s, code] -> generator input fp32 [B, 2 T40, dec_out]."""
+def decoder_pre(handle: int, asr: torch.Tensor, F0: torch.Tensor, N: torch.Tensor, codes: torch.Tensor,
+                nct: bool = False) -> torch.Tensor:
+    """a9: asr [B, T40, d_txt], F0 / N [B, 2 T40], codes [B, L_s, code] -> generator input fp32 [B, 2 T40, dec_out]
+    (nct: asr [B, d_txt, T40] in, [B, dec_out, 2 T40] out)."""
     eng = _eng(handle, asr, F0, N, codes)
     S = eng.spec
+    asr = _ntc(asr, nct)
     B, T40, D = asr.shape
     enc_in = eng.act("dec.enc_in", B, T40, S.d_txt + 2, eng.dec_dt)
     enc_in.t[:, :, :D].copy_(asr)
     pro = dict(asr_buf=enc_in, F0=F0.float().contiguous(), N=N.float().contiguous(), T40=T40)
     gen_in, _ = eng.decoder_pre(pro, codes.float().contiguous())
-    return _out(gen_in.t[:, :, :S.dec_out])
+    return _out(gen_in.t[:, :, :S.dec_out], nct)
 
 
 @register_fake("stzs::decoder_pre")
-def _(handle, asr, F0, N, codes):
-    return asr.new_empty((asr.shape[0], 2 * asr.shape[1], _spec(handle).dec_out), dtype=torch.float32)
+def _(handle, asr, F0, N, codes, nct=False):
+    T40 = asr.shape[2 if nct else 1]
+    shp = (asr.shape[0], _spec(handle).dec_out, 2 * T40) if nct else (asr.shape[0], 2 * T40, _spec(handle).dec_out)
+    return asr.new_empty(shp, dtype=torch.float32)
 
 
 @custom_op("stzs::sine_gen", mutates_args=(), device_types="cuda")
-def sine_gen(handle: int, F0: torch.Tensor, seeds: List[int]) -> torch.Tensor:
-    """a10: harmonic source of F0 [B, T80] and its n_fft STFT -> (real | imag) fp32 [B, T80 hop / hop_s + 1, n_fft + 2]."""
+def sine_gen(handle: int, F0: torch.Tensor, seeds: List[int], nct: bool = False) -> torch.Tensor:
+    """a10: harmonic source of F0 [B, T80] and its n_fft STFT -> (real | imag) fp32 [B, T80 hop / hop_s + 1, n_fft + 2]
+    ([B, n_fft + 2, Tf] with nct)."""
     eng = _eng(handle, F0)
     S = eng.spec
     har = eng.sine_gen(F0.float().contiguous(), list(seeds))
-    return _out(har.t[:, :, :S.har_ch])
+    Tf = F0.shape[1] * S.hop // S.istft_hop + 1  # (the engine's buffer has rows up to a multiple of the noise stride)
+    return _out(har.t[:, :Tf, :S.har_ch], nct)
 
 
 @register_fake("stzs::sine_gen")
-def _(handle, F0, seeds):
+def _(handle, F0, seeds, nct=False):
     S = _spec(handle)
-    return F0.new_empty((F0.shape[0], F0.shape[1] * S.hop // S.istft_hop + 1, S.har_ch), dtype=torch.float32)
+    Tf = F0.shape[1] * S.hop // S.istft_hop + 1
+    return F0.new_empty((F0.shape[0], S.har_ch, Tf) if nct else (F0.shape[0], Tf, S.har_ch), dtype=torch.float32)
 
 
 @custom_op("stzs::conv_transpose_up", mutates_args=(), device_types="cuda")
-def conv_transpose_up(handle: int, x: torch.Tensor, har: torch.Tensor, stage: int) -> torch.Tensor:
+def conv_transpose_up(handle: int, x: torch.Tensor, har: torch.Tensor, stage: int, nct: bool = False) -> torch.Tensor:
     """a11: generator stage `stage`'s LeakyReLU(0.1) + polyphase ConvTranspose1d (+ ReflectionPad(1,0) on the last
-    stage) + noise conv of the harmonic features har [B, Tf, n_fft + 2] -> fp32 [B, T_up, gen_ch[stage]]."""
+    stage) + noise conv of the harmonic features har [B, Tf, n_fft + 2] -> fp32 [B, T_up, gen_ch[stage]] (nct: x, har
+    and the output as [B, C, T])."""
     eng = _eng(handle, x, har)
     S = eng.spec
     from .engine import Act
+    har = _ntc(har, nct)
     B, Tf, hc = har.shape
     hb = eng.buf("op.har", (B, Tf, (hc + 31) // 32 * 32), eng.dec_dt, zero=True)
     hb[:, :, :hc].copy_(har)
-    xu = eng.upsample(_act_in(eng, "ups.x", x, eng.dec_dt), Act(hb, 0, hc), int(stage))
-    return _out(xu.t[:, :, :S.gen_ch[stage]])
+    xu = eng.upsample(_act_in(eng, "ups.x", x, eng.dec_dt, nct), Act(hb, 0, hc), int(stage))
+    return _out(xu.t[:, :, :S.gen_ch[stage]], nct)
 
 
 @register_fake("stzs::conv_transpose_up")
-def _(handle, x, har, stage):
+def _(handle, x, har, stage, nct=False):
     S = _spec(handle)
-    T_up = x.shape[1] * S.up_rates[stage] + (1 if stage == len(S.up_rates) - 1 else 0)
-    return x.new_empty((x.shape[0], T_up, S.gen_ch[stage]), dtype=torch.float32)
+    T_up = x.shape[2 if nct else 1] * S.up_rates[stage] + (1 if stage == len(S.up_rates) - 1 else 0)
+    shp = (x.shape[0], S.gen_ch[stage], T_up) if nct else (x.shape[0], T_up, S.gen_ch[stage])
+    return x.new_empty(shp, dtype=torch.float32)
 
 
 @custom_op("stzs::mrf_resblock", mutates_args=(), device_types="cuda")
-def mrf_resblock(handle: int, x: torch.Tensor, codes: torch.Tensor, stage: int) -> torch.Tensor:
+def mrf_resblock(handle: int, x: torch.Tensor, codes: torch.Tensor, stage: int, nct: bool = False) -> torch.Tensor:
     """a12: the multi-receptive-field fusion of generator stage `stage` (its rb_kernels AdaIN + Snake + dilated-conv
-    resblocks, averaged), AdaIN style from the pooled acoustic codes: x [B, T, C] -> fp32 [B, T, C]."""
+    resblocks, averaged), AdaIN style from the pooled acoustic codes: x [B, T, C] -> fp32 [B, T, C] (nct: [B, C, T])."""
     eng = _eng(handle, x, codes)
     gbd = eng.dec_style(codes.float().contiguous())
-    y = eng.mrf(_act_in(eng, "mrf.x", x, eng.dec_dt), int(stage), gbd, eng.W.dec_norm)
-    return _out(y.t[:, :, :x.shape[2]])
+    y = eng.mrf(_act_in(eng, "mrf.x", x, eng.dec_dt, nct), int(stage), gbd, eng.W.dec_norm)
+    return _out(y.t[:, :, :x.shape[1 if nct else 2]], nct)
 
 
 @register_fake("stzs::mrf_resblock")
-def _(handle, x, codes, stage):
+def _(handle, x, codes, stage, nct=False):
     return x.new_empty(x.shape, dtype=torch.float32)
 
 
 @custom_op("stzs::conv_post_istft", mutates_args=(), device_types="cuda")
-def conv_post_istft(handle: int, x: torch.Tensor) -> torch.Tensor:
-    """a13: LeakyReLU(0.01) + conv_post + exp / sin spectrum + iSTFT: x [B, Tf, gen_ch[-1]] -> wav fp32 [B, (Tf-1) hop_s]."""
+def conv_post_istft(handle: int, x: torch.Tensor, nct: bool = False) -> torch.Tensor:
+    """a13: LeakyReLU(0.01) + conv_post + exp / sin spectrum + iSTFT: x [B, Tf, gen_ch[-1]] ([B, gen_ch[-1], Tf] with
+    nct) -> wav fp32 [B, (Tf-1) hop_s]."""
     eng = _eng(handle, x)
-    wav = eng.istft(eng.conv_post(_act_in(eng, "post.x", x, eng.dec_dt)))
+    wav = eng.istft(eng.conv_post(_act_in(eng, "post.x", x, eng.dec_dt, nct)))
     return wav.clone()
 
 
 @register_fake("stzs::conv_post_istft")
-def _(handle, x):
-    return x.new_empty((x.shape[0], (x.shape[1] - 1) * _spec(handle).istft_hop), dtype=torch.float32)
+def _(handle, x, nct=False):
+    return x.new_empty((x.shape[0], (x.shape[2 if nct else 1] - 1) * _spec(handle).istft_hop), dtype=torch.float32)
 
 
 @custom_op("stzs::code_quantize", mutates_args=(), device_types="cuda")

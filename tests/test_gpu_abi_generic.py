@@ -73,8 +73,8 @@ def test_generic_sine_gen_and_conv_post_istft(eng, tiny, tiny_params):
     S, P, dev = tiny, tiny_params, eng.device
     g = torch.Generator().manual_seed(62)
     F0 = (100 + 150 * torch.rand(2, 40, generator=g)).to(dev)
-    har_e = eng.sine_gen(F0, [3, 4]).t[:, :, :S.har_ch].clone()
-    Tf = har_e.shape[1]
+    Tf = F0.shape[1] * S.hop // S.istft_hop + 1
+    har_e = eng.sine_gen(F0, [3, 4]).t[:, :Tf, :S.har_ch].clone()  # (buffer rows: a multiple of the noise stride)
     har = torch.zeros(2, Tf, 32, dtype=torch.bfloat16, device=dev)
     merge = torch.cat([P["gen.src_merge.w"].reshape(-1), P["gen.src_merge.b"]]).float().to(dev)
     seeds = torch.tensor([3, 4], dtype=torch.int32, device=dev)
@@ -150,7 +150,10 @@ def test_generic_conv_transpose_up(eng, tiny, tiny_params, stage):
     x = torch.randn(2, T, cin, generator=g).to(torch.bfloat16).to(dev)
     F0 = (100 + 150 * torch.rand(2, T80, generator=g)).to(dev)
     har = eng.sine_gen(F0, [1, 2])
+    ns = eng.noise_super  # the generic op computes the stride-6 noise conv: compare with that engine form
+    eng.noise_super = False
     want = eng.upsample(Act(x), har, stage).t.clone()
+    eng.noise_super = ns
     r, k, Co = S.up_rates[stage], S.up_kernels[stage], S.gen_ch[stage]
     last = stage == len(S.up_rates) - 1
     nk = 1 if last else 2 * int(np.prod(S.up_rates[stage + 1:]))
@@ -162,7 +165,7 @@ def test_generic_conv_transpose_up(eng, tiny, tiny_params, stage):
     y = torch.zeros_like(want)
     ins = [x, har.t, wu, P[f"gen.ups{stage}.b"].float().to(dev), wn, P[f"gen.noise_conv{stage}.b"].float().to(dev)]
     # har descriptor: the engine's buffer (row pitch 32, channels har_ch)
-    hv = har.t[:, :, :S.har_ch]
+    hv = har.t[:, :T80 * S.hop // S.istft_hop + 1, :S.har_ch]  # the Tf frames (buffer rows are rounded up)
     ins[1] = hv
     rc, _ = _call("conv_transpose_up", ins, [y[:, :, :Co]], L.params([r, int(last), nk, nstride, npad, S.har_ch, Co],
                                                                        [0.1]))

@@ -236,6 +236,42 @@ def test_op_conv_post_istft(handle, tiny, tiny_params):
     assert e < 2e-2
 
 
+def test_ops_nct_layout(handle, tiny, tiny_params, dec_inputs):
+    """the per-row operators with nct=True (torch Conv1d [B, C, T] tensors at the boundary): each is
+    the channels-last call with its operands and result transposed, bit for bit (the transpose is folded into the
+    operator's own buffer copies), and the oracle's NCT functions are matched directly."""
+    from oracle import stzs_ref as R
+    h, eng = handle
+    S, P = tiny, tiny_params
+    asr, F0, N, codes = dec_inputs
+    d = eng.device
+    asr_d, F0_d, N_d, c_d = asr.to(d), F0.to(d), N.to(d), codes.to(d)
+    a = torch.ops.stzs.decoder_pre(h, asr_d, F0_d, N_d, c_d)
+    b = torch.ops.stzs.decoder_pre(h, asr_d.transpose(1, 2).contiguous(), F0_d, N_d, c_d, nct=True)
+    assert b.shape == (2, S.dec_out, 2 * asr.shape[1]) and torch.equal(b, a.transpose(1, 2))
+    hs = torch.ops.stzs.sine_gen(h, F0_d, [3, 4])
+    hn = torch.ops.stzs.sine_gen(h, F0_d, [3, 4], nct=True)
+    assert torch.equal(hn, hs.transpose(1, 2))
+    g = torch.Generator().manual_seed(48)
+    for stage in (0, 1):
+        cin = S.dec_out if stage == 0 else S.gen_ch[0]
+        T = F0.shape[1] * (1 if stage == 0 else S.up_rates[0])
+        x = _bf(torch.randn(2, T, cin, generator=g)).to(d)
+        u = torch.ops.stzs.conv_transpose_up(h, x, hs, stage)
+        un = torch.ops.stzs.conv_transpose_up(h, x.transpose(1, 2).contiguous(), hn, stage, nct=True)
+        assert torch.equal(un, u.transpose(1, 2))
+        m = torch.ops.stzs.mrf_resblock(h, u, c_d, stage)
+        mn = torch.ops.stzs.mrf_resblock(h, u.transpose(1, 2).contiguous(), c_d, stage, nct=True)
+        assert torch.equal(mn, m.transpose(1, 2))
+        # the oracle takes NCT directly
+        want = R.upsample_stage(P, S, x.float().cpu().transpose(1, 2), _bf(hn.cpu()), stage)
+        assert rel_err(un.cpu(), want) < 2e-2
+    xp = _bf(torch.randn(2, 481, S.gen_ch[-1], generator=g) * 0.5)
+    w1 = torch.ops.stzs.conv_post_istft(h, xp.to(d))
+    w2 = torch.ops.stzs.conv_post_istft(h, xp.transpose(1, 2).contiguous().to(d), nct=True)
+    assert torch.equal(w1, w2)
+
+
 def test_op_code_quantize(handle, tiny, tiny_params):
     """stzs::code_quantize vs oracle quantize_codes: indices and dequantised codes bit-exact."""
     from oracle import stzs_ref as R

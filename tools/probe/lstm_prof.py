@@ -1,5 +1,7 @@
 """Per-phase cycle counts of the LSTM step (s_memtime, workgroup 0): build lstm.hip with
--DSTZS_LSTM_PROF into a probe library and run one v0-sized recurrence (B=64, H=256, T=80, 2 dirs)."""
+-DSTZS_LSTM_PROF into a probe library (once, in this container: `python tools/probe/lstm_prof.py --build`) and run
+one v0-sized recurrence (env B=64, H=256, T=80, 2 dirs).  B <= 2 takes the tagged-granule exchange (phases: sweep,
+MFMA + gates, cell + publish)."""
 import ctypes as C
 import os
 import subprocess
@@ -12,11 +14,14 @@ from stzs import _lib as L  # noqa: E402
 
 so = os.path.join(ROOT, "tools", "probe", "liblstmprof.so")
 src = os.path.join(ROOT, "styletts-zs_amd", "csrc")
-subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
-                       "-DSTZS_LSTM_PROF", "-I" + os.path.join(ROOT, "include"), "-I" + src,
-                       os.path.join(src, "lstm.hip"), "-o", so])
+if "--build" in sys.argv or not os.path.exists(so):
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
+                           "-DSTZS_LSTM_PROF", "-I" + os.path.join(ROOT, "include"), "-I" + src,
+                           os.path.join(src, "lstm.hip"), "-o", so])
+    if "--build" in sys.argv:
+        sys.exit(0)
 lib = C.CDLL(so)
-B, T, H = 64, int(os.environ.get("T", 80)), 256
+B, T, H = int(os.environ.get("B", 64)), int(os.environ.get("T", 80)), 256
 dev = "cuda:0"
 gx = torch.randn(B, T, 8 * H, device=dev) * 0.5
 whh = (torch.randn(2 * 4 * H * H, device=dev) * 0.05).to(torch.bfloat16)
