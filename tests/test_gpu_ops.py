@@ -406,6 +406,33 @@ def test_mrf_wide_bit_identical(eng, case):
         assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
 
 
+# single-chunk Snake convs (the stage-1 generator shapes): the tall form (STZS_CONV_MRFV_TALL, 256 / 192 rows per
+# workgroup) -- ragged last tiles, dilations 1..5 at every kernel width, residual / accumulate / statistics forms
+TALL_CASES = [
+    (3, 3001, 128, 128, 3, 1, "snake", False, False, True, 1),
+    (2, 1000, 128, 128, 3, 5, "snake", True, True, False, 1),
+    (2, 2500, 128, 128, 7, 3, "snake", True, False, True, 1),
+    (1, 701, 128, 128, 7, 1, "snake", False, True, True, 1),
+    (2, 2400, 128, 128, 11, 5, "snake", True, False, True, 1),
+    (3, 450, 128, 128, 11, 3, "snake", False, False, True, 1),
+    (2, 129, 128, 96, 11, 1, "snake", True, False, True, 1),    # Co < co_pad, one ragged tile
+]
+
+
+@pytest.mark.parametrize("case", TALL_CASES)
+def test_mrf_tall_bit_identical(eng, case):
+    """the tall stage-1 form (each wave 32 output channels x 256 rows, 192 for k11) vs the 128-row register-direct
+    form: the same staged operands in the same K order per output -> outputs and fused statistics bit-identical
+    (tolerance 0); and vs the fp32 reference at the persistent-conv tolerance."""
+    from stzs import _lib as L
+    a, sa, ref = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_TALL)
+    b, sb, _ = _run_mrf(eng, case, "frag32", ref=False)
+    assert torch.equal(a, b)
+    if sa is not None:
+        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
+    assert max_rel(a, ref) < 1.5e-2
+
+
 @pytest.mark.parametrize("case", PIPE_CASES)
 def test_mrf_pipelined_bit_identical(eng, case):
     """the persistent LDS-DMA-pipelined k3 kernel (csrc/mrfp.hip, STZS_CONV_MRF_PIPE) vs the one-tile-per-
