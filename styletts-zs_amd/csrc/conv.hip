@@ -566,8 +566,20 @@ typedef __attribute__((ext_vector_type(2))) long i64x2;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 template <int BTM, int SK>
 STZS_DEV bool splitk_combine(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem);
+// STZS_GEMM_PROF (a probe build only, tools/gemm_phase.py): lane 0 of every workgroup stamps s_memtime at the kernel's
+// start, after the first K-step landed, after the K loop, after the epilogue's stores issued and after they drained,
+// into splitk_ws (unused by the SK = 1 kernels) -- 8 words per workgroup.  Never defined in the library build.
+#ifdef STZS_GEMM_PROF
+#define GPROF(i)                                                                                              \
+    if (SK == 1 && a.splitk_ws && threadIdx.x == 0)                                                            \
+        reinterpret_cast<unsigned long long*>(a.splitk_ws)[(long)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = \
+            __builtin_amdgcn_s_memtime();
+#else
+#define GPROF(i)
+#endif
 template <typename TOut, int BTM, bool F8, int SK = 1>
 __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
+    GPROF(0)
     constexpr int MT = BTM / 32;           // 16-row tiles per wave (2 x 2 waves)
     constexpr int GS = gslot<BTM>();
     constexpr int AP = BTM / 64;           // A pieces (1 KB) per wave per K-step
@@ -652,6 +664,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     fill(1);
     __builtin_amdgcn_s_waitcnt(0x0F70 | PER_FILL);  // K-step 0 landed (K-step 1 may be in flight)
     __builtin_amdgcn_s_barrier();
+    GPROF(1)
     fill(2);
     rd(fa0, fb0, 0);
 #define STZS_GEMM_STEP(FA, FB, NA, NB)                                          \
@@ -683,6 +696,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         mma(fa0, fb0);
     }
 #undef STZS_GEMM_STEP
+    GPROF(2)
     if constexpr (F8) {  // dequantise: row scale (flat row, clamped like the A rows) x column scale
         float sw[4];
 #pragma unroll
@@ -702,6 +716,11 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         if (!splitk_combine<BTM, SK>(a, acc, smem)) return;
     }
     finish<TOut, true, BTM>(a, acc, smem, 0, 0, row0, by);
+#ifdef STZS_GEMM_PROF
+    GPROF(3)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GPROF(4)
+#endif
 }
 
 // In-launch split-K hand-off (MI355X guide: cdna_hip_programming.md, "In-launch split-K reduction", the sc1
@@ -1240,3 +1259,7 @@ extern "C" size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32
     const int64_t tiles = (rows + 63) / 64 * (co_pad / BCO);
     return (size_t)tiles * splitk * (64 / 32 * 4) * NTHR * 16;
 }
+
+#ifdef STZS_GEMM_PROF
+extern "C" int stzs_gemm_prof_conv(const stzs_conv_args* a, void* stream) { return stzs_conv1d_core(a, stream); }
+#endif

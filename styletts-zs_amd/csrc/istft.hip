@@ -11,14 +11,16 @@
 // order with the same frame synthesis code in both modes, so concatenated chunks are BIT-identical
 // to the whole-utterance output (tests/test_gpu_stream.py).
 //
-// Work split: one workgroup per FB frames of the chunk; the FB + halo frame signals overlapping its
-// output span are synthesised once into LDS, then each thread overlap-adds its output samples.
-// HBM-bound: reads n_fft + 2 floats per frame, writes hop_s samples per frame.
+// Work split: one workgroup per 256 - halo frames of the chunk, so the 256 frame signals overlapping its output span
+// (its own + the halo) are synthesised once into LDS by the 256 threads in ONE pass (256 own frames + 3 halo took a
+// second pass for 3 threads, i.e. the whole workgroup twice as long), then each thread overlap-adds its output
+// samples.  Spectrum from the hardware transcendentals (v_exp / v_sin / v_cos, ~1e-6 relative; the libm forms' range
+// reduction was most of the frame synthesis).  HBM-bound: reads n_fft + 2 floats per frame, writes hop_s samples.
 #include "common.hpp"
 
 namespace {
 
-constexpr int FB = 256;
+constexpr int NF = 256;  // frame signals per workgroup (its frames + the halo)
 
 struct IstftJob {
     const float* post;     // row j = frame f0 + j
@@ -37,7 +39,7 @@ __global__ __launch_bounds__(256) void istft_kernel(const IstftJob a) {
     constexpr int nfft = NFFT, nb = NFFT / 2 + 1;
     const int hs = a.hs;
     const int halo = halo_of(nfft, hs);
-    const int NF = FB + halo;
+    const int FB = NF - halo;        // frames of this workgroup
     float* fr = sm;                  // NF * nfft windowed frame signals
     float* twc = fr + NF * nfft;
     float* tws = twc + nfft;
@@ -79,10 +81,10 @@ __global__ __launch_bounds__(256) void istft_kernel(const IstftJob a) {
         float re[nb], im[nb];
 #pragma unroll
         for (int k = 0; k < nb; ++k) {
-            const float mag = expf(row[k]);
-            const float ph = sinf(row[nb + k]);
-            re[k] = mag * cosf(ph);
-            im[k] = mag * sinf(ph);
+            const float mag = __expf(row[k]);
+            const float ph = __sinf(row[nb + k]);
+            re[k] = mag * __cosf(ph);
+            im[k] = mag * __sinf(ph);
         }
 #pragma unroll
         for (int i = 0; i < nfft; ++i) {
@@ -130,7 +132,8 @@ void chunk_span(long f0, long Fc, int fin, int nfft, int hs, long* n0, long* n1,
 
 int launch(const IstftJob& j, int nfft, int B, long m_lo, hipStream_t s) {
     const int halo = (nfft + j.hs - 1) / j.hs - 1;
-    const size_t lds = (size_t)((FB + halo) * nfft + 3 * nfft) * 4;
+    const int FB = NF - halo;
+    const size_t lds = (size_t)(NF * nfft + 3 * nfft) * 4;
     // blocks cover the chunk's frames and, on the final chunk, the samples past its last frame start
     const long span_frames = (j.m_end - m_lo + j.hs - 1) / j.hs;
     long nblk = (span_frames + FB - 1) / FB;

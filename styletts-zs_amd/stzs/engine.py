@@ -106,7 +106,9 @@ class Act:
 
     @property
     def bs(self):
-        return self.t.shape[1] * self.t.shape[2]
+        """batch stride in elements: the tensor's own (a view of the first T rows of a longer buffer -- the harmonic
+        source's -- keeps the buffer's stride; for contiguous buffers this is T * ld)"""
+        return self.t.stride(0)
 
     @property
     def ptr(self):
@@ -1139,8 +1141,9 @@ class StyleTTSZS:
         # row pitch = the noise convs' padded K (32): the 1x1 noise conv then takes the LDS-DMA GEMM path
         dt = self.dec_dt
         # rows rounded up to a multiple of the first stage's noise-conv stride (zero past Tf): the buffer then reads as
-        # whole super-rows (engine.upsample's super-row noise conv)
-        har = Act(self.buf("gen.har", (B, self._har_rows(Tf), _rup(S.har_ch, 32)), dt, zero=True), 0, S.har_ch)
+        # whole super-rows (engine.upsample's super-row noise conv); the Act is the view of its Tf frames
+        hb = self.buf("gen.har", (B, self._har_rows(Tf), _rup(S.har_ch, 32)), dt, zero=True)
+        har = Act(hb[:, :Tf], 0, S.har_ch)
         a = L.SourceArgs()
         a.f0, a.seeds, a.merge_w, a.prefix, a.har = F0.data_ptr(), sd.data_ptr(), W.t(W.src_merge).data_ptr(), \
             pref.data_ptr(), har.ptr
@@ -1181,17 +1184,21 @@ class StyleTTSZS:
         xsrc = self.act(f"gen.xsrc{i}", B, Tn, c, dt)
         sup = W.noise_sup[i] if (not last and i < len(W.noise_sup)) else None
         sf0 = int(np.prod(S.up_rates[i + 1:])) if not last else 1
-        if (sup is not None and self.noise_super and har.dt == L.BF16 and har.t.shape[1] % sf0 == 0 and
-                har.t.shape[1] // sf0 >= Tn + 1 and sf0 * har.ld == sup.Ci):
+        rows_alloc = har.bs // har.ld  # rows of the buffer behind the Tf-frame view (zero past Tf)
+        if (sup is not None and self.noise_super and har.dt == L.BF16 and har.bs % (sf0 * har.ld) == 0 and
+                rows_alloc // sf0 >= Tn + 1 and sf0 * har.ld == sup.Ci and har.t.stride(1) == har.ld):
             # the strided noise conv on SUPER-ROWS (weights.noise_super_weights): the harmonic-source buffer read as
             # [B, rows / s, s * 32] is a k3 stride-1 conv over 192 channels -> the register-direct kernel (mrfv.hip)
             # instead of a stride-6 conv staging 6 rows of 64 B per output row
-            hs = har.t.view(B, har.t.shape[1] // sf0, sf0 * har.ld)
+            hs = har.t.as_strided((B, rows_alloc // sf0, sf0 * har.ld), (har.bs, sf0 * har.ld, 1))
             self.conv(sup, Act(hs), xsrc, pad=1, T_out=Tn, what=f"noise_conv{i}")
         elif not last:
-            self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, stride=sf0, pad=(sf0 + 1) // 2, what=f"noise_conv{i}")
+            # (T_out explicit: the harmonic buffer holds rows past the Tf frames -- zeros, rounded up for the super-row
+            # view -- so har.T would over-count the output rows)
+            self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, stride=sf0, pad=(sf0 + 1) // 2, T_out=Tn,
+                      what=f"noise_conv{i}")
         else:
-            self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, what=f"noise_conv{i}")
+            self.conv(W.noise_conv[i], har.sl(0, S.har_ch), xsrc, T_out=Tn, what=f"noise_conv{i}")
         self.conv(W.ups[i], x, xu, pro_act=L.ACT_LEAKY, pro_slope=0.1, ups_pad=(k - r) // 2, T_final=Tcur * r,
                   refl=1 if last else 0, res=xsrc, what=f"ups{i}")
         return xu
@@ -1307,7 +1314,7 @@ class StyleTTSZS:
             nw = len(ks)
             Bw = nw * B
             enc_w = self.act("dec.enc_in_w", Bw, Wn, S.d_txt + 2, dt)
-            har_w = Act(self.buf("gen.har_w", (Bw, self._har_rows(Tfw), har.ld), dt, zero=True), 0, S.har_ch)
+            har_w = Act(self.buf("gen.har_w", (Bw, self._har_rows(Tfw), har.ld), dt, zero=True)[:, :Tfw], 0, S.har_ch)
             F0w = self.buf("dec.F0w", (Bw, 2 * Wn), torch.float32)
             Nw = self.buf("dec.Nw", (Bw, 2 * Wn), torch.float32)
             cw_ = codes if nw == 1 else self.buf("dec.codes_w", (Bw,) + tuple(codes.shape[1:]), codes.dtype)

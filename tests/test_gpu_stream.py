@@ -179,8 +179,8 @@ def test_longform_30s_stream(gpu_device, v0):
 CHUNK_HALO = 10  # aligned frames of context on each side of a 1-s (40-frame) chunk
 
 
-@pytest.mark.parametrize("spec", ["tiny", "v0"])
-def test_chunked_decoder_vs_chunked_oracle(gpu_device, v0, spec):
+@pytest.mark.parametrize("spec,B", [("tiny", 1), ("tiny", 2), ("v0", 1)])
+def test_chunked_decoder_vs_chunked_oracle(gpu_device, v0, spec, B):
     """the CHUNKED streaming decoder (window-local statistics, global harmonic source) against the oracle's chunked
     restatement (oracle/stzs_ref.py decode_chunked), teacher-forced on the same aligned features / F0 / N / codes:
     bf16 decoder bound of tests/test_gpu_configs.py (waveform 1.05e-1 rel-L2, log-mel L1 7.5e-2); chunk boundaries
@@ -199,7 +199,6 @@ def test_chunked_decoder_vs_chunked_oracle(gpu_device, v0, spec):
         T40, chunk = 1200, 40  # 30 s in 1-s chunks (configs[4])
     eng = StyleTTSZS(S, P, device=gpu_device)
     g = torch.Generator().manual_seed(31)
-    B = 1
     asr = torch.randn(B, T40, S.d_txt, generator=g).to(torch.bfloat16).float()
     F0 = 100 + 150 * torch.rand(B, 2 * T40, generator=g)
     F0[:, :6] = 0.0
@@ -208,7 +207,8 @@ def test_chunked_decoder_vs_chunked_oracle(gpu_device, v0, spec):
     enc_in = eng.act("dec.enc_in", B, T40, S.d_txt + 2)
     enc_in.t[:, :, :S.d_txt] = asr.to(torch.bfloat16).to(gpu_device)
     pro = dict(asr_buf=enc_in, F0=F0.to(gpu_device), N=N.to(gpu_device), T40=T40)
-    parts = [(n0, w.clone()) for n0, w in eng.decode_chunked(pro, codes.to(gpu_device), [9], chunk, CHUNK_HALO)]
+    seeds = [9, 4][:B]
+    parts = [(n0, w.clone()) for n0, w in eng.decode_chunked(pro, codes.to(gpu_device), seeds, chunk, CHUNK_HALO)]
     torch.cuda.synchronize()
     nxt = 0
     for (n0, w), (a, b, _, _) in zip(parts, R.chunk_windows(T40, chunk, CHUNK_HALO)):
@@ -217,13 +217,13 @@ def test_chunked_decoder_vs_chunked_oracle(gpu_device, v0, spec):
     assert nxt == T40 * S.frame40 and len(parts) == len(R.chunk_windows(T40, chunk, CHUNK_HALO))
     wav = torch.cat([w for _, w in parts], 1).cpu()
     # the later windows decoded as ONE batch (default) == decoded one by one: the decoder is batch-invariant
-    one = [w.clone() for _, w in eng.decode_chunked(pro, codes.to(gpu_device), [9], chunk, CHUNK_HALO,
+    one = [w.clone() for _, w in eng.decode_chunked(pro, codes.to(gpu_device), seeds, chunk, CHUNK_HALO,
                                                      batch_windows=False)]
     torch.cuda.synchronize()
     assert torch.equal(torch.cat(one, 1).cpu(), wav)
-    ref, _ = R.decode_chunked(P, S, asr, F0, N, codes, [9], chunk, CHUNK_HALO)
+    ref, _ = R.decode_chunked(P, S, asr, F0, N, codes, seeds, chunk, CHUNK_HALO)
     e = rel_err(wav, ref)
     m = (R.log_mel(wav, S) - R.log_mel(ref, S)).abs().mean().item()
-    print(f"chunked decoder {spec}: {len(parts)} chunks, waveform rel-L2 {e:.3e}, log-mel L1 {m:.3e}")
+    print(f"chunked decoder {spec} B={B}: {len(parts)} chunks, waveform rel-L2 {e:.3e}, log-mel L1 {m:.3e}")
     assert torch.isfinite(wav).all()
     assert e < 1.05e-1 and m < 7.5e-2

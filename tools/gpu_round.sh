@@ -2,7 +2,7 @@
 # full GPU round trip (tag = $1): gpu parity tests, default bench (with CPU baseline), kernel-trace profile
 tag=${1:-x}
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/ -v -s -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t_$tag.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/ -x -v -s -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t_$tag.log 2>&1
 rc=$?; echo TEST $rc; grep -E "passed|failed|FAILED|Error" gpurun_out/t_$tag.log | tail -8
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$tag.log 2>&1 || exit $?
