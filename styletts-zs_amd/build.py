@@ -28,9 +28,10 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=
 # harmonic-source STFT built with them failed 104 of 512 swept two-shard passes, the same code with only its 7 swapped
 # operands pre-swapped by two v_mov_b32 (everything else still packed) 0 of 512 (tools/pk_bisect.py,
 # profiles/r04_*_pk_bisect*.log).  tests/test_isa_audit.py fails the build if any kernel of the
-# library contains the pattern; conv.hip's epilogues / prologues and source.hip's STFT sums are where hipcc made it.
+# library contains the pattern; conv.hip's epilogues / prologues, source.hip's STFT sums and mrfs.hip's staging transform
+# (per-lane channel constants) are where hipcc made it.
 NO_PK = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
-FILE_FLAGS = {"source.hip": NO_PK, "conv.hip": NO_PK}
+FILE_FLAGS = {"source.hip": NO_PK, "conv.hip": NO_PK, "mrfs.hip": NO_PK}
 
 
 def sources():
@@ -61,13 +62,13 @@ def _deps_mtime(src):
 def _compile(src, force, verbose):
     """compile one source unless its object is newer than every dependency AND was built by the same command:
     the exact command line is kept in a stamp file beside the object, so a change of FLAGS / FILE_FLAGS / HIPCC
-    (or of build.py itself) rebuilds it (an object from before a codegen flag existed is never reused)"""
+    rebuilds it (an object from before a codegen flag existed is never reused)"""
     obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
     stamp = obj + ".cmd"
     cmd = [HIPCC] + FLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     key = " ".join(cmd)
-    fresh = (os.path.exists(obj) and os.path.getmtime(obj) >= max(_deps_mtime(src), os.path.getmtime(__file__))
-             and os.path.exists(stamp) and open(stamp).read() == key)
+    fresh = (os.path.exists(obj) and os.path.getmtime(obj) >= _deps_mtime(src) and os.path.exists(stamp) and
+             open(stamp).read() == key)
     if not force and fresh:
         return obj
     if verbose:
@@ -88,12 +89,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, force, verbose), srcs))
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        tmp = LIB + ".tmp"  # linked aside and renamed: a reader (a copy of the tree) never sees a partial library
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
     return LIB
 
 

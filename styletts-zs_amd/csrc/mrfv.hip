@@ -398,6 +398,7 @@ void (*pick(int ks, bool one, bool al, bool wide, bool tall))(stzs_conv_args) {
 }  // namespace
 
 int stzs_mrfp_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrfp.hip (1: not applicable)
+int stzs_mrfs_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrfs.hip (1: not applicable)
 int stzs_ups_conv_launch(const stzs_conv_args& a, hipStream_t s);   // csrc/ups.hip (polyphase ConvTranspose)
 
 // internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32 weights
@@ -418,6 +419,10 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
     if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
+    {  // STZS_CONV_MRFS: the stage-1 convs warp-specialised and persistent (csrc/mrfs.hip)
+        const int r = stzs_mrfs_conv_launch(a, s);
+        if (r != 1) return r;
+    }
     if (!tall) {  // STZS_CONV_MRF_PIPE: the k3 single-chunk residual convs on the persistent LDS-DMA-pipelined form (mrfp.hip)
         const int r = stzs_mrfp_conv_launch(a, s);
         if (r != 1) return r;

@@ -220,6 +220,8 @@ class StyleTTSZS:
         self.noise_super = os.environ.get("STZS_NOISE_SUPER", "1") != "0"
         # the stage-1 MRF convs on the tall register-direct form (csrc/mrfv.hip MR > 8; bit-identical); STZS_MRFV_TALL
         self.mrfv_tall = os.environ.get("STZS_MRFV_TALL", "0") != "0"
+        # the stage-1 MRF convs warp-specialised and persistent (csrc/mrfs.hip; bit-identical); STZS_MRFS
+        self.mrfs = os.environ.get("STZS_MRFS", "0") != "0"
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
@@ -1398,7 +1400,8 @@ class StyleTTSZS:
         t1 = self.act(f"gen.t1_{i}", B, T, c, dt)
         mx, rx, sb = self.stats(x, f"gen.sx{i}")
         nk = len(S.rb_kernels)
-        tall = L.CONV_MRFV_TALL if self.mrfv_tall else 0  # (the kernel takes it for single-chunk convs only)
+        # (the kernels take these flags for the single-chunk stage-1 convs only)
+        tall = (L.CONV_MRFV_TALL if self.mrfv_tall else 0) | (L.CONV_MRFS if self.mrfs else 0)
         for j, res in enumerate(W.rb[i]):
             cur, cm, cr = x, mx, rx
             for m, lw in enumerate(res):

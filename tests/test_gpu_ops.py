@@ -433,6 +433,20 @@ def test_mrf_tall_bit_identical(eng, case):
     assert max_rel(a, ref) < 1.5e-2
 
 
+@pytest.mark.parametrize("case", TALL_CASES + [(64, 3001, 128, 128, 7, 3, "snake", True, True, True, 1)])
+def test_mrf_specialised_bit_identical(eng, case):
+    """the warp-specialised persistent stage-1 form (csrc/mrfs.hip, STZS_CONV_MRFS: producer waves stage tile i + 1
+    while consumer waves run tile i; one workgroup per CU walking a contiguous tile range) vs the register-direct form:
+    same staged operands, same K order, same statistics partials -> bit-identical (tolerance 0), incl. a grid with more
+    tiles than CUs (several tiles per workgroup, the weight ring running on across tiles)."""
+    from stzs import _lib as L
+    a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFS, ref=False)
+    b, sb, _ = _run_mrf(eng, case, "frag32", ref=False)
+    assert torch.equal(a, b)
+    if sa is not None:
+        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
+
+
 @pytest.mark.parametrize("case", PIPE_CASES)
 def test_mrf_pipelined_bit_identical(eng, case):
     """the persistent LDS-DMA-pipelined k3 kernel (csrc/mrfp.hip, STZS_CONV_MRF_PIPE) vs the one-tile-per-
