@@ -31,14 +31,6 @@ struct LdPlain {
 
 // operands stored write-through (sc1) in this launch: every load of them sc1 (bypasses this CU's L1 and the
 // XCD's L2 copy; MI355X guide Guideline 16, the sc1-load form of the hand-off).  base is wave-uniform.
-struct LdSc1 {
-    static STZS_DEV uint4 ld(const bf16_t* base, long off) {
-        const __amdgpu_buffer_rsrc_t r =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), 0, 0x7FFFFFFF, 0x00020000);
-        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off * 2), 0, 16));
-    }
-};
-
 // attention of queries [qb0, qb0 + 64) of row r, head h; lds >= Lds<DH>::BYTES, 16-B aligned
 template <int DH, class LD>
 STZS_DEV void attn_unit(const stzs_attn_args& a, long r, int h, int qb0, unsigned char* lds) {

@@ -1,6 +1,5 @@
 // Classifier-free guidance combine + Euler step of one sampler-state element, shared by
-// stzs_cfg_euler (csrc/misc.hip) and the fused denoiser output projection (csrc/rows.hip, STZS_FUSE_CFG) so the two
-// compute the same expression: d = du + s (dc - du) with CFG, x' = x + dsig (x - d) / s0.
+// stzs_cfg_euler (csrc/misc.hip): d = du + s (dc - du) with CFG, x' = x + dsig (x - d) / s0.
 #pragma once
 #include "common.hpp"
 

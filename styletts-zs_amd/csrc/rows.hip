@@ -19,16 +19,7 @@
 // The summation order of an output element -- sequential MFMA chain per wave, waves 0..3, then slices 0..Z-1 --
 // depends on K and Z only, never on the row count: results are batch-invariant (row blocks of up to 128 rows
 // tile larger M with identical per-element arithmetic).
-//
-// Fused forms (include/stzs_fused.h, stzs_conv_rows_fused): 16-row blocks (MT = 1), the output stored
-// write-through (sc1), and the consumer of the output run by a last arriver inside the same launch -- the row
-// LayerNorm of a 16-row block (FUSE_LN) or the attention of one (utterance, head) (FUSE_ATTN) -- with the same
-// device code as stzs_row_layernorm / stzs_attention, so results are bit-identical to the unfused pair.
 #include "common.hpp"
-#include "attn_body.hpp"
-#include "cfg.hpp"
-#include "rowln.hpp"
-#include "stzs_fused.h"
 
 namespace {
 
@@ -56,41 +47,6 @@ STZS_DEV float epi_act(float x, float slope) {
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((address_space(1))) unsigned int gu32;
 
-constexpr int FUSE_NONE = 0, FUSE_LN = STZS_FUSE_LN, FUSE_ATTN = STZS_FUSE_ATTN, FUSE_CFG = STZS_FUSE_CFG;
-
-struct RowsArgs {
-    stzs_conv_args c;
-    stzs_rows_fuse f;
-};
-
-// the fused forms' output stores: write-through (sc1) so a last arriver on any XCD reads them with sc1 loads
-template <typename T> struct Sc1St;
-template <> struct Sc1St<float> {
-    static STZS_DEV void st(const __amdgpu_buffer_rsrc_t& r, unsigned off_el, float v) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(off_el * 4u), 0, 16);
-    }
-};
-template <> struct Sc1St<bf16_t> {
-    static STZS_DEV void st(const __amdgpu_buffer_rsrc_t& r, unsigned off_el, float v) {
-        __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, (int)(off_el * 2u), 0, 16);
-    }
-};
-
-// one ticket on a hand-off counter (tid 0), broadcast through LDS: true in the arrival that completes `need`
-STZS_DEV bool ticket(unsigned int* c, unsigned need, int* s_flag) {
-    if (threadIdx.x == 0) {
-        gu32* ctr = (gu32*)c;
-        const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == need - 1;
-        if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = last;
-    }
-    __syncthreads();
-    const bool last = *s_flag != 0;
-    __syncthreads();  // every thread has read the flag before it is written again
-    return last;
-}
-
 // A fragment of 16 rows x 32 k from TIn rows (bf16: one 16-B load; fp32: two, scaled by cscale and rounded RNE)
 template <typename TIn> struct AFrag;
 template <> struct AFrag<bf16_t> {
@@ -110,12 +66,9 @@ template <> struct AFrag<float> {
     }
 };
 
-template <typename TIn, typename TOut, int MT, int KPW, int EACT, bool SPLIT, int FUSE>
-__global__ __launch_bounds__(NTHR) void gemm_rows(const RowsArgs ra) {
-    const stzs_conv_args& a = ra.c;
-    constexpr int RED_BYTES = 4 * MT * 64 * 16;
-    constexpr int LDS_BYTES = FUSE == FUSE_ATTN && stzs_attn::Lds<64>::BYTES > RED_BYTES ? stzs_attn::Lds<64>::BYTES : RED_BYTES;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+template <typename TIn, typename TOut, int MT, int KPW, int EACT, bool SPLIT>
+__global__ __launch_bounds__(NTHR) void gemm_rows(const stzs_conv_args a) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[4 * MT * 64 * 16];
     auto red = reinterpret_cast<float4 (*)[MT][64]>(lds);
     __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -261,7 +214,6 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const RowsArgs ra) {
     }
     // ---- fused epilogue ----
     TOut* Y = reinterpret_cast<TOut*>(a.y);
-    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, 0x7FFFFFFF, 0x00020000);
     const float bias = hb ? braw : 0.f;
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
@@ -277,99 +229,7 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const RowsArgs ra) {
             x = hr ? x + res_v[s][i] : x;
             x *= a.alpha;
             x = ha ? x + a.beta * ai_v[s][i] : x;
-            if constexpr (FUSE != FUSE_NONE)
-                Sc1St<TOut>::st(yr, (unsigned)(roff(R, a.ldy, a.bsy) + n), x);
-            else
-                DT<TOut>::st(Y + roff(R, a.ldy, a.bsy) + n, x);
-        }
-    }
-    if constexpr (FUSE != FUSE_NONE) {
-        // hand-off (MI355X guide Guideline 16, sc1 form): every wave drains its write-through stores, the barrier
-        // inside ticket() orders them before the ticket; the completing arriver reads with sc1 loads only
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const stzs_rows_fuse& f = ra.f;
-        if constexpr (FUSE == FUSE_LN) {
-            // the block's 16 rows, complete once every column tile has arrived: one row per wave at a time
-            if (!ticket(f.ctr + blockIdx.y, gridDim.x, &s_last)) return;
-            const int nv = f.ln.C >> 3;
-            const float* X = reinterpret_cast<const float*>(f.ln.x);
-            const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X), 0, 0x7FFFFFFF, 0x00020000);
-            // the wave's 4 rows (r0 + wave + 4 j) loaded at once -- one sc1 round trip instead of four -- from
-            // clamped addresses (rows past the end are loaded, never stored); C <= 512 here (one vector per lane)
-            if (nv <= 64) {
-                f32x4 raw[4][2];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int r = min(r0 + wave + 4 * j, nR - 1);
-                    const int off = (int)(((long)r * f.ln.ldx + min(lane, nv - 1) * 8) * 4);
-                    raw[j][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 16));
-                    raw[j][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 16));
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int r = r0 + wave + 4 * j;
-                    if (r >= nR) break;
-                    float v[1][8];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        v[0][q] = raw[j][0][q];
-                        v[0][4 + q] = raw[j][1][q];
-                    }
-                    stzs_ln::ln_row_finish<bf16_t, 1>(f.ln, r, lane, v);
-                }
-                return;
-            }
-            for (int j = 0; j < 4; ++j) {
-                const int r = r0 + wave + 4 * j;
-                if (r >= nR) break;
-                float v[4][8];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (lane + i * 64 < nv) {
-                        const int off = (int)(((long)r * f.ln.ldx + (lane + i * 64) * 8) * 4);
-                        const f32x4 lo = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 16));
-                        const f32x4 hi = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 16));
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            v[i][q] = lo[q];
-                            v[i][4 + q] = hi[q];
-                        }
-                    }
-                }
-                stzs_ln::ln_row_finish<bf16_t, 4>(f.ln, r, lane, v);
-            }
-        } else if constexpr (FUSE == FUSE_CFG) {
-            // this tile's 16 columns of every state row, complete once every row block has arrived
-            if (!ticket(f.ctr + ct, gridDim.y, &s_last)) return;
-            const int Bc = f.cfg_B, on = f.cfg_on;
-            const long N = (long)T * a.Co;  // state elements per utterance row
-            const float* D = reinterpret_cast<const float*>(a.y);
-            const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(D), 0, 0x7FFFFFFF, 0x00020000);
-            const int ncol = min(16, a.Co - ct * 16);
-            const int per = T * ncol;  // elements of one utterance row in this tile
-            for (int e = tid; e < Bc * per; e += NTHR) {
-                const int b = e / per, q = e - b * per;
-                const int t = q / ncol, c = ct * 16 + (q - t * ncol);
-                const long i = (long)b * N + (long)t * a.Co + c;
-                const float dc = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dr, (int)(i * 4), 0, 16));
-                const float du = on ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dr, (int)((i + Bc * N) * 4), 0, 16)) : 0.f;
-                const float xn = stzs_cfg_euler_elem(f.cfg_x[i], dc, du, on, f.cfg_scale, f.cfg_sigma, f.cfg_dsig);
-                f.cfg_x[i] = xn;
-                if (on) f.cfg_x[i + Bc * N] = xn;
-            }
-        } else {
-            // the (utterance, head) units this block's rows and this tile's head complete
-            const int dm = f.attn.heads * 64;
-            const int h = ((ct * 16) % dm) / 64;
-            const unsigned tph = (unsigned)(a.Co / dm) * 4u;  // 16-column tiles per head
-            const int u0 = r0 / T, u1 = min(a.B - 1, (r0 + 16 * MT - 1) / T);
-            for (int u = u0; u <= u1; ++u) {
-                const unsigned nb = (unsigned)((u * T + T - 1) / (16 * MT) - (u * T) / (16 * MT) + 1);
-                if (!ticket(f.ctr + u * f.attn.heads + h, tph * nb, &s_last)) continue;
-                for (int qb = 0; qb < T; qb += 64) stzs_attn::attn_unit<64, stzs_attn::LdSc1>(f.attn, u, h, qb, lds);
-                __syncthreads();  // LDS free before a next unit
-            }
+            DT<TOut>::st(Y + roff(R, a.ldy, a.bsy) + n, x);
         }
     }
 }
@@ -378,28 +238,11 @@ __global__ __launch_bounds__(NTHR) void gemm_rows(const RowsArgs ra) {
 template <typename TIn, typename TOut, int MT, int KPW, bool SPLIT>
 void* pick_act(int act) {
     switch (act) {
-        case STZS_ACT_GELU: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_GELU, SPLIT, FUSE_NONE>;
-        case STZS_ACT_SILU: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_SILU, SPLIT, FUSE_NONE>;
-        case STZS_ACT_NONE: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_NONE, SPLIT, FUSE_NONE>;
+        case STZS_ACT_GELU: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_GELU, SPLIT>;
+        case STZS_ACT_SILU: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_SILU, SPLIT>;
+        case STZS_ACT_NONE: return (void*)gemm_rows<TIn, TOut, MT, KPW, STZS_ACT_NONE, SPLIT>;
         default: return nullptr;
     }
-}
-
-// the fused forms: 16-row blocks, no epilogue activation
-template <typename TIn, typename TOut, int FUSE>
-void* pick_fused(int kpw, bool split) {
-#define STZS_ROWS_F(n) \
-    case n: return split ? (void*)gemm_rows<TIn, TOut, 1, n, STZS_ACT_NONE, true, FUSE> \
-                         : (void*)gemm_rows<TIn, TOut, 1, n, STZS_ACT_NONE, false, FUSE>;
-    switch (kpw) {
-        STZS_ROWS_F(1)
-        STZS_ROWS_F(2)
-        STZS_ROWS_F(4)
-        STZS_ROWS_F(8)
-        STZS_ROWS_F(16)
-        default: return nullptr;
-    }
-#undef STZS_ROWS_F
 }
 
 template <typename TIn, typename TOut, int MT>
@@ -436,9 +279,8 @@ extern "C" size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgr
     return kgroups > 1 ? (size_t)tiles * kgroups * mt * 64 * 16 : 0;
 }
 
-// validates the linear (and the fused consumer, f != nullptr) and launches; f's counters must hold
-// stzs_rows_fuse_counters() zeroed words
-static int rows_launch(const stzs_conv_args& a, const stzs_rows_fuse* f, hipStream_t s) {
+// validates the linear and launches
+int stzs_rows_gemm_launch(const stzs_conv_args& a, hipStream_t s) {
     const bool lin = a.ks == 1 && a.stride == 1 && a.pad == 0 && a.ups == 0 && a.T_in == a.T_out &&
                      a.pro_mode == STZS_PRO_NONE && a.pro_act == STZS_ACT_NONE && !a.stat_part && !a.x_scale;
     if (!lin || (a.flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 | STZS_CONV_W_F32 | STZS_CONV_W_X3 |
@@ -457,72 +299,16 @@ static int rows_launch(const stzs_conv_args& a, const stzs_rows_fuse* f, hipStre
     if (a.ldx < a.ci_pad && a.in_dtype == STZS_BF16) return STZS_ESHAPE;  // fragments read [0, ci_pad) of each row
     if (a.in_dtype == STZS_F32 && a.ldx < a.ci_pad) return STZS_ESHAPE;
     const long M = (long)a.B * a.T_in;
-    if (f) {
-        if (!f->ctr || a.epi_act != STZS_ACT_NONE) return STZS_EINVAL;
-        const long ybytes = ((long)(a.B - 1) * a.bsy + (long)a.T_in * a.ldy) * (a.out_dtype == STZS_F32 ? 4 : 2);
-        if (ybytes >= 0x7FFFFFFF) return STZS_ESHAPE;  // 32-bit buffer offsets of the write-through stores
-        if (f->mode == STZS_FUSE_LN) {
-            const stzs_rowln_args& l = f->ln;
-            if (a.out_dtype != STZS_F32 || l.x != a.y || l.ldx != a.ldy || (a.B > 1 && a.bsy != (long)a.T_in * a.ldy) ||
-                l.R != M || l.C != a.Co || l.C % 8 || l.C > 2048 || l.in_dtype != STZS_F32 || l.out_dtype != STZS_BF16 ||
-                !l.y || l.gdiv <= 0 || (l.G && (l.gs % 8 || !stzs_aligned(l.G, 32))) ||
-                (l.Bt && (l.bs % 8 || !stzs_aligned(l.Bt, 32))) || l.ldy % 8 || l.ldx % 8)
-                return STZS_ESHAPE;
-        } else if (f->mode == STZS_FUSE_CFG) {
-            const int R = f->cfg_on ? 2 * f->cfg_B : f->cfg_B;
-            if (a.out_dtype != STZS_F32 || !f->cfg_x || f->cfg_B <= 0 || a.B != R || a.ldy != a.Co ||
-                (a.B > 1 && a.bsy != (long)a.T_in * a.Co) || (long)a.B * a.T_in * a.Co >= 0x1FFFFFFF)
-                return STZS_ESHAPE;
-        } else if (f->mode == STZS_FUSE_ATTN) {
-            const stzs_attn_args& t = f->attn;
-            const int dm = t.heads * t.dh;
-            if (a.out_dtype != STZS_BF16 || t.precise != 0 || t.dh != 64 || t.heads <= 0 || t.q != a.y || t.R != a.B ||
-                t.Lq != a.T_in || a.Co % dm || !t.k || !t.v || !t.o || t.Lk <= 0 || t.ldq % 8 || t.ldk % 8 ||
-                t.ldv % 8 || t.bsq % 8 || t.bsk % 8 || t.bsv % 8 || t.ldq != a.ldy || t.bsq != a.bsy)
-                return STZS_ESHAPE;
-        } else {
-            return STZS_EINVAL;
-        }
-    }
-    const int mt = f ? 1 : rows_mt(M);
+    const int mt = rows_mt(M);
     dim3 grid((unsigned)((a.Co + 15) / 16), (unsigned)((M + 16 * mt - 1) / (16 * mt)), (unsigned)Z);
     void* k = nullptr;
     const bool split = Z > 1;
-    if (f && f->mode == STZS_FUSE_LN) {
-        if (a.in_dtype == STZS_BF16) k = pick_fused<bf16_t, float, FUSE_LN>(kpw, split);
-        else if (a.in_dtype == STZS_F32) k = pick_fused<float, float, FUSE_LN>(kpw, split);
-        else return STZS_EDTYPE;
-    } else if (f && f->mode == STZS_FUSE_CFG) {
-        if (a.in_dtype != STZS_BF16) return STZS_EDTYPE;
-        k = pick_fused<bf16_t, float, FUSE_CFG>(kpw, split);
-    } else if (f) {
-        if (a.in_dtype != STZS_BF16) return STZS_EDTYPE;
-        k = pick_fused<bf16_t, bf16_t, FUSE_ATTN>(kpw, split);
-    } else if (a.in_dtype == STZS_BF16 && a.out_dtype == STZS_BF16) k = pick<bf16_t, bf16_t>(mt, kpw, split, a.epi_act);
+    if (a.in_dtype == STZS_BF16 && a.out_dtype == STZS_BF16) k = pick<bf16_t, bf16_t>(mt, kpw, split, a.epi_act);
     else if (a.in_dtype == STZS_BF16 && a.out_dtype == STZS_F32) k = pick<bf16_t, float>(mt, kpw, split, a.epi_act);
     else if (a.in_dtype == STZS_F32 && a.out_dtype == STZS_F32) k = pick<float, float>(mt, kpw, split, a.epi_act);
     else return STZS_EDTYPE;
     if (!k) return STZS_EINVAL;  // an epilogue activation this form does not instantiate
-    RowsArgs ra;
-    ra.c = a;
-    if (f) ra.f = *f;
-    else memset(&ra.f, 0, sizeof ra.f);
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(RowsArgs)>(k), grid, dim3(NTHR), 0, s, ra);
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(stzs_conv_args)>(k), grid, dim3(NTHR), 0, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
-}
-
-int stzs_rows_gemm_launch(const stzs_conv_args& a, hipStream_t s) { return rows_launch(a, nullptr, s); }
-
-extern "C" size_t stzs_rows_fuse_counters(const stzs_conv_args* a, const stzs_rows_fuse* f) {
-    if (!a || !f || a->B <= 0 || a->T_in <= 0) return 0;
-    if (f->mode == STZS_FUSE_LN) return (size_t)(((long)a->B * a->T_in + 15) / 16);
-    if (f->mode == STZS_FUSE_ATTN) return f->attn.heads > 0 ? (size_t)a->B * f->attn.heads : 0;
-    if (f->mode == STZS_FUSE_CFG) return a->Co > 0 ? (size_t)((a->Co + 15) / 16) : 0;
-    return 0;
-}
-
-extern "C" int stzs_conv_rows_fused(const stzs_conv_args* a, const stzs_rows_fuse* f, void* stream) {
-    if (!a || !f || !a->x || !a->w || !a->y) return STZS_EINVAL;
-    return rows_launch(*a, f, reinterpret_cast<hipStream_t>(stream));
 }

@@ -72,16 +72,6 @@ class AttnArgs(C.Structure):
                [(n, i32) for n in ("R", "Lq", "Lk", "heads", "dh", "precise")]
 
 
-class RowsFuse(C.Structure):
-    """stzs_rows_fuse (include/stzs_fused.h): the consumer fused into a small-M linear's launch"""
-    _fields_ = [("mode", i32), ("pad0", i32), ("ctr", vp), ("ln", RowLNArgs), ("attn", AttnArgs), ("cfg_x", vp),
-                ("cfg_B", i32), ("cfg_on", i32), ("cfg_scale", f32), ("cfg_sigma", f32), ("cfg_dsig", f32),
-                ("cfg_pad", f32)]
-
-
-FUSE_LN, FUSE_ATTN, FUSE_CFG = 1, 2, 3  # include/stzs_fused.h
-
-
 class LstmArgs(C.Structure):
     _fields_ = [("gx", vp), ("whhT", vp), ("y", vp), ("xchg", vp), ("sync", vp),
                 ("ldg", i64), ("bsg", i64), ("ldy", i64), ("bsy", i64),
@@ -224,8 +214,6 @@ EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_co
            "stzs_dn_cond", "stzs_dn_cond_steps", "stzs_adaln_expand", "stzs_cfg_euler",
            "stzs_state_init", "stzs_mean_rows", "stzs_copy2d", "stzs_embed", "stzs_embed_f32", "stzs_dn_cond_steps_f32", "stzs_pack_conv_size", "stzs_pack_conv",
            "stzs_pack_lstm", "stzs_pack_lstm_x3"] + [f"stzs_{o}{sfx}" for o in GENERIC_OPS for sfx in ("", "_workspace")]
-# include/stzs_fused.h
-EXPORTS_FUSED = ["stzs_rows_fuse_counters", "stzs_conv_rows_fused"]
 
 _lib = None
 
@@ -251,8 +239,6 @@ def load():
         "stzs_conv1d": ([P(ConvArgs), vp], i32),
         "stzs_conv_splitk_workspace": ([i64, i32, i32], C.c_size_t),
         "stzs_conv_rows_workspace": ([i64, i32, i32], C.c_size_t),
-        "stzs_rows_fuse_counters": ([P(ConvArgs), P(RowsFuse)], C.c_size_t),
-        "stzs_conv_rows_fused": ([P(ConvArgs), P(RowsFuse), vp], i32),
         "stzs_chan_stats_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
         "stzs_chan_stats_final": ([P(StatsArgs), i32, vp], i32),

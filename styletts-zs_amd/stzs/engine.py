@@ -78,7 +78,6 @@ def _rup(x, m):
     return (x + m - 1) // m * m
 
 
-_FUSED = object()  # conv(): the CFG + Euler step ran inside the linear's launch
 
 
 @dataclass
@@ -151,7 +150,7 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
                  packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None, dn_rows=None,
-                 fuse_rows=False, te_splitk=None):
+                 te_splitk=None):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
@@ -199,15 +198,6 @@ class StyleTTSZS:
         self.dn_rows = _table_env("STZS_DN_ROWS", DN_ROWS) if dn_rows is None else dict(dn_rows)
         # split-K slices of the text-encoder convs (LATENCY_TE_SPLITK); 0 = off
         self.te_splitk = int(os.environ.get("STZS_TE_SPLITK", TE_SPLITK)) if te_splitk is None else int(te_splitk)
-        # the consumers of the small-M denoiser linears fused into their launches (include/stzs_fused.h: the
-        # LayerNorm after the residual linears, the attention after the q / qkv linears, the CFG + Euler step after the
-        # output projection; bit-identical, 32 launches fewer per NFE).  OFF by default: measured SLOWER at batch 1
-        # (configs[1] p50 8.56 -> 10.1 ms, each in-launch hand-off ~5 us dearer than the launch it removes,
-        # profiles/r03_t_fused_latency_ab.log); STZS_FUSE_ROWS=0 / 1 overrides the constructor
-        fz = os.environ.get("STZS_FUSE_ROWS")
-        self.fuse_rows = bool(fuse_rows) if fz is None else fz != "0"
-        # which consumers fuse (STZS_FUSE_MODES, e.g. "ln,attn,cfg")
-        self.fuse_modes = set(os.environ.get("STZS_FUSE_MODES", "ln,attn,cfg").split(","))
         # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
         # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
@@ -312,13 +302,12 @@ class StyleTTSZS:
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
              T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, splitk=0, rows=0, attn=None,
-             cfg=None, what="conv"):
+             what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
         output fused into the conv epilogue (per-tile partials) + one small finalize launch.
         post_ln (stzs_rowln_args) / attn ((q, k, v, o) Acts): the LayerNorm / attention that consumes y, launched
-        behind the linear, or folded into its launch on the fused small-M form (fuse_rows, include/stzs_fused.h).
-        cfg = (B, cfg_on, scale, sigma, dsig): the sampler's CFG + Euler step on y = D of the state acc_in, folded
-        in the same way (returns _FUSED then: the caller skips its stzs_cfg_euler launch); ignored otherwise."""
+        behind the linear.  (r03 also ran them, and the sampler's CFG + Euler step, inside the small-M linear's launch
+        by its last-arriving workgroups: bit-identical but slower at batch 1, removed in r04 -- DESIGN.md §5.)"""
         W = self.W
         a = L.ConvArgs()
         a.x, a.w, a.y = x.ptr, self._t(cw.w).data_ptr(), y.ptr
@@ -408,23 +397,6 @@ class StyleTTSZS:
             a.splitk = splitk
             a.splitk_ws = self._scratch("csk_ws", tiles * splitk * 16384).data_ptr()
             a.splitk_ctr = self._counters("csk_ctr", tiles).data_ptr()
-        fz = None
-        fm = self.fuse_modes
-        if (a.flags & L.CONV_ROWS) and self.fuse_rows and ((post_ln is not None and "ln" in fm) or
-                                                          (attn is not None and "attn" in fm) or
-                                                          (cfg is not None and post_ln is None and attn is None and
-                                                           "cfg" in fm)):
-            fz = L.RowsFuse()
-            if post_ln is not None:
-                fz.mode, fz.ln = L.FUSE_LN, post_ln
-            elif attn is not None:
-                fz.mode, fz.attn = L.FUSE_ATTN, self._attn_args(*attn)
-            else:
-                fz.mode, fz.cfg_x = L.FUSE_CFG, acc_in.ptr
-                fz.cfg_B, fz.cfg_on, fz.cfg_scale, fz.cfg_sigma, fz.cfg_dsig = cfg
-            n = self.lib.stzs_rows_fuse_counters(C.byref(a), C.byref(fz))
-            assert n > 0, what
-            fz.ctr = self._counters("fuse_ctr", n).data_ptr()
         st = None
         if stats_key is not None:
             Cc = _rup(cw.Co, 8)
@@ -434,8 +406,7 @@ class StyleTTSZS:
             st = (slab, Cc, self.buf(stats_key + ".m", (y.B, Cc), torch.float32),
                   self.buf(stats_key + ".r", (y.B, Cc), torch.float32))
         tm = self.timer
-        launch = (lambda: self.lib.stzs_conv1d(C.byref(a), self.stream())) if fz is None else \
-            (lambda: self.lib.stzs_conv_rows_fused(C.byref(a), C.byref(fz), self.stream()))
+        launch = lambda: self.lib.stzs_conv1d(C.byref(a), self.stream())
         if tm is not None and (tm["all"] or what in tm["tags"]):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -453,17 +424,12 @@ class StyleTTSZS:
             byt = x.B * x.T * x.C * x.t.element_size() + y.B * a.T_out * (cw.ups or 1) * cw.Co * y.t.element_size() + \
                 opnd(res) + opnd(acc_in) + wbytes
             tm["rec"].append((what, e0, e1, flops, byt, (cw.ks, dil, a.T_out, cw.Co), self.stage))
-        elif fz is None:
-            self._call(self.lib.stzs_conv1d, a, what)
         else:
-            self.launches += 1
-            L.check(launch(), what + ".fused")
-        if post_ln is not None and fz is None:  # the LayerNorm that consumes this linear's output (stzs_rowln_args)
+            self._call(self.lib.stzs_conv1d, a, what)
+        if post_ln is not None:  # the LayerNorm that consumes this linear's output (stzs_rowln_args)
             self._call(self.lib.stzs_row_layernorm, post_ln, what + ".ln", cost=_ln_cost(post_ln))
-        if attn is not None and fz is None:  # the attention whose q (k, v) this linear produced
+        if attn is not None:  # the attention whose q (k, v) this linear produced
             self.attention(*attn)
-        if fz is not None and cfg is not None and post_ln is None and attn is None:
-            return _FUSED
         if st is None:
             return y
         slab, Cc, mean, rstd = st
@@ -748,9 +714,7 @@ class StyleTTSZS:
                 "state_init")
         D = self.act("dn.D", R, S.L_s, S.code_dim, torch.float32)
         for i in range(steps):
-            eu = (B, int(cfg), float(cfg_scale), float(sig[i]), float(sig[i + 1] - sig[i]))
-            if self.denoiser_step(st, i, Act(x), D, euler=eu):
-                continue  # the CFG + Euler update ran inside the output projection's launch
+            self.denoiser_step(st, i, Act(x), D)
             self.launches += 1
             L.check(self.lib.stzs_cfg_euler(x.data_ptr(), D.t.data_ptr(), B, N, int(cfg), float(cfg_scale),
                                             float(sig[i]), float(sig[i + 1] - sig[i]), self.stream()), "cfg_euler")
@@ -832,11 +796,9 @@ class StyleTTSZS:
                                            self.stream()), "adaln_expand.f")
         return dict(R=R, sig=list(sigmas), kv=kv, modx=modx, fmodx=fmodx)
 
-    def denoiser_step(self, st: dict, i: int, xa: Act, D: Act, euler=None) -> bool:
+    def denoiser_step(self, st: dict, i: int, xa: Act, D: Act):
         """one NFE: D = c_skip x + c_out F(c_in x, sigma_i) for the R rows of xa, with the conditioning prepared
-        by denoiser_prepare (6 layers: adaLN-modulated self-attention, cross-attention, GELU FFN).
-        euler = (B, cfg, scale, sigma, dsig): the sampler's CFG + Euler update of xa that follows; True when it
-        ran inside the output projection's launch (fuse_rows), False when the caller still has to launch it."""
+        by denoiser_prepare (6 layers: adaLN-modulated self-attention, cross-attention, GELU FFN)."""
         S, W = self.spec, self.W
         R, kv, modx, fmodx = st["R"], st["kv"], st["modx"], st["fmodx"]
         Ls, d = S.L_s, S.dn_d
@@ -900,12 +862,11 @@ class StyleTTSZS:
                 self.quant(ff, ff8, s_ff)
             self.conv(lw["ff2" + sfx], xf, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=sf,
                       post_ln=lns[3 * l + 3], splitk=sk.get("ff2", 0), rows=rk.get("ff2", 0), what="ff2")
-        return self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], rows=rk.get("out", 0),
-                         cfg=euler, what="dn.out") is _FUSED
+        self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], rows=rk.get("out", 0), what="dn.out")
 
     def _ln_args(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=0.0, y_scale=None):
-        """stzs_rowln_args of a modulated LayerNorm x -> y (launched by stzs_row_layernorm, or fused into a
-        GEMM epilogue as stzs_conv_args.post_ln)."""
+        """stzs_rowln_args of a modulated LayerNorm x -> y (launched by stzs_row_layernorm behind the linear that
+        produces x: conv(post_ln=...))."""
         a = L.RowLNArgs()
         a.x, a.y, a.G, a.Bt = x.ptr, y.ptr, G, Bt
         a.ldx, a.ldy, a.gs, a.bs = x.ld, y.ld, gs, bs

@@ -12,7 +12,7 @@ import pytest
 from conftest import ROOT
 
 
-HEADERS = ("stzs.h", "stzs_fused.h")
+HEADERS = ("stzs.h",)
 
 
 def _header(name="stzs.h"):
@@ -24,9 +24,6 @@ def test_library_exports_every_declared_symbol():
     assert sorted(f for f in os.listdir(os.path.join(ROOT, "include")) if f.endswith(".h")) == sorted(HEADERS)
     decl = set(re.findall(r"\b(stzs_[a-z0-9_]+)\s*\(", _header()))
     assert decl == set(_lib.EXPORTS), decl ^ set(_lib.EXPORTS)
-    fused = set(re.findall(r"\b(stzs_[a-z0-9_]+)\s*\(", _header("stzs_fused.h")))
-    assert fused == set(_lib.EXPORTS_FUSED), fused ^ set(_lib.EXPORTS_FUSED)
-    decl |= fused
     L = _lib.load()
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r"\b(stzs_[a-z0-9_]+)\b", nm))
@@ -65,14 +62,14 @@ STRUCTS = {
     "stzs_dwup_args": "DwupArgs", "stzs_f0n_args": "F0nArgs", "stzs_source_args": "SourceArgs",
     "stzs_istft_args": "IstftArgs", "stzs_istft_stream_args": "IstftStreamArgs", "stzs_quant_args": "QuantArgs", "stzs_frames_args": "FramesArgs",
     "stzs_logmel_args": "LogMelArgs", "stzs_pool_args": "PoolArgs", "stzs_copy_args": "CopyArgs",
-    "stzs_vq_args": "VqArgs", "stzs_tensor_t": "Tensor", "stzs_params_t": "Params", "stzs_rows_fuse": "RowsFuse",
+    "stzs_vq_args": "VqArgs", "stzs_tensor_t": "Tensor", "stzs_params_t": "Params",
 }
 
 
 def test_ctypes_structs_match_c_layout():
     """compile a probe with gcc against include/stzs.h and compare sizeof + every field offset."""
     from stzs import _lib
-    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "stzs.h"', '#include "stzs_fused.h"', "int main(void){"]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "stzs.h"', "int main(void){"]
     for cname, pyname in STRUCTS.items():
         py = getattr(_lib, pyname)
         lines.append(f'printf("{pyname} size %zu\\n", sizeof({cname}));')

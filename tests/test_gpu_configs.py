@@ -289,26 +289,3 @@ def test_latency_engine_batch_invariant(v0):
         o1 = e.synth(tok[i:i + 1], ref[i:i + 1], noise=eps[i:i + 1], durations=dur[i:i + 1], seeds=[seeds[i]], **kw)
         for k in ("codes", "F0", "wav"):
             assert torch.equal(o1[k].cpu(), keep[k][i:i + 1]), (i, k)
-
-
-def test_latency_engine_fused_linears_bit_identical(v0):
-    """the latency engine with its fused small-M linears switched on (fuse_rows; off by default: slower) (include/stzs_fused.h: the LayerNorm after dn.in / sa_o / ca_o /
-    ff2, the self / cross attention after qkv / ca_q and the CFG + Euler step after dn.out inside the linear's launch) vs the same engine launching them
-    separately: codes, F0 and waveform bit-identical at batch 1 and 2, and 32 launches fewer per NFE."""
-    from stzs.engine import latency_engine
-    S, P, eng = v0
-    e = latency_engine(S, eng.W, eng.device)
-    kw = dict(steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG)
-    for nb in (1, 2):
-        tok, ref, eps, dur, seeds = bench.rank_inputs(S, nb, 11)
-        outs, nl = [], []
-        for on in (True, False):
-            e.fuse_rows = on
-            n0 = e.launches
-            o = e.synth(tok, ref, noise=eps, durations=dur, seeds=seeds, **kw)
-            nl.append(e.launches - n0)
-            outs.append({k: o[k].detach().clone().cpu() for k in ("codes", "F0", "wav")})
-        e.fuse_rows = False
-        for k in ("codes", "F0", "wav"):
-            assert torch.equal(outs[0][k], outs[1][k]), (nb, k)
-        assert nl[1] - nl[0] == 32 * bench.STEPS_LATENCY, nl

@@ -1,6 +1,6 @@
 """Per-phase cycle counts of the LSTM step (s_memtime, workgroup 0): build lstm.hip with
 -DSTZS_LSTM_PROF into a probe library (once, in this container: `python tools/probe/lstm_prof.py --build`) and run
-one v0-sized recurrence (env B=64, H=256, T=80, 2 dirs).  B <= 2 takes the tagged-granule exchange (phases: sweep,
+one v0-sized recurrence (env B=64, H=256, T=80, 2 dirs; LSTM_PROF_SO = the probe library's file name).  B <= 2 takes the tagged-granule exchange (phases: sweep,
 MFMA + gates, cell + publish)."""
 import ctypes as C
 import os
@@ -12,7 +12,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts-zs_amd")]
 import torch  # noqa: E402
 from stzs import _lib as L  # noqa: E402
 
-so = os.path.join(ROOT, "tools", "probe", "liblstmprof.so")
+so = os.path.join(ROOT, "tools", "probe", os.environ.get("LSTM_PROF_SO", "liblstmprof.so"))  # A/B: another build
 src = os.path.join(ROOT, "styletts-zs_amd", "csrc")
 if "--build" in sys.argv or not os.path.exists(so):
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
@@ -43,3 +43,14 @@ for it in range(3):
     tot = sum(ph)
     print(f"rc={rc} {e0.elapsed_time(e1)*1e3:.0f} us, per step {e0.elapsed_time(e1)*1e3/T:.2f} us; cycles/step by phase "
           f"(poll, load+sync, mfma+gates, cell+store, drain+signal): {[round(v / T) for v in ph]} total {tot / T:.0f}")
+ref = os.environ.get("LSTM_REF_SO")  # compare y with another build on the same inputs
+if ref:
+    lib2 = C.CDLL(os.path.join(ROOT, "tools", "probe", ref))
+    y0 = y.clone()
+    y.zero_()
+    sync.zero_()
+    xchg.zero_()
+    rc = lib2.stzs_lstm(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    d = (y.float() - y0.float()).abs().max().item()
+    print(f"vs {ref}: rc={rc} max |dy| {d:.3e} bit-identical {torch.equal(y, y0)}")
