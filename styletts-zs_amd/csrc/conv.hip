@@ -353,9 +353,11 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     // chunks [cc_lo, cc_hi) -- K-steps [k_lo, k_hi) of the chunk-major weight stream -- and hands its fp32 partial
     // to the tile's last arriver (splitk_combine_rt), which runs the fused epilogue.  For the small grids of the
     // batch-1 front end (text-encoder k5 convs: 4 workgroups x 80 K-steps at batch 1).
+    // Slice z takes chunks [z n / S, (z+1) n / S): equal slices when S divides n, otherwise sizes differing by one
+    // (the decoder / predictor AdaIN convs of the batch-1 engine: 9 chunks in 3 or 4 slices)
     const int SKr = a.splitk > 1 ? a.splitk : 1;
-    const int cc_lo = SKr > 1 ? (int)blockIdx.z * (nchunk / SKr) : 0;
-    const int cc_hi = SKr > 1 ? cc_lo + nchunk / SKr : nchunk;
+    const int cc_lo = SKr > 1 ? (int)blockIdx.z * nchunk / SKr : 0;
+    const int cc_hi = SKr > 1 ? ((int)blockIdx.z + 1) * nchunk / SKr : nchunk;
     const int k_lo = cc_lo * ks * kpc, k_hi = cc_hi * ks * kpc;
 
     auto fill = [&](int k) {
@@ -1129,8 +1131,8 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
         STZS_LAUNCH_CHECK();
         return STZS_OK;
     }
-    if (a.splitk > 1) {  // conv_mfma: split over input-channel chunks (the chunk count must divide)
-        if (F8 || (a.splitk != 2 && a.splitk != 4) || (a.ci_pad / a.cic) % a.splitk || !a.splitk_ws || !a.splitk_ctr ||
+    if (a.splitk > 1) {  // conv_mfma: split over input-channel chunks (2..8 slices, at least one chunk each)
+        if (F8 || a.splitk > 8 || a.splitk > a.ci_pad / a.cic || !a.splitk_ws || !a.splitk_ctr ||
             !stzs_aligned(a.splitk_ws, 16) || !stzs_aligned(a.splitk_ctr, 4))
             return STZS_EINVAL;
         grid.z = (unsigned)a.splitk;

@@ -51,6 +51,10 @@ LATENCY_DN_ROWS = dict(inp=1, qkv=1, o=1, q=1, co=1, ff1=1, ff2=4, out=1)
 # latency engine's value.  STZS_TE_SPLITK overrides an engine built without te_splitk.
 TE_SPLITK = 0
 LATENCY_TE_SPLITK = 4
+# split-K slices of the decoder / predictor AdaIN-block convs (their generic-layout copies, BlkW.conv1s / conv2s) in
+# the batch-1 latency engine: at 200-400 frames a decoder conv is 16 tiles x 108 K-steps on 16 CUs; 0 = off
+BLK_SPLITK = 0
+LATENCY_BLK_SPLITK = 4
 
 
 _ES = {L.F32: 4, L.BF16: 2, L.F8: 1}
@@ -150,7 +154,7 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
                  packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None, dn_rows=None,
-                 te_splitk=None):
+                 te_splitk=None, blk_splitk=None):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
@@ -198,6 +202,8 @@ class StyleTTSZS:
         self.dn_rows = _table_env("STZS_DN_ROWS", DN_ROWS) if dn_rows is None else dict(dn_rows)
         # split-K slices of the text-encoder convs (LATENCY_TE_SPLITK); 0 = off
         self.te_splitk = int(os.environ.get("STZS_TE_SPLITK", TE_SPLITK)) if te_splitk is None else int(te_splitk)
+        # split-K slices of the bf16 AdaIN-block convs (LATENCY_BLK_SPLITK); 0 = the register-direct form
+        self.blk_splitk = int(os.environ.get("STZS_BLK_SPLITK", BLK_SPLITK)) if blk_splitk is None else int(blk_splitk)
         # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
         # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
@@ -378,10 +384,8 @@ class StyleTTSZS:
         if a.flags & 8:  # LDS-DMA GEMM: the slices split the K-steps (a function of K only: batch invariance holds)
             while splitk > 1 and (cw.ci_pad // 32) % splitk:
                 splitk //= 2
-        elif splitk > 1:  # conv_mfma: the slices split the input-channel chunks, 2 or 4 of them
-            splitk = min(splitk, 4)
-            while splitk > 1 and (cw.ci_pad // cw.cic) % splitk:
-                splitk //= 2
+        elif splitk > 1:  # conv_mfma: the slices split the input-channel chunks (2..8, at most one slice per chunk)
+            splitk = min(splitk, 8, cw.ci_pad // cw.cic)
         if splitk > 1 and (a.flags & 8) and not cw.f8 and cw.wx3 is None and cw.w32 is None:
             # in-launch split-K (stzs_conv_args.splitk): per-branch fp32 slabs + self-resetting tile counters
             nb = self.lib.stzs_conv_splitk_workspace(x.B * x.T, cw.co_pad, splitk)
@@ -389,8 +393,7 @@ class StyleTTSZS:
             a.splitk, a.splitk_ws = splitk, self._scratch("sk_ws", nb // 4).data_ptr()
             a.splitk_ctr = self._counters("sk_ctr", nb // (splitk * 32768)).data_ptr()
         elif (splitk > 1 and not (a.flags & (8 | L.CONV_ROWS | L.CONV_W_X3 | L.CONV_W_F32 | L.CONV_W_FRAG32 |
-                                             L.CONV_W_LANE16 | L.CONV_W_NARROW32)) and not cw.f8 and
-              (cw.ci_pad // cw.cic) % splitk == 0):
+                                             L.CONV_W_LANE16 | L.CONV_W_NARROW32)) and not cw.f8):
             # conv_mfma split over input-channel chunks: one 64-KB fp32 slab per (128-row tile, slice) + a ticket
             # per tile (grid.x is at most B x ceil(T_out / 128))
             tiles = x.B * ((a.T_out + 127) // 128) * (cw.co_pad // 128)
@@ -1004,10 +1007,14 @@ class StyleTTSZS:
     def blk(self, bw, x: Act, out: Act, ng, gb: torch.Tensor, key, dt=torch.bfloat16):
         """AdainResBlk1d: out = (conv2(act(AdaIN(conv1(up(act(AdaIN(x))))))) + sc(x)) / sqrt 2."""
         B, T = x.B, x.T
-        off1, c1 = ng.offsets[bw.name + ".norm1"]
-        off2, c2 = ng.offsets[bw.name + ".norm2"]
+        off1, n1 = ng.offsets[bw.name + ".norm1"]
+        off2, n2 = ng.offsets[bw.name + ".norm2"]
         gbase, gbs = gb.data_ptr(), ng.total
         m1, r1, sb1 = self.stats(x, key + ".s1")
+        # batch-1 engine: the generic-layout copies split-K (blk_splitk), else the register-direct convs
+        sk = self.blk_splitk if dt == torch.bfloat16 else 0
+        c1 = bw.conv1s if (sk and bw.conv1s is not None) else bw.conv1
+        c2 = bw.conv2s if (sk and bw.conv2s is not None) else bw.conv2
         To = 2 * T if bw.up else T
         r = self.act(key + ".r", B, To, bw.dout, dt)
         if bw.up:
@@ -1015,13 +1022,13 @@ class StyleTTSZS:
             a = L.DwupArgs()
             a.x, a.y, a.mean, a.rstd, a.gb = x.ptr, u.ptr, m1.data_ptr(), r1.data_ptr(), gbase + off1 * 4
             a.w, a.wb = self.W.t(bw.pool_w).data_ptr(), self.W.t(bw.pool_b).data_ptr()
-            a.ldx, a.bsx, a.ldy, a.bsy, a.stat_bs, a.gb_bs, a.gb_beta_off = x.ld, x.bs, u.ld, u.bs, sb1, gbs, c1
+            a.ldx, a.bsx, a.ldy, a.bsy, a.stat_bs, a.gb_bs, a.gb_beta_off = x.ld, x.bs, u.ld, u.bs, sb1, gbs, n1
             a.B, a.T, a.C, a.slope, a.dtype = B, T, bw.din, 0.2, x.dt
             self._call(self.lib.stzs_adain_dwup, a, key + ".dwup")
-            _, (m2, r2, sb2) = self.conv(bw.conv1, u, r, pad=1, stats_key=key + ".s2", what=key + ".conv1")
+            _, (m2, r2, sb2) = self.conv(c1, u, r, pad=1, stats_key=key + ".s2", splitk=sk, what=key + ".conv1")
         else:
-            _, (m2, r2, sb2) = self.conv(bw.conv1, x, r, pad=1, pro=(m1, r1, sb1, gbase + off1 * 4, gbs, c1),
-                                         pro_act=L.ACT_LEAKY, pro_slope=0.2, stats_key=key + ".s2",
+            _, (m2, r2, sb2) = self.conv(c1, x, r, pad=1, pro=(m1, r1, sb1, gbase + off1 * 4, gbs, n1),
+                                         pro_act=L.ACT_LEAKY, pro_slope=0.2, stats_key=key + ".s2", splitk=sk,
                                          what=key + ".conv1")
         if bw.sc is not None:
             scb = self.act(key + ".sc", B, T, bw.dout, dt)
@@ -1029,8 +1036,9 @@ class StyleTTSZS:
             res = scb
         else:
             res = x
-        self.conv(bw.conv2, r, out, pad=1, pro=(m2, r2, sb2, gbase + off2 * 4, gbs, c2), pro_act=L.ACT_LEAKY,
-                  pro_slope=0.2, res=res, res_tdiv=2 if bw.up else 1, alpha=1.0 / math.sqrt(2.0), what=key + ".conv2")
+        self.conv(c2, r, out, pad=1, pro=(m2, r2, sb2, gbase + off2 * 4, gbs, n2), pro_act=L.ACT_LEAKY,
+                  pro_slope=0.2, res=res, res_tdiv=2 if bw.up else 1, alpha=1.0 / math.sqrt(2.0), splitk=sk,
+                  what=key + ".conv2")
         return out
 
     # ------------------------------------------------------------------ (c) decoder
@@ -1494,7 +1502,7 @@ def latency_engine(spec: Spec, packed: PackedModel, device="cuda:0") -> "StyleTT
     the oracle): the same packed weights, the denoiser layer linears on the whole-chip small-M form
     (LATENCY_DN_ROWS, csrc/rows.hip) and split-K ffn2 wherever the rows form does not apply (LATENCY_DN_SPLITK)."""
     return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS,
-                      te_splitk=LATENCY_TE_SPLITK)
+                      te_splitk=LATENCY_TE_SPLITK, blk_splitk=LATENCY_BLK_SPLITK)
 
 
 class CheckedGraph:

@@ -394,6 +394,10 @@ class BlkW:
     sc: Optional[ConvW]
     pool_w: Optional[str]
     pool_b: Optional[str]
+    # the register-direct (frag32) convs again in the generic conv_mfma layout: the batch-1 engine runs them split-K
+    # over input-channel chunks (StyleTTSZS(blk_splitk=...)): a 5-s utterance's decoder conv is 16 tiles otherwise
+    conv1s: Optional[ConvW] = None
+    conv2s: Optional[ConvW] = None
 
 
 def _lane16_ok(w) -> bool:
@@ -417,13 +421,15 @@ def pack_blk(A: Arena, P, name, up=False, x3=False) -> BlkW:
     c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1) and not f1, frag32=f1, x3=x3)
     c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2) and not f2, frag32=f2, x3=x3)
     sc = pack_conv(A, name + ".sc", P[name + ".sc.w"], x3=x3) if name + ".sc.w" in P else None
+    c1s = pack_conv(A, name + ".conv1s", w1, P[name + ".conv1.b"]) if f1 and not x3 else None
+    c2s = pack_conv(A, name + ".conv2s", w2, P[name + ".conv2.b"]) if f2 and not x3 else None
     pw = pb = None
     if up:
         pw = A.add(name + ".poolw", P[name + ".pool.w"].reshape(-1, 3).float())
         pb = A.add(name + ".poolb", P[name + ".pool.b"].float())
     din = P[name + ".conv1.w"].shape[1]
     dout = P[name + ".conv1.w"].shape[0]
-    return BlkW(name, din, dout, up, c1, c2, sc, pw, pb)
+    return BlkW(name, din, dout, up, c1, c2, sc, pw, pb, c1s, c2s)
 
 
 class PackedModel:

@@ -101,6 +101,9 @@ SPLITK_CASES = [  # (B, T, Ci, Co, k, epilogue): the text-encoder shape, then T_
     (3, 300, 512, 256, 3, "acc"),
     (3, 300, 512, 256, 3, "acc_inplace"),
     (2, 200, 512, 384, 1, "leaky"),  # 1x1 with a prologue: conv_mfma, not the LDS-DMA GEMM
+    # the decoder conv1 input width (1090 -> 9 chunks: uneven slices 4 | 5 and 2 | 2 | 2 | 3), statistics + prologue
+    (2, 200, 1090, 256, 3, "stats"),
+    (1, 200, 1090, 256, 3, "leaky"),
 ]
 
 
