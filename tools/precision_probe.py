@@ -3,9 +3,10 @@
 1. sensitivity: a random relative perturbation of ONE stage's output (codes, F0, N, aligned text, text features)
    -> end-to-end log-mel L1 vs the unperturbed oracle;
 2. arithmetic: every conv / linear / attention matmul / LSTM matmul of the oracle emulated with bf16x3 split
-   operands (hi*hi + hi*lo + lo*hi, fp32 accumulate, fp32 activations) and with bf16 operands (hi*hi only).
+   operands (hi*hi + hi*lo + lo*hi, fp32 accumulate, fp32 activations), with the WEIGHT operand rounded to bf16 and
+   the activation split (hi*hi + lo*hi: two products; attention keeps three), and with bf16 operands (hi*hi only).
 
-    python tools/precision_probe.py        (~1-2 min on 8 threads)
+    python tools/precision_probe.py        (~1-2 min on 8 threads; env MODES=3,2,1, SENS=0 skips part 1)
 Oracle use: this is a measurement tool (tools/), not product code.
 """
 import math
@@ -43,18 +44,19 @@ def pert(x, d):
 
 
 base = o["wav"]
+SENS = os.environ.get("SENS", "1") != "0"
 print("== sensitivity: relative perturbation of one stage -> end-to-end log-mel L1")
-for d in (1e-6, 1e-5, 1e-4):
+for d in ((1e-6, 1e-5, 1e-4) if SENS else ()):
     c2 = pert(o["codes"], d)
     pr = R.predict_prosody(P, S, o["h_txt"], c2, dur)
     print(f"codes {d:.0e}: F0 {rel(pr['F0'], o['F0']):.2e} mel "
           f"{mel(R.decode(P, S, pr['asr'], pr['F0'], pr['N'], c2, [7]), base):.2e}", flush=True)
-for d in (1e-6, 1e-5, 1e-4):
+for d in ((1e-6, 1e-5, 1e-4) if SENS else ()):
     print(f"F0 {d:.0e}: mel {mel(R.decode(P, S, o['asr'], pert(o['F0'], d), o['N'], o['codes'], [7]), base):.2e}")
-for d in (1e-5, 1e-4):
+for d in ((1e-5, 1e-4) if SENS else ()):
     print(f"N {d:.0e}: mel {mel(R.decode(P, S, o['asr'], o['F0'], pert(o['N'], d), o['codes'], [7]), base):.2e}")
     print(f"asr {d:.0e}: mel {mel(R.decode(P, S, pert(o['asr'], d), o['F0'], o['N'], o['codes'], [7]), base):.2e}")
-for d in (1e-5, 1e-4):
+for d in ((1e-5, 1e-4) if SENS else ()):
     h2 = pert(o["h_txt"], d)
     c2 = R.sample_style(P, S, h2, o["prompt"], eps, bench.STEPS_LATENCY, bench.CFG)
     pr = R.predict_prosody(P, S, h2, c2, dur)
@@ -72,13 +74,16 @@ def _split(x):
     return h, (x - h).to(torch.bfloat16).float()
 
 
-def x3(op, a, b, bias=None, *args, **kw):
+def x3(op, a, b, bias=None, *args, w_op=True, **kw):
+    """op(a, b) on split operands; b is the weight (w_op) except in the attention products."""
     ah, al = _split(a)
     bh, bl = _split(b)
     if MODE["n"] == 1:
         return op(ah, bh, bias, *args, **kw) if bias is not None or args or kw else op(ah, bh)
     r = op(ah, bh, bias, *args, **kw) if bias is not None or args or kw else op(ah, bh)
     lo = (lambda u, v: op(u, v, None, *args, **kw)) if bias is not None or args or kw else op
+    if MODE["n"] == 2 and w_op:  # bf16 weight, split activation: two products
+        return r + lo(al, bh)
     return r + lo(ah, bl) + lo(al, bh)
 
 
@@ -93,8 +98,8 @@ def mha(q, k, v, heads):
     q = q.view(Rr, Lq, heads, dh).transpose(1, 2)
     k = k.view(Rr, k.shape[1], heads, dh).transpose(1, 2)
     v = v.view(Rr, v.shape[1], heads, dh).transpose(1, 2)
-    a = torch.softmax(x3(_mm, q, k.transpose(-1, -2)) / math.sqrt(dh), dim=-1)
-    return x3(_mm, a, v).transpose(1, 2).reshape(Rr, Lq, D)
+    a = torch.softmax(x3(_mm, q, k.transpose(-1, -2), w_op=False) / math.sqrt(dh), dim=-1)
+    return x3(_mm, a, v, w_op=False).transpose(1, 2).reshape(Rr, Lq, D)
 
 
 def bilstm(x, P_, name):
@@ -117,12 +122,14 @@ def bilstm(x, P_, name):
 
 R._mha, R.bilstm = mha, bilstm
 print("== split-operand emulation, every GEMM-like op, fp32 activations (prompt codes teacher-forced)")
-for n in (3, 1):
+for n in [int(v) for v in os.environ.get("MODES", "3,2,1").split(",")]:
     MODE["n"] = n
     o2 = R.synth(P, S, tok, ref, bench.STEPS_LATENCY, bench.CFG, eps, dur, seeds=[7], prompt_idx=o["prompt_idx"])
-    print(f"{'bf16x3' if n == 3 else 'bf16  '}: h {rel(o2['h_txt'], o['h_txt']):.2e} codes {rel(o2['codes'], o['codes']):.2e} "
+    print(f"{ {3: 'bf16x3', 2: 'w-bf16 x-split', 1: 'bf16'}[n] }: h {rel(o2['h_txt'], o['h_txt']):.2e} codes {rel(o2['codes'], o['codes']):.2e} "
           f"F0 {rel(o2['F0'], o['F0']):.2e} N {rel(o2['N'], o['N']):.2e} wav {rel(o2['wav'], o['wav']):.2e} "
           f"log-mel L1 {mel(o2['wav'], o['wav']):.2e}", flush=True)
-MODE["n"] = 3
-w = R.decode(P, S, o["asr"], o["F0"], o["N"], o["codes"], [7])
-print(f"bf16x3 decoder only (teacher-forced): wav {rel(w, o['wav']):.2e} log-mel L1 {mel(w, o['wav']):.2e}")
+for n in (3, 2):
+    MODE["n"] = n
+    w = R.decode(P, S, o["asr"], o["F0"], o["N"], o["codes"], [7])
+    print(f"{ {3: 'bf16x3', 2: 'w-bf16 x-split'}[n] } decoder only (teacher-forced): wav {rel(w, o['wav']):.2e} "
+          f"log-mel L1 {mel(w, o['wav']):.2e}", flush=True)
