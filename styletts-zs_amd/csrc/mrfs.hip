@@ -15,6 +15,10 @@
 // stores.  One workgroup barrier per tile hands the buffers over.  s_waitcnt vmcnt is per wave, so the consumers'
 // weight and residual loads never wait behind the producers' input loads.  The consumers stream the weight fragments
 // PD K-steps ahead as mrfv does, the ring running on across tiles (every tile uses the same K-steps).
+// NC = 2 (the stage-0 convs, 256 -> 256 channels): the unit of the pipeline is one (tile, 128-channel input chunk);
+// each consumer wave owns 64 output channels (mrfv's wide form: bit-identical to it), accumulates chunk 0 then
+// chunk 1 and runs the epilogue after chunk 1.  Producers and consumers run separate loops with the same barrier
+// count, so the consumers' accumulators are not live across the producers' staging code (register pressure).
 #include "common.hpp"
 
 namespace {
@@ -39,19 +43,20 @@ STZS_DEV void row_sum16(float* x) {
 // staged rows per 16-row pass (as mrfv sb_rows: k3 dil <= 8, k7 / k11 dil <= 5)
 constexpr int sb_of(int ks) { return ks == 3 ? 9 : (ks == 7 ? 10 : 12); }
 
-template <bool HR, bool HA, int KS, bool AL>
+template <bool HR, bool HA, int KS, bool AL, int NC>
 __global__ __launch_bounds__(NTH, 1) void mrfs_conv(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int NKC = KS * 4;              // 32-wide K-steps of the one 128-channel chunk
+    constexpr int NKC = KS * 4;              // 32-wide K-steps of one 128-channel chunk
     constexpr int SB = sb_of(KS);
     // RESW: every weight fragment of the K loop resident in registers (k3: 96 VGPRs).  Off: with the producer's and the
     // consumer's registers allocated together it spilled 28 VGPRs; the k3 K loop streams its weights like k7 / k11
     constexpr bool RESW = false;
     // streamed weights: K-steps in flight ahead of the MFMAs.  The ring slot of K-step s is s % (PD + 1) with s the
-    // compile-time index within the tile, so PD + 1 must divide NKC = 4 KS for the ring to stay aligned when it runs
-    // on into the next tile (register arrays need compile-time indices): PD = 3
-    constexpr int PD = RESW ? 0 : 3;
-    static_assert(RESW || NKC % (PD + 1) == 0, "the weight ring wraps at tile boundaries");
+    // compile-time index within the unit, so PD + 1 must divide NKC = 4 KS for the ring to stay aligned when it runs
+    // on into the next unit (register arrays need compile-time indices): PD = 3; the two-chunk form's K-step is twice
+    // as long (4 fragments): PD = 1, as mrfv's wide form
+    constexpr int PD = RESW ? 0 : (NC == 1 ? 3 : 1);
+    static_assert(RESW || NKC % (PD + 1) == 0, "the weight ring wraps at unit boundaries");
     const int dil = a.dil;
     const int rows_in = BT + (KS - 1) * dil;
     const int buf_bytes = (rows_in * P + 15) & ~15;
@@ -63,19 +68,21 @@ __global__ __launch_bounds__(NTH, 1) void mrfs_conv(const stzs_conv_args a) {
     const int per = (ntiles + G - 1) / G;
     const int tbeg = blockIdx.x * per;
     const int tend = min(ntiles, tbeg + per);
-    const int nmy = tend > tbeg ? tend - tbeg : 0;  // uniform per workgroup: every wave runs the same barriers
+    // pipeline units (tile, chunk), chunk fastest; uniform per workgroup: every wave runs the same barriers
+    const int nmy = tend > tbeg ? (tend - tbeg) * NC : 0;
 
     // ------------------------------------------------------------------ producer: stage tile `tile` into buffer b
     const int ptid = tid - 256;  // producers 0..255 (the mrfv staging thread map)
     const int cv = ptid & 15, rsub = ptid >> 4;
-    auto stage = [&](int tile, int b) {
+    auto stage = [&](int u, int b) {
+        const int tile = tbeg + u / NC, cc = u % NC;
         const int bq = tile / tpb;
         const int t0 = (tile - bq * tpb) * BT;
         const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x) + (long)bq * a.bsx;
-        const int c = cv * 8;
+        const int c = cc * 128 + cv * 8;
         const bool c_ok = c < a.Ci;
         const int cl = c_ok ? c : 0;
-        const bool interior = t0 - a.pad >= 0 && t0 - a.pad + 16 * SB <= a.T_in && 128 <= a.Ci;
+        const bool interior = t0 - a.pad >= 0 && t0 - a.pad + 16 * SB <= a.T_in && cc * 128 + 128 <= a.Ci;
         uint4 raw[SB];
 #pragma unroll
         for (int i = 0; i < SB; ++i) {
@@ -136,54 +143,69 @@ __global__ __launch_bounds__(NTH, 1) void mrfs_conv(const stzs_conv_args a) {
     };
 
     // ------------------------------------------------------------------ consumer state
-    constexpr int NA = 2;
-    const int cw = wave & 3;  // consumer wave: output channels cw * 32 ..
-    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + cw * 128 + lane;
-    bf16x8 wres[RESW ? NKC : 1][NA];
-    bf16x8 wf[PD + 1][NA];
-    int kq = 0;  // streamed: the next K-step (mod NKC) the ring loads
-    if (!producer) {
-        if constexpr (RESW) {
-#pragma unroll
-            for (int s = 0; s < NKC; ++s)
-#pragma unroll
-                for (int j = 0; j < NA; ++j) wres[s][j] = Wf[(long)s * 512 + 64 * j];
-        } else {
-#pragma unroll
-            for (int i = 0; i < PD; ++i)
-#pragma unroll
-                for (int j = 0; j < NA; ++j) wf[i][j] = Wf[(long)i * 512 + 64 * j];
-            kq = PD;
-        }
-    }
+    constexpr int NA = 2 * NC;  // A fragments (16 output channels each) per wave and K-step
+    constexpr int NKT = NC * NKC;  // K-steps of a tile (the weight ring's period)
+    // consumer wave: NC == 1 output channels 32 cw ..; NC == 2 (mrfv's wide map) the packed waves ow0, ow0 + 1 of
+    // 128-channel tile ct
+    const int ct = NC == 1 ? 0 : (wave & 3) >> 1;
+    const int ow0 = NC == 1 ? (wave & 3) : (wave & 1) * 2;
+    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + (long)ct * NKT * 512 + ow0 * 128 + lane;
     const int xoff0 = (lane & 15) * P + (lane >> 4) * 16;
     const int dP = dil * P;
     const int g = lane >> 4, n = lane & 15;
-    const int co0 = cw * 32 + g * 8;
-    const bool col_ok = co0 < a.Co;
-    const int coc = col_ok ? co0 : 0;
-    float bias[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) bias[i] = (!producer && a.bias) ? a.bias[coc + i] : 0.f;
     const bool stat = a.stat_part != nullptr;
     const int nch = (a.T_out + 63) / 64;
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
 
-    auto compute = [&](int tile, int b) {
+    if (NC > 1 && producer) {  // ---------------------------------------- producer loop (two-chunk form)
+        if (nmy > 0) stage(0, 0);
+        __syncthreads();
+        for (int i = 0; i < nmy; ++i) {
+            if (i + 1 < nmy) stage(i + 1, (i + 1) & 1);
+            __syncthreads();  // unit i + 1 staged; unit i's buffer free for unit i + 2
+        }
+        return;
+    }
+    // ------------------------------------------------------------------ consumer loop
+    bf16x8 wres[RESW ? NKC : 1][NA];
+    bf16x8 wf[PD + 1][NA];
+    int kq = 0;  // streamed: the next K-step (mod NKT) the ring loads
+    if (producer) {
+    } else if constexpr (RESW) {
+#pragma unroll
+        for (int s = 0; s < NKC; ++s)
+#pragma unroll
+            for (int j = 0; j < NA; ++j) wres[s][j] = Wf[(long)s * 512 + 64 * j];
+    } else {
+#pragma unroll
+        for (int i = 0; i < PD; ++i)
+#pragma unroll
+            for (int j = 0; j < NA; ++j) wf[i][j] = Wf[(long)i * 512 + 64 * j];
+        kq = PD;
+    }
+    auto compute = [&](f32x4 (&acc)[NA][8], int u, int b) {
+        const int tile = tbeg + u / NC, cc = u % NC;
         const int bq = tile / tpb;
         const int t0 = (tile - bq * tpb) * BT;
         const unsigned char* S = smem + b * buf_bytes;
-        f32x4 acc[NA][8];
         bf16x8 xf[8];
         const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (NC > 1) {
+            if (cc == 0) {
+#pragma unroll
+                for (int j = 0; j < NA; ++j)
+#pragma unroll
+                    for (int mt = 0; mt < 8; ++mt) acc[j][mt] = zero;
+            }
+        }
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(S + xoff0 + mt * 16 * P);
 #pragma unroll
         for (int s = 0; s < NKC; ++s) {
-            if constexpr (!RESW) {  // the ring runs on across tiles: K-step kq of this or the next tile
+            if constexpr (!RESW) {  // the ring runs on across units: K-step kq of this or the next unit
 #pragma unroll
                 for (int j = 0; j < NA; ++j) wf[(s + PD) % (PD + 1)][j] = Wf[(long)kq * 512 + 64 * j];
-                kq = kq + 1 == NKC ? 0 : kq + 1;
+                kq = kq + 1 == NKT ? 0 : kq + 1;
             }
             const int sn = s + 1;
             const int offn = (sn >> 2) * dP + (sn & 3) * 64;
@@ -192,7 +214,7 @@ __global__ __launch_bounds__(NTH, 1) void mrfs_conv(const stzs_conv_args a) {
 #pragma unroll
                 for (int j = 0; j < NA; ++j) {
                     const bf16x8 wv = RESW ? wres[s][j] : wf[s % (PD + 1)][j];
-                    acc[j][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, xf[mt], s == 0 ? zero : acc[j][mt], 0, 0, 0);
+                    acc[j][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, xf[mt], (NC == 1 && s == 0) ? zero : acc[j][mt], 0, 0, 0);
                 }
                 if (sn < NKC) xf[mt] = *reinterpret_cast<const bf16x8*>(S + xoff0 + offn + mt * 16 * P);
             }
@@ -204,19 +226,35 @@ __global__ __launch_bounds__(NTH, 1) void mrfs_conv(const stzs_conv_args a) {
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        // ---- epilogue (mrfv's, one 32-channel group per wave): lane (g, n) holds time t0 + mt 16 + n, channels co0..+7
+        if (cc != NC - 1) return;
+        // ---- epilogue (mrfv's): lane (g, n) holds time t0 + mt 16 + n, channels co0..+7 of each 32-channel group
         const char* Rq = reinterpret_cast<const char*>(a.res) + (long)bq * a.bsr * 2;
         const char* Aq = reinterpret_cast<const char*>(a.acc_in) + (long)bq * a.bsa * 2;
-        uint4 rr[8], aa[8];
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-            const int t = t0 + mt * 16 + n;
-            const int tc = t < a.T_out ? t : a.T_out - 1;
-            if constexpr (HR) rr[mt] = *reinterpret_cast<const uint4*>(Rq + (unsigned)(tc * (int)a.ldr + coc) * 2u);
-            if constexpr (HA) aa[mt] = *reinterpret_cast<const uint4*>(Aq + (unsigned)(tc * (int)a.lda + coc) * 2u);
-        }
+        for (int sw = 0; sw < NC; ++sw) {  // (two-chunk form: the wave's two 32-channel groups one after the other)
+        const int co0 = ct * 128 + (ow0 + sw) * 32 + g * 8;
+        const bool col_ok = co0 < a.Co;
+        const int coc = col_ok ? co0 : 0;
+        float bias[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
+        // residual / accumulate rows: all 8 row tiles at once, or per 64-row half where both operands are present in
+        // the two-chunk form (its 128 accumulator VGPRs leave no room for 64 more)
+        constexpr int RQ = (NC > 1 && HR && HA) ? 4 : 8;
+        uint4 rr[RQ], aa[RQ];
+        auto load_ra = [&](int mt0) {
+#pragma unroll
+            for (int q = 0; q < RQ; ++q) {
+                const int t = t0 + (mt0 + q) * 16 + n;
+                const int tc = t < a.T_out ? t : a.T_out - 1;
+                if constexpr (HR) rr[q] = *reinterpret_cast<const uint4*>(Rq + (unsigned)(tc * (int)a.ldr + coc) * 2u);
+                if constexpr (HA) aa[q] = *reinterpret_cast<const uint4*>(Aq + (unsigned)(tc * (int)a.lda + coc) * 2u);
+            }
+        };
+        if constexpr (RQ == 8) load_ra(0);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+            if constexpr (RQ == 4) load_ra(h * 4);
             float ss[8], sq[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
@@ -229,10 +267,10 @@ __global__ __launch_bounds__(NTH, 1) void mrfs_conv(const stzs_conv_args a) {
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[nt][mt][r] + bias[nt * 4 + r];
+                    for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[sw * 2 + nt][mt][r] + bias[nt * 4 + r];
                 if constexpr (HR) {
                     float f[8];
-                    unpack8(rr[mt], f);
+                    unpack8(rr[RQ == 8 ? mt : m], f);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) v[i] += f[i];
                 }
@@ -242,7 +280,7 @@ __global__ __launch_bounds__(NTH, 1) void mrfs_conv(const stzs_conv_args a) {
                 }
                 if constexpr (HA) {
                     float f[8];
-                    unpack8(aa[mt], f);
+                    unpack8(aa[RQ == 8 ? mt : m], f);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) v[i] = fmaf(a.beta, f[i], v[i]);
                 }
@@ -272,39 +310,55 @@ __global__ __launch_bounds__(NTH, 1) void mrfs_conv(const stzs_conv_args a) {
                 }
             }
         }
-    };
-
-    // ------------------------------------------------------------------ the tile pipeline
-    if (nmy > 0 && producer) stage(tbeg, 0);
-    __syncthreads();
-    for (int i = 0; i < nmy; ++i) {
-        if (!producer) {
-            compute(tbeg + i, i & 1);
-        } else if (i + 1 < nmy) {
-            stage(tbeg + i + 1, (i + 1) & 1);
         }
-        __syncthreads();  // tile i + 1 staged, tile i's buffer free for tile i + 2
+    };
+    if constexpr (NC == 1) {
+        // one loop for both roles (measured: with separate loops hipcc spilled 28-99 VGPRs of the k7 / k11 forms)
+        if (nmy > 0 && producer) stage(0, 0);
+        __syncthreads();
+        for (int i = 0; i < nmy; ++i) {
+            if (!producer) {
+                f32x4 acc[NA][8];
+                compute(acc, i, i & 1);
+            } else if (i + 1 < nmy) {
+                stage(i + 1, (i + 1) & 1);
+            }
+            __syncthreads();  // unit i + 1 staged, unit i's buffer free for unit i + 2
+        }
+    } else {
+        __syncthreads();  // unit 0 staged
+        f32x4 acc[NA][8];
+#pragma unroll 1
+        for (int i = 0; i < nmy; ++i) {
+            compute(acc, i, i & 1);
+            __syncthreads();
+        }
     }
 }
 
-template <bool HR, bool HA, bool AL>
+template <bool HR, bool HA, bool AL, int NC>
 void (*pick_ks(int ks))(stzs_conv_args) {
     switch (ks) {
-        case 3: return mrfs_conv<HR, HA, 3, AL>;
-        case 7: return mrfs_conv<HR, HA, 7, AL>;
-        case 11: return mrfs_conv<HR, HA, 11, AL>;
+        case 3: return mrfs_conv<HR, HA, 3, AL, NC>;
+        case 7: return mrfs_conv<HR, HA, 7, AL, NC>;
+        case 11: return mrfs_conv<HR, HA, 11, AL, NC>;
         default: return nullptr;
     }
+}
+template <bool HR, bool HA, bool AL>
+void (*pick_nc(int ks, int nc))(stzs_conv_args) {
+    return nc == 1 ? pick_ks<HR, HA, AL, 1>(ks) : pick_ks<HR, HA, AL, 2>(ks);
 }
 
 }  // namespace
 
 // internal entry (csrc/mrfv.hip stzs_mrfv_conv_launch): 1 = not this form (the caller goes on), else a status.
-// Taken for STZS_CONV_MRFS: FRAG32 weights, Snake prologue, one 128-channel input chunk and one 128-channel column
-// tile, stride 1, the dilation within the staging of its kernel width.
+// Taken for STZS_CONV_MRFS: FRAG32 weights, Snake prologue, 128 -> 128 channels (stage 1) or 256 -> 256 (stage 0:
+// two input chunks, one 256-channel column tile), stride 1, the dilation within the staging of its kernel width.
 __attribute__((visibility("hidden"))) int stzs_mrfs_conv_launch(const stzs_conv_args& a, hipStream_t s) {
     if (!(a.flags & STZS_CONV_MRFS)) return 1;
-    if (a.pro_act != STZS_ACT_SNAKE || a.ci_pad != 128 || a.co_pad != 128 || a.cic != 128 || a.stride != 1 ||
+    const int nc = a.ci_pad / 128;
+    if (a.pro_act != STZS_ACT_SNAKE || (nc != 1 && nc != 2) || a.co_pad != a.ci_pad || a.cic != 128 || a.stride != 1 ||
         (a.ks != 3 && a.ks != 7 && a.ks != 11) || a.ups || a.refl || a.gate || a.epi_act != STZS_ACT_NONE ||
         a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.splitk > 1 || a.x_scale)
         return 1;
@@ -312,10 +366,10 @@ __attribute__((visibility("hidden"))) int stzs_mrfs_conv_launch(const stzs_conv_
     if (rows_in > 16 * sb_of(a.ks) || !a.pro_alpha || (a.res && a.res_tdiv != 1)) return 1;
     const size_t lds = 2 * (((size_t)rows_in * P + 15) & ~(size_t)15);
     const bool R = a.res != nullptr, A = a.acc_in != nullptr, al = a.alpha != 1.f;
-    void (*k)(stzs_conv_args) = R ? (A ? (al ? pick_ks<true, true, true>(a.ks) : pick_ks<true, true, false>(a.ks))
-                                       : (al ? pick_ks<true, false, true>(a.ks) : pick_ks<true, false, false>(a.ks)))
-                                  : (A ? (al ? pick_ks<false, true, true>(a.ks) : pick_ks<false, true, false>(a.ks))
-                                       : (al ? pick_ks<false, false, true>(a.ks) : pick_ks<false, false, false>(a.ks)));
+    void (*k)(stzs_conv_args) = R ? (A ? (al ? pick_nc<true, true, true>(a.ks, nc) : pick_nc<true, true, false>(a.ks, nc))
+                                       : (al ? pick_nc<true, false, true>(a.ks, nc) : pick_nc<true, false, false>(a.ks, nc)))
+                                  : (A ? (al ? pick_nc<false, true, true>(a.ks, nc) : pick_nc<false, true, false>(a.ks, nc))
+                                       : (al ? pick_nc<false, false, true>(a.ks, nc) : pick_nc<false, false, false>(a.ks, nc)));
     if (!k) return 1;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     const long ntiles = (long)a.B * ((a.T_out + BT - 1) / BT);

@@ -216,7 +216,8 @@ class StyleTTSZS:
         self.noise_super = os.environ.get("STZS_NOISE_SUPER", "1") != "0"
         # the stage-1 MRF convs on the tall register-direct form (csrc/mrfv.hip MR > 8; bit-identical); STZS_MRFV_TALL
         self.mrfv_tall = os.environ.get("STZS_MRFV_TALL", "0") != "0"
-        # the stage-1 MRF convs warp-specialised and persistent (csrc/mrfs.hip; bit-identical); STZS_MRFS
+        # the generator MRF convs (stage 1: 128 channels, stage 0: 256) warp-specialised and persistent (csrc/mrfs.hip;
+        # bit-identical); STZS_MRFS
         self.mrfs = os.environ.get("STZS_MRFS", "0") != "0"
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)

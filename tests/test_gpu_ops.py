@@ -433,12 +433,22 @@ def test_mrf_tall_bit_identical(eng, case):
     assert max_rel(a, ref) < 1.5e-2
 
 
-@pytest.mark.parametrize("case", TALL_CASES + [(64, 3001, 128, 128, 7, 3, "snake", True, True, True, 1)])
+MRFS_STAGE0_CASES = [  # 256 -> 256 channels: the two-chunk form (pipeline unit = tile x input chunk)
+    (2, 1500, 256, 256, 3, 1, "snake", False, False, True, 1),
+    (2, 1000, 256, 256, 7, 3, "snake", True, True, False, 1),   # residual + accumulate: per-half epilogue loads
+    (1, 900, 256, 256, 11, 5, "snake", True, False, True, 1),
+    (3, 300, 256, 256, 3, 5, "snake", False, True, True, 1),
+    (24, 2000, 256, 256, 11, 1, "snake", True, True, False, 1),  # more units than CUs
+]
+
+
+@pytest.mark.parametrize("case", TALL_CASES + [(64, 3001, 128, 128, 7, 3, "snake", True, True, True, 1)] + MRFS_STAGE0_CASES)
 def test_mrf_specialised_bit_identical(eng, case):
-    """the warp-specialised persistent stage-1 form (csrc/mrfs.hip, STZS_CONV_MRFS: producer waves stage tile i + 1
-    while consumer waves run tile i; one workgroup per CU walking a contiguous tile range) vs the register-direct form:
-    same staged operands, same K order, same statistics partials -> bit-identical (tolerance 0), incl. a grid with more
-    tiles than CUs (several tiles per workgroup, the weight ring running on across tiles)."""
+    """the warp-specialised persistent MRF form (csrc/mrfs.hip, STZS_CONV_MRFS: producer waves stage unit i + 1
+    while consumer waves run unit i; one workgroup per CU walking a contiguous tile range; stage 1 one chunk per tile,
+    stage 0 two) vs the register-direct form: same staged operands, same K order, same statistics partials ->
+    bit-identical (tolerance 0), incl. grids with more tiles than CUs (several tiles per workgroup, the weight ring
+    running on across tiles)."""
     from stzs import _lib as L
     a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFS, ref=False)
     b, sb, _ = _run_mrf(eng, case, "frag32", ref=False)
