@@ -4,35 +4,29 @@
 // The input projection x W_ih^T + b is one MFMA GEMM over all steps (stzs_conv1d); this kernel
 // runs only the sequential part, latency-bound by construction.  Design (weights never move):
 //   * per (direction, group of <= 64 utterances) the 4H gate columns are split over P = H/32
-//     workgroups; workgroup p owns hidden units [32p, 32p + 32) = 128 gate columns.  bf16 mode: wave w owns
-//     row tile w >> 1 and units 16 (w & 1) .. + 16, and keeps the W_hh^T B-fragments of ALL FOUR gates of
-//     those units (4 x H/32) in REGISTERS for the whole launch;
+//     workgroups; workgroup p owns hidden units [32p, 32p + 32) = 128 gate columns, and each of its
+//     4 waves keeps ITS gate's 2 x (H/32) W_hh^T B-fragments in REGISTERS for the whole launch;
 //   * per step: h_{t-1} [<=64 x H] (bf16) is read from a double-buffered exchange slab with
-//     16-B write-through (sc1) buffer loads, all in flight at once, into one of two LDS A tiles; 16x16x32
-//     MFMAs give the four gate pre-activations of a lane's 4 (utterance, unit) cells in its own
-//     accumulators, so the cell update (c in registers; sigmoid / tanh from v_exp + v_rcp) follows the
-//     MFMAs with no gate exchange and no barrier; a DPP quad gather packs 4 units' h per lane, published
-//     with one 8-B write-through store (r04: the gates used to meet in an LDS slab, 512 threads x 4 cells
-//     behind a second barrier -- the batch-1 step spent 1 276 of its 3 950 cycles there,
-//     profiles/r04_e_lstm_prof_b1.log);
+//     16-B write-through (sc1) buffer loads, all in flight at once, into an LDS A tile; 16x16x32
+//     MFMAs give the gate pre-activations (8 waves: two per gate, each half of the row tiles), gates
+//     meet in LDS, each of the 512 threads updates 4 (utterance, unit) cells (c in registers;
+//     sigmoid / tanh from v_exp + v_rcp) and publishes its h with one 8-B write-through store
+//     (data-tagged granules -- Guideline 16 R2 -- measured slower: 64 KB re-swept per step);
 //   * hand-off (MI355X guide, Guideline 16 'Valid forms' table row 1): every storing wave drains
 //     vmcnt(0), workgroup barrier, ONE lane adds to the direction's agent-scope arrival counter;
 //     consumers poll that counter with sc1 loads, then all loads of the slab are sc1 (no fences).
 //     Spins are bounded: on timeout the kernel records an error word and finishes (never hangs).
 // Residency: grid = P x ndir x groups <= 64 workgroups, one per CU: always co-resident on MI355X.
 // SMALL BATCHES (a group of <= TAG_ROWS utterances, bf16 mode -- configs[1] runs at batch 1): h travels as
-// data-tagged granules instead (MI355X guide Guideline 16 R2, payload <= 4 KB): each even lane publishes the h of
-// its unit pair as one 8-B {tag = step + 1, bf16 pair} word with an agent-scope atomic store, and the consumers sweep
+// data-tagged granules instead (MI355X guide Guideline 16 R2, payload <= 4 KB): each cell thread publishes its
+// 4 h values as two 8-B {tag = step + 1, bf16 pair} words with agent-scope atomic stores, and the consumers sweep
 // the granules until every tag matches -- one fabric round trip per step instead of drain + counter + poll +
 // slab load.  The granule region (the first TAG_BYTES of the workspace) starts zeroed and every call leaves it
 // zeroed (the last workgroup to finish resets it), so a tag can only match a value of the current call.
 // PRECISE (stzs_lstm_args.precise, the split-operand mode): h travels as hi = bf16(h) and lo = bf16(h - hi)
 // (one slab row = hi[H] | lo[H]), W_hh^T as hi and lo fragments, the recurrent product is
 // h_lo W_hi + h_hi W_lo + h_hi W_hi on the same MFMAs (~fp32 accuracy), the gates use libm expf / tanhf,
-// and y is written in fp32.  Its hi + lo fragments of all four gates would not fit in registers: it keeps the
-// r03 layout (waves = two per gate, each half of the row tiles; the gates meet in an LDS slab).
-#include <stdlib.h>
-
+// and y is written in fp32.
 #include "common.hpp"
 
 namespace {
@@ -68,27 +62,18 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 STZS_DEV float acc_sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
 
-template <int NKS, bool PR, bool GS>
+template <int NKS, bool PR>
 __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.H, G4 = 4 * H;
     const int hp = H + 8;
     constexpr int NH = PR ? 2 : 1;  // slab row = hi[H] (| lo[H])
-    // GS (the r03 gate-slab layout: precise mode, or STZS_LSTM_GATESLAB=1): one A tile [NH][64][hp] + the gate slab
-    // gs [64][4*UNITS + 4]; else two A tiles [2][64][hp] (step s reads
-    // tile s & 1, so the next step's staging never waits for this step's MFMA reads) and no gate slab
-    static_assert(GS || !PR, "the precise mode keeps the gate slab");
-    constexpr int NAT = GS ? NH : 2;
-    bf16_t* As0 = reinterpret_cast<bf16_t*>(smem);
-    float* gs = reinterpret_cast<float*>(smem + ((NH * MROWS * hp * 2 + 15) & ~15));
+    bf16_t* As = reinterpret_cast<bf16_t*>(smem);                                   // [NH][64][hp]
+    float* gs = reinterpret_cast<float*>(smem + ((NH * MROWS * hp * 2 + 15) & ~15)); // [64][4*UNITS + 4]
     __shared__ int s_ok, s_last;
     const int gp = 4 * UNITS + 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // GS: 8 waves, two per gate, each half of the row tiles.  Else wave = (row tile mw = wave >> 1, unit half
-    // uh = wave & 1): all four gates of 16 units x 16 rows, so a lane's gate pre-activations for its cells sit in its
-    // own accumulators (no gate slab, no second barrier)
-    const int gate = wave & 3, mh = wave >> 2;
-    const int uh = wave & 1, mw = wave >> 1;
+    const int gate = wave & 3, mh = wave >> 2;  // 8 waves: two per gate, each half of the row tiles
     const int p = blockIdx.x, dir = blockIdx.y, grp = blockIdx.z;
     const int P = H / UNITS;
     const int b0 = grp * MROWS;
@@ -108,12 +93,11 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
 
     // W_hh^T fragments of this wave's gate (g = wave) for the workgroup's 32 units, in registers
     const bf16_t* Wd = reinterpret_cast<const bf16_t*>(a.whhT) + (long)dir * (G4 / 16) * NKS * 512;
-    constexpr int NWC = GS ? 2 : 4;  // column tiles in registers: GS (gate, 2 x 16 units), else (4 gates, 16 units)
-    bf16x8 bw[NWC][NKS], bwl[PR ? 2 : 1][PR ? NKS : 1];
+    bf16x8 bw[2][NKS], bwl[PR ? 2 : 1][PR ? NKS : 1];
     const long lo_off = (long)2 * (G4 / 16) * NKS * 512;  // PR: the lo fragments follow both directions' hi ones
 #pragma unroll
-    for (int c = 0; c < NWC; ++c) {
-        const int ct = GS ? (gate * H + p * UNITS) / 16 + c : (c * H + p * UNITS) / 16 + uh;
+    for (int c = 0; c < 2; ++c) {
+        const int ct = (gate * H + p * UNITS) / 16 + c;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             bw[c][ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)ct * NKS + ks) * 512 + lane * 8);
@@ -125,11 +109,9 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     const int crow = tid >> 3, cu0 = (tid & 7) * CPT;
     const bool cvalid = crow < nrows;
     const int cb = b0 + (cvalid ? crow : 0);
-    float c[CPT];  // PR: cells (crow, cu0 + j); else (row mw 16 + (lane >> 4) 4 + j, unit p 32 + uh 16 + (lane & 15))
+    float c[CPT];
 #pragma unroll
     for (int j = 0; j < CPT; ++j) c[j] = 0.f;
-    const int un = lane & 15, rg = lane >> 4;
-    const int urow0 = mw * 16 + rg * 4;  // non-PR: this lane's first cell row (+ j)
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
     float* Yf = reinterpret_cast<float*>(a.y);
     if (tid == 0) s_ok = 1;
@@ -143,26 +125,14 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     for (int s = 0; s < a.T; ++s) {
         PROF(0)
         const int t = dir == 0 ? s : a.T - 1 - s;
-        bf16_t* As = GS ? As0 : As0 + (s & 1) * MROWS * hp;
         // gate input projections of this thread's cells (issued early, consumed after the MFMAs)
         float4 gx[4];
-        if constexpr (GS) {
-            const float* G = a.gx + (long)cb * a.bsg + (long)t * a.ldg + dir * G4 + p * UNITS + cu0;
+        const float* G = a.gx + (long)cb * a.bsg + (long)t * a.ldg + dir * G4 + p * UNITS + cu0;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) gx[g] = *reinterpret_cast<const float4*>(G + g * H);
-        } else {  // gx[g][j]: gate g of cell j (rows past the group read as 0)
-            const float* G = a.gx + (long)t * a.ldg + dir * G4 + p * UNITS + uh * 16 + un;
-#pragma unroll
-            for (int j = 0; j < CPT; ++j) {
-                const int row = urow0 + j;
-                const float* Gr = G + (long)(b0 + (row < nrows ? row : 0)) * a.bsg;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) gx[g][j] = row < nrows ? Gr[g * H] : 0.f;
-            }
-        }
+        for (int g = 0; g < 4; ++g) gx[g] = *reinterpret_cast<const float4*>(G + g * H);
         // ---- wait for h_{s-1} from all P workgroups, stage it into the A tile ----
         if (s == 0) {
-            for (int e = tid; e < NAT * MROWS * hp / 8; e += 512) reinterpret_cast<uint4*>(As0)[e] = make_uint4(0, 0, 0, 0);
+            for (int e = tid; e < NH * MROWS * hp / 8; e += 512) reinterpret_cast<uint4*>(As)[e] = make_uint4(0, 0, 0, 0);
         } else if (tagged) {
             // sweep h_{s-1}'s granules (tag s) straight into the A tile: no counter, no fence
             const gu64* src = gran + ((s - 1) & 1) * TAG_ROWS * (H / 2);
@@ -214,71 +184,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         }
         __syncthreads();
         PROF(2)
-        if constexpr (!GS) {
-            // ---- all four gates of this wave's 16 units for its 16 rows, cells updated in the accumulators ----
-            // hw[j]: bf16 h of units u..u+3 of row urow0 + j, gathered into lane u (u % 4 == 0)
-            __attribute__((ext_vector_type(2))) unsigned int hw[CPT];
-            const bool live = mw < nmt;  // wave-uniform
-            if (live) {
-                f32x4 acc[4] = {};
-#pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) {
-                    const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (mw * 16 + un) * hp + ks * 32 + 8 * rg);
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[g][ks], acc[g], 0, 0, 0);
-                }
-                PROF(3)
-                float hv[CPT] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int j = 0; j < CPT; ++j) {
-                    if (mw * 16 + j >= nrows) break;  // wave-uniform: no lane of the wave has a valid row j
-                    const float gi = acc[0][j] + gx[0][j], gf = acc[1][j] + gx[1][j], gg = acc[2][j] + gx[2][j],
-                                go = acc[3][j] + gx[3][j];
-                    const float ig = fast_sigmoid(gi), fg = fast_sigmoid(gf), og = fast_sigmoid(go);
-                    c[j] = fg * c[j] + ig * fast_tanh(gg);
-                    hv[j] = og * fast_tanh(c[j]);
-                }
-#pragma unroll
-                for (int j = 0; j < CPT; ++j) {  // DPP quad_perm [1,2,3,3] / [2,3,3,3] / [3,3,3,3]: units u + 1, 2, 3
-                    const float h1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(hv[j]), 0xF9, 0xF, 0xF, false));
-                    const float h2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(hv[j]), 0xFE, 0xF, 0xF, false));
-                    const float h3 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(hv[j]), 0xFF, 0xF, 0xF, false));
-                    hw[j][0] = pack2bf(hv[j], h1);
-                    hw[j][1] = pack2bf(h2, h3);
-                }
-                if (tagged) {  // granule (row, units u, u + 1) from each even lane: {tag = s + 1, the bf16 pair}
-                    const unsigned long long tg = (unsigned long long)(unsigned)(s + 1) << 32;
-#pragma unroll
-                    for (int j = 0; j < CPT; ++j)
-                        if (urow0 + j < nrows && (un & 1) == 0)
-                            __hip_atomic_store(gran + (s & 1) * TAG_ROWS * (H / 2) + (urow0 + j) * (H / 2) + (p * UNITS + uh * 16 + un) / 2,
-                                               tg | hw[j][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < CPT; ++j)
-                        if (urow0 + j < nrows && (un & 3) == 0)
-                            __builtin_amdgcn_raw_buffer_store_b64(hw[j], xr, ((s & 1) * MROWS * H + (urow0 + j) * H + p * UNITS + uh * 16 + un) * 2, 0, 16);
-                }
-            }
-            PROF(4)
-            if (!tagged) {  // slab hand-off: every storing wave drained, then one arrival per workgroup
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            // the layer output (read by later launches only) leaves after the signal.  No barrier before the next
-            // step: it stages into the other A tile, and this one is restaged only after the next step's barrier
-            if (live) {
-#pragma unroll
-                for (int j = 0; j < CPT; ++j)
-                    if (urow0 + j < nrows && (un & 3) == 0)
-                        *reinterpret_cast<uint2*>(Y + (long)(b0 + urow0 + j) * a.bsy + (long)t * a.ldy + dir * H + p * UNITS + uh * 16 + un) =
-                            make_uint2(hw[j][0], hw[j][1]);
-            }
-            PROF(5)
-            continue;
-        }
-        // ---- (GS) gates of this wave's gate g = wave for all rows: [64 x 32 units] ----
+        // ---- gates of this wave's gate g = wave for all rows: [64 x 32 units] ----
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi) {
             const int mt = mh * 2 + mi;
@@ -437,17 +343,12 @@ extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     if (a->precise && (a->ldy % 4 || a->bsy % 4)) return STZS_ESHAPE;
     const int hp = a->H + 8;
     const int nh = a->precise ? 2 : 1;
-    // the gate-slab layout (precise, or STZS_LSTM_GATESLAB=1 -- the r03 bf16 form, kept as an A/B option): A tiles
-    // (hi | lo) + the gate slab; else two A tiles (the kernel's LDS layout comment)
-    const char* gse = getenv("STZS_LSTM_GATESLAB");  // read per call (tests flip it)
-    const bool gs = a->precise || (gse && gse[0] == '1');
-    const size_t lds = gs ? ((nh * MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4
-                          : (size_t)2 * MROWS * hp * 2;
+    const size_t lds = ((nh * MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4;
     dim3 grid(P, a->ndir, groups);
     switch (a->H / 32) {
 #define STZS_LSTM_CASE(n)                                                                                   \
     case n: {                                                                                               \
-        auto k = a->precise ? lstm_xchg<n, true, true> : (gs ? lstm_xchg<n, false, true> : lstm_xchg<n, false, false>); \
+        auto k = a->precise ? lstm_xchg<n, true> : lstm_xchg<n, false>;                                     \
         if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
         hipLaunchKernelGGL(k, grid, dim3(512), lds, s, *a);                                                 \
         break;                                                                                              \
