@@ -169,14 +169,6 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * 128 output channels per workgroup instead of its default wide form (256 per workgroup: every staged input row
  * transformed once per 256 channels instead of once per 128).  Bit-identical either way; an A/B switch. */
 #define STZS_CONV_MRFV_NARROW 8192
-/* flags bit (FRAG32 weights, Snake prologue, ci_pad == 128: the stage-1 generator convs): the TALL register-direct
- * form -- 256 rows (192 for k11) x 128 output channels per workgroup, each wave 32 channels x all rows, so a weight
- * fragment from L2 feeds twice the MFMAs.  Bit-identical to the 128-row form; an A/B switch. */
-#define STZS_CONV_MRFV_TALL 16384
-/* flags bit (FRAG32 weights, Snake prologue, ci_pad == co_pad == 128: the stage-1 generator convs): the warp-specialised
- * persistent form (csrc/mrfs.hip) -- one 512-thread workgroup per CU, producer waves stage tile i + 1 while consumer
- * waves run tile i's K loop and epilogue.  Bit-identical to the register-direct form. */
-#define STZS_CONV_MRFS 32768
 size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 

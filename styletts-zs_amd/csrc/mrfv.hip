@@ -36,11 +36,6 @@ constexpr int P = 272;  // staged input row pitch, bytes (conflict-free ds_read_
 // of the Snake) whether or not its row is used, and a k3 tile with SB = 12 transformed 192 rows for 130-138
 constexpr int sb_rows(int ks) { return ks == 3 ? 9 : (ks == 7 ? 10 : 12); }
 constexpr int SB_MAX = 12;
-// TALL stage-1 form (MR > 8 row tiles of 16 per workgroup, one 128-channel chunk): the rows staged per 16-row pass
-constexpr int sb_rows_tall(int ks, int mr) { return (16 * mr + (ks == 3 ? 10 : (ks == 7 ? 18 : 50)) + 15) / 16; }
-// row tiles per workgroup of the tall form: 256 rows for k3 / k7 (<= 274 staged rows, 74.5 KB), 192 for k11 (d <= 5:
-// 242 rows, 65.8 KB) -- two workgroups per CU either way; a multiple of 4 (the 64-row statistics chunks)
-constexpr int mr_tall(int ks) { return ks == 11 ? 12 : 16; }
 constexpr int CS_BYTES = 5 * 128 * 4;  // per-channel prologue constants
 
 // x[0..N) summed over the 16 lanes of each DPP row, in place, VALU only.  Each step is ONE v_add_f32 with the DPP
@@ -68,16 +63,9 @@ STZS_DEV void row_sum16_n(float* x) {
 // inputs with co_pad % 256 == 0): 256, so a 256-channel layer stages (loads + AdaIN + Snake) each input row ONCE
 // instead of once per 128-channel tile, and every B fragment read from LDS feeds 4 MFMAs instead of 2.  Same K
 // order per output element either way (bit-identical).
-// MR: 16-row tiles per workgroup.  8 (128 rows): the narrow / wide forms.  16 or 12 (the TALL stage-1 form, NCH = 1,
-// WPW = 1): each wave still owns 32 output channels but computes them for 256 (192) rows, so a weight fragment loaded
-// from L2 feeds MR MFMAs instead of 8 (half the weight traffic per FLOP), a K-step is 2 MR MFMAs per wave (twice the
-// time for the next weight K-step to arrive), and the dilation halo is a smaller share of the staged rows; two
-// workgroups per CU (VGPR- and LDS-limited) instead of three.  Same K order per output element: bit-identical.
-template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int MR = 8>
-__global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC)) void mrfv_conv(const stzs_conv_args a) {
+template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1>
+__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
     static_assert(WPW == 1 || (WPW == 2 && NCH != 1), "the wide form is for multi-chunk inputs");
-    static_assert(MR == 8 || (NCH == 1 && WPW == 1 && MR % 4 == 0), "the tall form: one chunk, 32 channels per wave");
-    constexpr int BT = 16 * MR;
     constexpr int NA = 2 * WPW;  // A fragments (16 output channels each) per wave and K-step
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NKC = KS * 4;  // 32-wide K-steps per 128-channel chunk
@@ -93,7 +81,7 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
     const int bq = bx / tpb;
     const int t0 = (bx - bq * tpb) * BT;
     const int nchunk = NCH ? NCH : a.ci_pad >> 7;
-    constexpr int SB = MR == 8 ? sb_rows(KS) : sb_rows_tall(KS, MR);
+    constexpr int SB = sb_rows(KS);
     // weights: [co tile][chunk][tap][kq][wave][nt][lane][8] bf16 -> 512 bf16x8 per K-step.  Wide form: wave w takes
     // the packed waves 2 (w & 1) and 2 (w & 1) + 1 of 128-channel tile 2 by + (w >> 1) -- consecutive in the stream
     const int ct = WPW == 1 ? by : by * 2 + (wave >> 1);
@@ -104,7 +92,7 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
 #pragma unroll
         for (int j = 0; j < NA; ++j) w[j] = p[64 * j];
     };
-    f32x4 acc[NA][MR];
+    f32x4 acc[NA][8];
 
     const int xoff0 = (lane & 15) * P + (lane >> 4) * 16;
     const int dP = dil * P;
@@ -117,7 +105,7 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
     // time, and two spill its 256 VGPRs)
     constexpr int PD = WPW == 2 ? 1 : STZS_MRFV_PD;
     bf16x8 wf[PD + 1][NA];
-    bf16x8 xf[MR];
+    bf16x8 xf[8];
 
     for (int cc = 0; cc < nchunk; ++cc) {
         const int kb = cc * NKC;
@@ -234,14 +222,14 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
             constexpr bool FIRST = decltype(first_tag)::value;
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int mt = 0; mt < MR; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
+            for (int mt = 0; mt < 8; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
 #pragma unroll
             for (int s = 0; s < NKC; ++s) {
                 if (s + PD < NKC) wload(wf[(s + PD) % (PD + 1)], kb + s + PD);
                 const int sn = s + 1;
                 const int offn = (sn >> 2) * dP + (sn & 3) * 64;
 #pragma unroll
-                for (int mt = 0; mt < MR; ++mt) {
+                for (int mt = 0; mt < 8; ++mt) {
                     const bool z = FIRST && s == 0;
 #pragma unroll
                     for (int j = 0; j < NA; ++j)
@@ -252,7 +240,7 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
                     __builtin_amdgcn_sched_group_barrier(0x020, NA, 0);  // the weight loads first
                 }
 #pragma unroll
-                for (int mt = 0; mt < MR; ++mt) {
+                for (int mt = 0; mt < 8; ++mt) {
                     __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
                     if (sn < NKC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
@@ -266,7 +254,7 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
 #pragma unroll
                 for (int i = 0; i < NA; ++i)
 #pragma unroll
-                    for (int j = 0; j < MR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
             kloop(std::integral_constant<bool, false>{});
         }
@@ -290,33 +278,27 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
     float bias[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
-    // the residual / accumulate rows of a 64-row chunk: with MR = 8 both chunks' rows go out at once (the second
-    // chunk's HBM latency hides behind the first chunk's epilogue); the tall form loads chunk by chunk (registers)
-    constexpr int RQ = MR == 8 ? 8 : 4;
-    uint4 rr[RQ], aa[RQ];
-    auto load_ra = [&](int mt0) {
+    // the residual / accumulate rows of BOTH halves in flight at once (the second half's HBM latency hides
+    // behind the first half's epilogue); uniform utterance bases + 32-bit per-lane offsets
+    uint4 rr[8], aa[8];
 #pragma unroll
-        for (int q = 0; q < RQ; ++q) {
-            const int t = t0 + (mt0 + q) * 16 + n;
-            const int tc = t < a.T_out ? t : a.T_out - 1;
-            if constexpr (HR) {
-                const int tr = TD1 ? tc : tc / a.res_tdiv;
-                rr[q] = *reinterpret_cast<const uint4*>(Rq + (unsigned)(tr * (int)a.ldr + coc) * 2u);
-            }
-            if constexpr (HA) aa[q] = *reinterpret_cast<const uint4*>(Aq + (unsigned)(tc * (int)a.lda + coc) * 2u);
+    for (int mt = 0; mt < 8; ++mt) {
+        const int t = t0 + mt * 16 + n;
+        const int tc = t < a.T_out ? t : a.T_out - 1;
+        if constexpr (HR) {
+            const int tr = TD1 ? tc : tc / a.res_tdiv;
+            rr[mt] = *reinterpret_cast<const uint4*>(Rq + (unsigned)(tr * (int)a.ldr + coc) * 2u);
         }
-    };
-    if constexpr (RQ == 8) load_ra(0);
+        if constexpr (HA) aa[mt] = *reinterpret_cast<const uint4*>(Aq + (unsigned)(tc * (int)a.lda + coc) * 2u);
+    }
 #pragma unroll
-    for (int h = 0; h < MR / 4; ++h) {  // 64-row chunks: one statistics partial each
-        if constexpr (RQ == 4) load_ra(h * 4);
+    for (int h = 0; h < 2; ++h) {  // two 64-row halves: one statistics partial each
         float ss[8], sq[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const int mt = h * 4 + m;
-            const int q = RQ == 8 ? mt : m;
             const int t = t0 + mt * 16 + n;
             const bool ok = col_ok && t < a.T_out;
             float v[8];
@@ -326,7 +308,7 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
                 for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[sw * 2 + nt][mt][r] + bias[nt * 4 + r];
             if constexpr (HR) {
                 float f[8];
-                unpack8(rr[q], f);
+                unpack8(rr[mt], f);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] += f[i];
             }
@@ -336,7 +318,7 @@ __global__ __launch_bounds__(NTH, MR > 8 ? 2 : (NCH == 1 ? STZS_MRFV_OCC1 : STZS
             }
             if constexpr (HA) {
                 float f[8];
-                unpack8(aa[q], f);
+                unpack8(aa[mt], f);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = fmaf(a.beta, f[i], v[i]);
             }
@@ -378,18 +360,8 @@ void (*pick_ks(int ks))(stzs_conv_args) {
         default: return nullptr;
     }
 }
-template <int PACT, bool HR, bool HA, bool AL>
-void (*pick_tall(int ks))(stzs_conv_args) {
-    switch (ks) {
-        case 3: return mrfv_conv<PACT, HR, HA, 3, 1, AL, 1, mr_tall(3)>;
-        case 7: return mrfv_conv<PACT, HR, HA, 7, 1, AL, 1, mr_tall(7)>;
-        case 11: return mrfv_conv<PACT, HR, HA, 11, 1, AL, 1, mr_tall(11)>;
-        default: return nullptr;
-    }
-}
 template <int PACT, bool HR, bool HA>
-void (*pick(int ks, bool one, bool al, bool wide, bool tall))(stzs_conv_args) {
-    if (tall) return al ? pick_tall<PACT, HR, HA, true>(ks) : pick_tall<PACT, HR, HA, false>(ks);
+void (*pick(int ks, bool one, bool al, bool wide))(stzs_conv_args) {
     if (wide) return al ? pick_ks<PACT, HR, HA, 0, true, 2>(ks) : pick_ks<PACT, HR, HA, 0, false, 2>(ks);
     if (al) return one ? pick_ks<PACT, HR, HA, 1, true>(ks) : pick_ks<PACT, HR, HA, 0, true>(ks);
     return one ? pick_ks<PACT, HR, HA, 1, false>(ks) : pick_ks<PACT, HR, HA, 0, false>(ks);
@@ -398,32 +370,20 @@ void (*pick(int ks, bool one, bool al, bool wide, bool tall))(stzs_conv_args) {
 }  // namespace
 
 int stzs_mrfp_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrfp.hip (1: not applicable)
-int stzs_mrfs_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrfs.hip (1: not applicable)
 int stzs_ups_conv_launch(const stzs_conv_args& a, hipStream_t s);   // csrc/ups.hip (polyphase ConvTranspose)
 
 // internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32 weights
 __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s) {
     if (a.ups > 0) return stzs_ups_conv_launch(a, s);
-    // the tall stage-1 form (STZS_CONV_MRFV_TALL): one 128-channel chunk, Snake prologue, dilation within its staging
-    const int mrt = a.ks == 11 ? mr_tall(11) : mr_tall(3);
-    const bool tall = (a.flags & STZS_CONV_MRFV_TALL) && a.pro_act == STZS_ACT_SNAKE && a.ci_pad == 128 &&
-                      (a.ks == 3 || a.ks == 7 || a.ks == 11) &&
-                      16 * mrt + (a.ks - 1) * a.dil <= 16 * sb_rows_tall(a.ks, mrt);
-    const int BTl = tall ? 16 * mrt : BT;
-    const int rows_in = BTl + (a.ks - 1) * a.dil;
-    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO ||
-        (!tall && rows_in > 16 * (a.ks == 3 ? sb_rows(3) : a.ks == 7 ? sb_rows(7) : SB_MAX)) ||
+    const int rows_in = BT + (a.ks - 1) * a.dil;
+    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || rows_in > 16 * (a.ks == 3 ? sb_rows(3) : a.ks == 7 ? sb_rows(7) : SB_MAX) ||
         a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.gate || a.epi_act != STZS_ACT_NONE || a.ups ||
         a.refl || a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv <= 0)) ||
         (a.acc_in && (a.lda % 8 || a.bsa % 8)) || (a.stat_part && a.stat_ld < a.Co))
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
     if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
-    {  // STZS_CONV_MRFS: the stage-1 convs warp-specialised and persistent (csrc/mrfs.hip)
-        const int r = stzs_mrfs_conv_launch(a, s);
-        if (r != 1) return r;
-    }
-    if (!tall) {  // STZS_CONV_MRF_PIPE: the k3 single-chunk residual convs on the persistent LDS-DMA-pipelined form (mrfp.hip)
+    {  // STZS_CONV_MRF_PIPE: the k3 single-chunk residual convs on the persistent LDS-DMA-pipelined form (mrfp.hip)
         const int r = stzs_mrfp_conv_launch(a, s);
         if (r != 1) return r;
     }
@@ -434,13 +394,13 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     // CU two workgroups (at batch 1 a stage-0 conv has 32 row tiles: the narrow form's 64 workgroups finish sooner),
     // unless STZS_CONV_MRFV_NARROW.  Both forms are bit-identical, so the choice never changes a result.
     const long wide_tiles = (long)a.B * ((a.T_out + BT - 1) / BT) * (a.co_pad / (2 * BCO));
-    const bool wide = !tall && a.pro_act == STZS_ACT_SNAKE && a.ci_pad > 128 && a.co_pad % (2 * BCO) == 0 &&
+    const bool wide = a.pro_act == STZS_ACT_SNAKE && a.ci_pad > 128 && a.co_pad % (2 * BCO) == 0 &&
                       wide_tiles >= 512 && !(a.flags & STZS_CONV_MRFV_NARROW);
     if (a.pro_act == STZS_ACT_SNAKE) {
         const bool one = a.ci_pad == 128;
         const bool al = a.alpha != 1.f;
-        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide, tall) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide, tall))
-              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide, tall) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide, tall));
+        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide))
+              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide));
     } else if (!A && a.ks == 3) {  // the AdaIN residual blocks of the decoder / prosody predictor
         if (a.pro_act == STZS_ACT_LEAKY)
             k = R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true>;
@@ -449,7 +409,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     }
     if (!k) return STZS_ESHAPE;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BTl - 1) / BTl), a.co_pad / (wide ? 2 * BCO : BCO));
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / (wide ? 2 * BCO : BCO));
     hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;

@@ -26,8 +26,6 @@ CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD
 CONV_MRF_PIPE = 512  # include/stzs.h STZS_CONV_MRF_PIPE (k3 residual MRF convs on csrc/mrfp.hip, opt-in)
 CONV_ROWS = 2048  # include/stzs.h STZS_CONV_ROWS (small-M linear on the whole chip, csrc/rows.hip)
 CONV_UPS_NOISE = 4096  # include/stzs.h STZS_CONV_UPS_NOISE (ConvTranspose + fused 1x1 noise conv, csrc/ups.hip)
-CONV_MRFS = 32768  # include/stzs.h STZS_CONV_MRFS (stage-1 MRF convs warp-specialised + persistent, csrc/mrfs.hip)
-CONV_MRFV_TALL = 16384  # include/stzs.h STZS_CONV_MRFV_TALL (stage-1 MRF convs on 256 / 192-row tiles)
 CONV_MRFV_NARROW = 8192  # include/stzs.h STZS_CONV_MRFV_NARROW (register-direct MRF conv at 128 channels per workgroup)
 
 vp = C.c_void_p

@@ -214,11 +214,6 @@ class StyleTTSZS:
         # the first stage's strided noise conv on super-rows of the harmonic source (register-direct kernel, bf16
         # engines); STZS_NOISE_SUPER=0: the stride-6 conv_mfma form
         self.noise_super = os.environ.get("STZS_NOISE_SUPER", "1") != "0"
-        # the stage-1 MRF convs on the tall register-direct form (csrc/mrfv.hip MR > 8; bit-identical); STZS_MRFV_TALL
-        self.mrfv_tall = os.environ.get("STZS_MRFV_TALL", "0") != "0"
-        # the generator MRF convs (stage 1: 128 channels, stage 0: 256) warp-specialised and persistent (csrc/mrfs.hip;
-        # bit-identical); STZS_MRFS
-        self.mrfs = os.environ.get("STZS_MRFS", "0") != "0"
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
@@ -1370,8 +1365,6 @@ class StyleTTSZS:
         t1 = self.act(f"gen.t1_{i}", B, T, c, dt)
         mx, rx, sb = self.stats(x, f"gen.sx{i}")
         nk = len(S.rb_kernels)
-        # (the kernels take these flags for the single-chunk stage-1 convs only)
-        tall = (L.CONV_MRFV_TALL if self.mrfv_tall else 0) | (L.CONV_MRFS if self.mrfs else 0)
         for j, res in enumerate(W.rb[i]):
             cur, cm, cr = x, mx, rx
             for m, lw in enumerate(res):
@@ -1380,13 +1373,13 @@ class StyleTTSZS:
                 o2, c2 = ng.offsets[lw["n2"]]
                 _, (tm, tr, _) = self.conv(lw["c1"], cur, t1, pad=dil * (k - 1) // 2, dil=dil,
                                            pro=(cm, cr, sb, gbase + o1 * 4, gbs, c1), pro_act=L.ACT_SNAKE,
-                                           pro_alpha=lw["a1"], stats_key=f"gen.st{i}", flags=tall, what="rb.c1")
+                                           pro_alpha=lw["a1"], stats_key=f"gen.st{i}", what="rb.c1")
                 last = m == len(res) - 1
                 out = xs if last else (bufA if cur is not bufA else bufB)
                 r2 = self.conv(lw["c2"], t1, out, pad=(k - 1) // 2, pro=(tm, tr, sb, gbase + o2 * 4, gbs, c2),
                                pro_act=L.ACT_SNAKE, pro_alpha=lw["a2"], res=cur, alpha=(1.0 / nk) if last else 1.0,
                                acc_in=(xs if (last and j > 0) else None), beta=1.0,
-                               stats_key=None if last else f"gen.sc{i}.{m % 2}", flags=tall, what="rb.c2")
+                               stats_key=None if last else f"gen.sc{i}.{m % 2}", what="rb.c2")
                 if not last:
                     _, (cm, cr, _) = r2
                     cur = out

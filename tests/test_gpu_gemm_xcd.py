@@ -130,7 +130,8 @@ def test_conv_mfma_splitk(eng, splitk, case):
     cw = pack_conv(A, "t", w, b)
     A.finalize("cuda:0")
     cw.w, cw.b = A[cw.w], A[cw.b]
-    xd = x.to(torch.bfloat16).cuda()
+    xd = torch.zeros(B, T, (Ci + 7) // 8 * 8, dtype=torch.bfloat16, device="cuda:0")  # rows 16-B aligned
+    xd[:, :, :Ci] = x.to(torch.bfloat16).cuda()
     rd = r.to(torch.bfloat16).cuda()
     accd = acc.to(torch.bfloat16).cuda()
     alpha, beta = (0.7, 0.5) if epi.startswith("acc") else (1.0, 0.0)

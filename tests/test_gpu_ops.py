@@ -406,57 +406,6 @@ def test_mrf_wide_bit_identical(eng, case):
         assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
 
 
-# single-chunk Snake convs (the stage-1 generator shapes): the tall form (STZS_CONV_MRFV_TALL, 256 / 192 rows per
-# workgroup) -- ragged last tiles, dilations 1..5 at every kernel width, residual / accumulate / statistics forms
-TALL_CASES = [
-    (3, 3001, 128, 128, 3, 1, "snake", False, False, True, 1),
-    (2, 1000, 128, 128, 3, 5, "snake", True, True, False, 1),
-    (2, 2500, 128, 128, 7, 3, "snake", True, False, True, 1),
-    (1, 701, 128, 128, 7, 1, "snake", False, True, True, 1),
-    (2, 2400, 128, 128, 11, 5, "snake", True, False, True, 1),
-    (3, 450, 128, 128, 11, 3, "snake", False, False, True, 1),
-    (2, 129, 128, 96, 11, 1, "snake", True, False, True, 1),    # Co < co_pad, one ragged tile
-]
-
-
-@pytest.mark.parametrize("case", TALL_CASES)
-def test_mrf_tall_bit_identical(eng, case):
-    """the tall stage-1 form (each wave 32 output channels x 256 rows, 192 for k11) vs the 128-row register-direct
-    form: the same staged operands in the same K order per output -> outputs and fused statistics bit-identical
-    (tolerance 0); and vs the fp32 reference at the persistent-conv tolerance."""
-    from stzs import _lib as L
-    a, sa, ref = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_TALL)
-    b, sb, _ = _run_mrf(eng, case, "frag32", ref=False)
-    assert torch.equal(a, b)
-    if sa is not None:
-        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
-    assert max_rel(a, ref) < 1.5e-2
-
-
-MRFS_STAGE0_CASES = [  # 256 -> 256 channels: the two-chunk form (pipeline unit = tile x input chunk)
-    (2, 1500, 256, 256, 3, 1, "snake", False, False, True, 1),
-    (2, 1000, 256, 256, 7, 3, "snake", True, True, False, 1),   # residual + accumulate: per-half epilogue loads
-    (1, 900, 256, 256, 11, 5, "snake", True, False, True, 1),
-    (3, 300, 256, 256, 3, 5, "snake", False, True, True, 1),
-    (24, 2000, 256, 256, 11, 1, "snake", True, True, False, 1),  # more units than CUs
-]
-
-
-@pytest.mark.parametrize("case", TALL_CASES + [(64, 3001, 128, 128, 7, 3, "snake", True, True, True, 1)] + MRFS_STAGE0_CASES)
-def test_mrf_specialised_bit_identical(eng, case):
-    """the warp-specialised persistent MRF form (csrc/mrfs.hip, STZS_CONV_MRFS: producer waves stage unit i + 1
-    while consumer waves run unit i; one workgroup per CU walking a contiguous tile range; stage 1 one chunk per tile,
-    stage 0 two) vs the register-direct form: same staged operands, same K order, same statistics partials ->
-    bit-identical (tolerance 0), incl. grids with more tiles than CUs (several tiles per workgroup, the weight ring
-    running on across tiles)."""
-    from stzs import _lib as L
-    a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFS, ref=False)
-    b, sb, _ = _run_mrf(eng, case, "frag32", ref=False)
-    assert torch.equal(a, b)
-    if sa is not None:
-        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
-
-
 @pytest.mark.parametrize("case", PIPE_CASES)
 def test_mrf_pipelined_bit_identical(eng, case):
     """the persistent LDS-DMA-pipelined k3 kernel (csrc/mrfp.hip, STZS_CONV_MRF_PIPE) vs the one-tile-per-

@@ -49,9 +49,6 @@ for (T, C, k, dil) in cases:
         forms = [("lane16", c16, 0), ("mrfv", cfr, 0)]
         # single-chunk: the persistent form; two chunks: the narrow (128 channels per workgroup) register-direct form
         forms.append(("mrfp", cfr, L.CONV_MRF_PIPE) if C == 128 else ("mrfvN", cfr, L.CONV_MRFV_NARROW))
-        if C == 128:
-            forms.append(("tall", cfr, L.CONV_MRFV_TALL))
-        forms.append(("mrfs", cfr, L.CONV_MRFS))
         for name, cw, fl in forms:
             y = Act(torch.zeros(B, T, C, device=dev, dtype=torch.bfloat16))
             kw = dict(pad=dil * (k - 1) // 2, dil=dil, pro=(mean, rstd, C, gb.data_ptr(), 2 * C, C),
