@@ -16,12 +16,19 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts-zs_amd")]
 SO = os.path.join(ROOT, "tools", "probe", "libgemmprof.so")
-if "--build" in sys.argv:
+if "--build" in sys.argv:  # the whole library (conv.hip calls into the other kernels' launchers) with the stamps on
     src = os.path.join(ROOT, "styletts-zs_amd", "csrc")
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
-                           "-ffp-contract=fast", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
-                           "-DSTZS_GEMM_PROF", "-I" + os.path.join(ROOT, "include"), "-I" + src,
-                           os.path.join(src, "conv.hip"), "-o", SO])
+    sys.path.insert(0, os.path.join(ROOT, "styletts-zs_amd"))
+    import build as B  # noqa: E402
+    objs = []
+    tmp = os.path.join("/tmp", "gemmprof_build")
+    os.makedirs(tmp, exist_ok=True)
+    for f in B.sources():
+        o = os.path.join(tmp, os.path.basename(f) + ".o")
+        subprocess.check_call([B.HIPCC] + B.FLAGS + B.FILE_FLAGS.get(os.path.basename(f), []) +
+                              ["-DSTZS_GEMM_PROF", "-c", f, "-o", o])
+        objs.append(o)
+    subprocess.check_call([B.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", SO])
     sys.exit(0)
 
 import torch  # noqa: E402
