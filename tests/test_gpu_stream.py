@@ -113,10 +113,12 @@ def _windows_l1(a, b, S, sec=5):
 
 
 # configs[4] bounds, ~2x the values measured on MI355X (r04):
-TOL_LF_CODES = 5e-2        # fp8 sampler codes vs the fp32 oracle (measured 2.43e-2)
-TOL_LF_MEL = 1.6e-1        # exact fp8 30-s path, log-mel L1 vs the oracle on the GPU's codes
-TOL_LF_TF_WAV = 1.05e-1    # decoder teacher-forced on the oracle's aligned features / F0 / N at 30 s: waveform rel-L2
-TOL_LF_TF_MEL = 7.5e-2     # ... and its log-mel L1 (the 5-s decoder bounds of tests/test_gpu_configs.py)
+# measured r04_h (profiles/r04_h_gpu_tests.log): codes 2.43e-2; exact path log-mel L1 1.53e-1 (per 5 s 0.068 -> 0.26: the
+# harmonic source's phase drifts over 30 s of F0 integration); teacher-forced wav 5.26e-2, log-mel 3.63e-2 (flat per 5 s)
+TOL_LF_CODES = 5e-2        # fp8 sampler codes vs the fp32 oracle (2.1x measured)
+TOL_LF_MEL = 3.0e-1        # exact fp8 30-s path, log-mel L1 vs the oracle on the GPU's codes (2.0x measured)
+TOL_LF_TF_WAV = 1.05e-1    # decoder teacher-forced on the oracle's aligned features / F0 / N at 30 s: waveform rel-L2 (2.0x)
+TOL_LF_TF_MEL = 7.5e-2     # ... and its log-mel L1 (2.1x measured; the 5-s decoder bounds of tests/test_gpu_configs.py)
 
 
 def test_longform_30s_stream(gpu_device, v0):
