@@ -91,17 +91,14 @@ for M in [int(v) for v in os.environ.get("M", "3200,6400").split(",")]:
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3
-        st = stamps.view(-1, 8)
-        st = st[st[:, 0] != 0].double()
+        st = stamps.view(-1, 8)[:, :5].cpu()
+        st = st[(st != 0).all(dim=1)].double()  # workgroups that stamped all five points
         n = st.shape[0]
-        t0 = st[:, 0].min()
-        span = (st[:, 4].max() - t0).item()
-        clk = span / us if us > 0 else 0.0  # shader cycles per us over the stamped span
+        # (s_memtime counters are per XCD and not aligned across XCDs: only differences within a workgroup are used)
         ph = {"fill (start -> K-step 0 landed)": st[:, 1] - st[:, 0], "K loop": st[:, 2] - st[:, 1],
               "epilogue issue": st[:, 3] - st[:, 2], "store drain": st[:, 4] - st[:, 3],
-              "workgroup total": st[:, 4] - st[:, 0], "start offset vs first": st[:, 0] - t0}
-        print(f"{name:5s} M={M} K={K} N={N}: {n} workgroups, launch {us:.1f} us (events), stamped span {span:.0f} cyc",
-              flush=True)
+              "workgroup total": st[:, 4] - st[:, 0]}
+        print(f"{name:5s} M={M} K={K} N={N}: {n} workgroups stamped, launch {us:.1f} us (events)", flush=True)
         for k, v in ph.items():
             q = torch.quantile(v, torch.tensor([0.5, 0.9], dtype=torch.float64))
             print(f"    {k:34s} median {q[0].item():8.0f} cyc  p90 {q[1].item():8.0f} cyc", flush=True)
