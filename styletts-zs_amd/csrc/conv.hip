@@ -511,6 +511,15 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
 }
 
 // Accumulators -> LDS (fp32, padded rows) -> vectorised fused epilogue.
+// STZS_GEMM_PROF probe build: the epilogue's own stamps (slots 5: accumulators in LDS, 6: bias / gate constants in LDS)
+#ifdef STZS_GEMM_PROF
+#define GPROF_E(i)                                                                                            \
+    if (FLAT && a.splitk <= 1 && a.splitk_ws && threadIdx.x == 0)                                              \
+        reinterpret_cast<unsigned long long*>(a.splitk_ws)[(long)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = \
+            __builtin_amdgcn_s_memtime();
+#else
+#define GPROF_E(i)
+#endif
 template <typename TOut, bool FLAT, int BTM>
 STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0,
                      int by) {
@@ -526,6 +535,7 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigne
             for (int r = 0; r < 4; ++r)
                 ep[(wt * (BTM / 2) + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
     if (a.flags & 4) return;
+    GPROF_E(5)
     float* c_bias = ep + BT * EP_PITCH;       // [BCO] bias, [BCO] gate (conv mode: one utterance)
     float* c_gate = c_bias + BCO;
     if (tid < BCO) {
@@ -535,6 +545,7 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigne
         c_gate[tid] = (!FLAT && a.gate) ? a.gate[(long)bq * a.gate_bs + co] : 1.f;
     }
     __syncthreads();
+    GPROF_E(6)
     if (epi_vec(a)) {
         if (a.res && a.acc_in) epilogue_act<TOut, FLAT, true, true, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
         else if (a.res) epilogue_act<TOut, FLAT, true, true, false, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);

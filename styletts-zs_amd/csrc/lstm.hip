@@ -18,8 +18,9 @@
 //     Spins are bounded: on timeout the kernel records an error word and finishes (never hangs).
 // Residency: grid = P x ndir x groups <= 64 workgroups, one per CU: always co-resident on MI355X.
 // SMALL BATCHES (a group of <= TAG_ROWS utterances, bf16 mode -- configs[1] runs at batch 1): h travels as
-// data-tagged granules instead (MI355X guide Guideline 16 R2, payload <= 4 KB): each cell thread publishes its
-// 4 h values as two 8-B {tag = step + 1, bf16 pair} words with agent-scope atomic stores, and the consumers sweep
+// data-tagged granules instead (MI355X guide Guideline 16 R2, payload <= 4 KB): the cell update is mapped one GATE per
+// lane (quad = unit: the g = 0 lane gathers f / g / o by DPP), and even units publish their h pair as one 8-B
+// {tag = step + 1, bf16 pair} word with an agent-scope atomic store, and the consumers sweep
 // the granules until every tag matches -- one fabric round trip per step instead of drain + counter + poll +
 // slab load.  The granule region (the first TAG_BYTES of the workspace) starts zeroed and every call leaves it
 // zeroed (the last workgroup to finish resets it), so a tag can only match a value of the current call.
@@ -55,8 +56,17 @@ STZS_DEV unsigned poll_ge(gu32* ctr, unsigned target, gu32* err, gu32* status, u
     return 1;
 }
 
-STZS_DEV float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-STZS_DEV float fast_tanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
+// gate activations and the cell update with every rounding pinned (no contraction choice left to hipcc): the
+// batch-1 cell map below computes them in other lanes and in another order than the counter form, and both must give
+// the same bits (a batch of 1 == the same utterance inside a larger batch, test_latency_engine_batch_invariant)
+STZS_DEV float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(__fadd_rn(1.f, __expf(-x))); }
+STZS_DEV float fast_tanh(float x) { return fmaf(-2.f, __builtin_amdgcn_rcpf(__fadd_rn(1.f, __expf(2.f * x))), 1.f); }
+STZS_DEV float cell_c(float ig, float fg, float tg, float c) { return fmaf(fg, c, __fmul_rn(ig, tg)); }
+STZS_DEV float cell_h(float og, float c) { return __fmul_rn(og, fast_tanh(c)); }
+template <int CTRL>
+STZS_DEV float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
@@ -110,6 +120,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     const bool cvalid = crow < nrows;
     const int cb = b0 + (cvalid ? crow : 0);
     float c[CPT];
+    float c1 = 0.f;  // the tagged (batch <= 2) cell map's one cell per quad
 #pragma unroll
     for (int j = 0; j < CPT; ++j) c[j] = 0.f;
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y);
@@ -127,9 +138,17 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         const int t = dir == 0 ? s : a.T - 1 - s;
         // gate input projections of this thread's cells (issued early, consumed after the MFMAs)
         float4 gx[4];
-        const float* G = a.gx + (long)cb * a.bsg + (long)t * a.ldg + dir * G4 + p * UNITS + cu0;
+        float gxs = 0.f;  // tagged (batch <= 2): this lane's one gate input (the batch-1 cell map below)
+        if (tagged) {
+            if (tid < nrows * 128) {
+                const int row = tid >> 7, u = (tid >> 2) & 31, g = tid & 3;
+                gxs = a.gx[(long)(b0 + row) * a.bsg + (long)t * a.ldg + dir * G4 + g * H + p * UNITS + u];
+            }
+        } else {
+            const float* G = a.gx + (long)cb * a.bsg + (long)t * a.ldg + dir * G4 + p * UNITS + cu0;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) gx[g] = *reinterpret_cast<const float4*>(G + g * H);
+            for (int g = 0; g < 4; ++g) gx[g] = *reinterpret_cast<const float4*>(G + g * H);
+        }
         // ---- wait for h_{s-1} from all P workgroups, stage it into the A tile ----
         if (s == 0) {
             for (int e = tid; e < NH * MROWS * hp / 8; e += 512) reinterpret_cast<uint4*>(As)[e] = make_uint4(0, 0, 0, 0);
@@ -214,6 +233,31 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         __syncthreads();
         PROF(3)
         // ---- cell update, publish h ----
+        if (tagged) {
+            // batch-1 cell map: lane (row, unit u, gate g) = tid (row 7 bits up, u = (tid >> 2) & 31, g = tid & 3)
+            // activates ONE gate (two transcendentals instead of the counter form's ten per cell chain), the quad's
+            // g = 0 lane gathers f / g / o by DPP and updates the cell; even units publish {tag, h_u, h_u+1} granules
+            if (tid < nrows * 128) {
+                const int row = tid >> 7, u = (tid >> 2) & 31, g = tid & 3;
+                const float pre = gs[row * gp + g * UNITS + u] + gxs;
+                const float act = g == 2 ? fast_tanh(pre) : fast_sigmoid(pre);
+                const float fg = dpp_f<0x55>(act), gt = dpp_f<0xAA>(act), og = dpp_f<0xFF>(act);  // quad lanes 1, 2, 3
+                c1 = cell_c(act, fg, gt, c1);  // (meaningful in the g = 0 lane)
+                const float h = cell_h(og, c1);
+                const float h1 = __shfl_down(h, 4, 64);  // unit u + 1's h (its g = 0 lane)
+                if (g == 0 && (u & 1) == 0) {
+                    const unsigned pr = pack2bf(h, h1);
+                    gu64* gp8 = gran + (s & 1) * TAG_ROWS * (H / 2) + row * (H / 2) + (p * UNITS + u) / 2;
+                    __hip_atomic_store(gp8, ((unsigned long long)(unsigned)(s + 1) << 32) | pr, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    *reinterpret_cast<unsigned*>(Y + (long)(b0 + row) * a.bsy + (long)t * a.ldy + dir * H + p * UNITS + u) = pr;
+                }
+            }
+            // no barrier here: the next step writes As only after every wave passed this step's post-MFMA barrier
+            // (its As reads are consumed), and gs only after the next post-staging barrier
+            PROF(5)
+            continue;
+        }
         float hv[CPT];
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
@@ -226,25 +270,11 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
                 hv[j] = og * tanhf(c[j]);
             } else {
                 const float ig = fast_sigmoid(gi), fg = fast_sigmoid(gf), og = fast_sigmoid(go);
-                c[j] = fg * c[j] + ig * fast_tanh(gg);
-                hv[j] = og * fast_tanh(c[j]);
+                c[j] = cell_c(ig, fg, fast_tanh(gg), c[j]);
+                hv[j] = cell_h(og, c[j]);
             }
         }
         const uint2 hb = make_uint2(pack2bf(hv[0], hv[1]), pack2bf(hv[2], hv[3]));
-        if (tagged) {
-            if (cvalid) {  // two {tag, bf16 pair} granules; the data is the signal
-                gu64* g = gran + (s & 1) * TAG_ROWS * (H / 2) + crow * (H / 2) + (p * UNITS + cu0) / 2;
-                const unsigned long long tg = (unsigned long long)(unsigned)(s + 1) << 32;
-                __hip_atomic_store(g, tg | hb.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(g + 1, tg | hb.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const long yo = (long)cb * a.bsy + (long)t * a.ldy + dir * H + p * UNITS + cu0;
-                *reinterpret_cast<uint2*>(Y + yo) = hb;
-            }
-            // no barrier here: the next step writes As only after every wave passed this step's post-MFMA
-            // barrier (its As reads are consumed), and gs only after the next post-staging barrier
-            PROF(5)
-            continue;
-        }
         if (cvalid) {
             const __attribute__((ext_vector_type(2))) unsigned int hw = {hb.x, hb.y};
             const int so = ((s & 1) * MROWS * NH * H + crow * NH * H + p * UNITS + cu0) * 2;

@@ -1028,7 +1028,7 @@ class StyleTTSZS:
                                          what=key + ".conv1")
         if bw.sc is not None:
             scb = self.act(key + ".sc", B, T, bw.dout, dt)
-            self.conv(bw.sc, x, scb, what=key + ".sc")
+            self.conv(bw.sc, x, scb, splitk=sk, what=key + ".sc")
             res = scb
         else:
             res = x

@@ -23,11 +23,15 @@ if "--build" in sys.argv:  # the whole library (conv.hip calls into the other ke
     objs = []
     tmp = os.path.join("/tmp", "gemmprof_build")
     os.makedirs(tmp, exist_ok=True)
-    for f in B.sources():
+    import concurrent.futures as cf
+
+    def one(f):
         o = os.path.join(tmp, os.path.basename(f) + ".o")
         subprocess.check_call([B.HIPCC] + B.FLAGS + B.FILE_FLAGS.get(os.path.basename(f), []) +
                               ["-DSTZS_GEMM_PROF", "-c", f, "-o", o])
-        objs.append(o)
+        return o
+    with cf.ThreadPoolExecutor(max_workers=8) as ex:
+        objs = list(ex.map(one, B.sources()))
     subprocess.check_call([B.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", SO])
     sys.exit(0)
 
@@ -91,12 +95,13 @@ for M in [int(v) for v in os.environ.get("M", "3200,6400").split(",")]:
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3
-        st = stamps.view(-1, 8)[:, :5].cpu()
-        st = st[(st != 0).all(dim=1)].double()  # workgroups that stamped all five points
+        st = stamps.view(-1, 8)[:, :7].cpu()
+        st = st[(st != 0).all(dim=1)].double()  # workgroups that stamped all seven points
         n = st.shape[0]
         # (s_memtime counters are per XCD and not aligned across XCDs: only differences within a workgroup are used)
         ph = {"fill (start -> K-step 0 landed)": st[:, 1] - st[:, 0], "K loop": st[:, 2] - st[:, 1],
-              "epilogue issue": st[:, 3] - st[:, 2], "store drain": st[:, 4] - st[:, 3],
+              "epi: accumulators -> LDS": st[:, 5] - st[:, 2], "epi: bias / gate -> LDS": st[:, 6] - st[:, 5],
+              "epi: vector loop (issue)": st[:, 3] - st[:, 6], "store drain": st[:, 4] - st[:, 3],
               "workgroup total": st[:, 4] - st[:, 0]}
         print(f"{name:5s} M={M} K={K} N={N}: {n} workgroups stamped, launch {us:.1f} us (events)", flush=True)
         for k, v in ph.items():
