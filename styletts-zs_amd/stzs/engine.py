@@ -378,6 +378,7 @@ class StyleTTSZS:
                 a.splitk_ctr = self._counters("rows_ctr", nb // (rows * 16)).data_ptr()
             splitk = 0
         if a.flags & 8:  # LDS-DMA GEMM: the slices split the K-steps (a function of K only: batch invariance holds)
+            splitk = min(splitk, 4)  # (gemm_glds takes 2 or 4 slices)
             while splitk > 1 and (cw.ci_pad // 32) % splitk:
                 splitk //= 2
         elif splitk > 1:  # conv_mfma: the slices split the input-channel chunks (2..8, at most one slice per chunk)

@@ -1,7 +1,5 @@
-# r04_j: batch-1 LSTM cell map (A/B probe + tests), latency engine block split-K 0 / 4 / 8, gemm_glds epilogue stamps
+# r04_j (part 2): latency engine block split-K 0 / 4 / 8, gemm_glds epilogue stamps, latency trace
 mkdir -p gpurun_out
-(B=1 LSTM_PROF_SO=liblstmprof.so timeout -k 10 60 python -u tools/probe/lstm_prof.py && B=1 LSTM_PROF_SO=liblstmprof_b1.so LSTM_REF_SO=liblstmprof.so timeout -k 10 60 python -u tools/probe/lstm_prof.py && B=2 LSTM_PROF_SO=liblstmprof_b1.so LSTM_REF_SO=liblstmprof.so timeout -k 10 60 python -u tools/probe/lstm_prof.py) > gpurun_out/r04_j_lstm_ab.log 2>&1 || exit $?
-timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_ops.py tests/test_gpu_configs.py tests/test_gpu_gemm_xcd.py tests/test_gpu_abi_generic.py tests/test_gpu_torch_ops.py -k "lstm or latency or splitk or configs1 or bilstm" > gpurun_out/r04_j_tests.log 2>&1 || exit $?
 (for v in 0 4 8 0 4 8; do STZS_BLK_SPLITK=$v timeout -k 10 100 python tools/lat_probe.py || exit $?; done) > gpurun_out/r04_j_blk_ab.log 2>&1 || exit $?
 timeout -k 10 150 python -u tools/gemm_phase.py > gpurun_out/r04_j_gemm_phase.log 2>&1 || exit $?
 export TMPDIR=/tmp
