@@ -32,6 +32,20 @@ constexpr int EP_PITCH = BCO + 4;         // fp32 epilogue row pitch (floats)
 
 STZS_DEV int gswz(int r) { return (0x1320 >> (((r >> 2) & 3) * 4)) & 3; }
 
+// flat row R -> (utterance q, step R - q T) without a 64-bit integer division (hipcc expands `long / int` into a
+// ~100-instruction routine: the FLAT epilogue ran one per output row vector, r04 gemm_phase).  For R < 2^22 the float
+// quotient R (1 / T) is within one of R / T and one correction step makes it exact (as csrc/rows.hip); beyond, the
+// plain division.  `small` must be uniform (nR < 2^22).
+STZS_DEV long rowdiv(long R, int T, float invT, bool small) {
+    if (small) {
+        int q = (int)((float)(int)R * invT);
+        const int r = (int)R - q * T;
+        q += r < 0 ? -1 : (r >= T ? 1 : 0);
+        return q;
+    }
+    return R / T;
+}
+
 template <int PACT>
 STZS_DEV float pro_act(float x, float slope, float alpha, float ialpha) {
     if constexpr (PACT == STZS_ACT_SNAKE) {
@@ -107,6 +121,8 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
     TOut* Y = reinterpret_cast<TOut*>(a.y);
     const int ncol = a.ups > 0 ? a.ups * a.Co : a.Co;
     const long nrows_flat = (long)a.B * a.T_out;
+    const bool small_rows = nrows_flat + BTM < (1L << 22);
+    const float invTo = 1.f / (float)a.T_out;
     const long t_hi = a.ups > 0 ? (long)a.T_final + a.refl - 1 : (long)a.T_out - 1;
     const int cv = tid & 15;
     const int n = by * BCO + cv * 8;
@@ -164,7 +180,7 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
             if (FLAT) {
                 const long Rr = row0 + tl;
                 ok = ok && Rr < nrows_flat;
-                bb = Rr / a.T_out;
+                bb = rowdiv(Rr, a.T_out, invTo, small_rows);
                 t = Rr - bb * a.T_out;
             } else {
                 bb = bq;
@@ -407,6 +423,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         const int rstep = NTHR >> lv;
         RawT raw[SB];
         bool okv[SB];
+        const float invTi = 1.f / (float)a.T_in;  // (FLAT rows -> utterance, rowdiv)
         auto issue = [&](int v0) {
             const int rb = (v0 >> lv) + (tid >> lv);
 #pragma unroll
@@ -419,7 +436,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
                     const long nR = (long)a.B * a.T_in;
                     ok = ok && R < nR;
                     R = R < nR ? R : nR - 1;
-                    const long bb = R / a.T_in;
+                    const long bb = rowdiv(R, a.T_in, invTi, nR < (1L << 22));
                     off = bb * a.bsx + (R - bb * a.T_in) * a.ldx + cic0;
                 } else {
                     int tin = t0 * a.stride - a.pad + r;
@@ -966,6 +983,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3(const stzs_conv_args a) {
     const bf16_t* Wh = reinterpret_cast<const bf16_t*>(a.w) + (long)blockIdx.y * NK * (BCO * 32);
     const TIn* X = reinterpret_cast<const TIn*>(a.x) + (FLAT ? 0 : (long)bq * a.bsx);
     const long nR = (long)a.B * a.T_in;
+    const float invTi = 1.f / (float)a.T_in;  // (FLAT rows -> utterance, rowdiv)
     auto fill = [&](int k) {
         const bf16_t* src = Wh + (long)k * (BCO * 32) + wave * 1024 + lane * 8;
         unsigned char* dst = ring + (k % NSLOT) * XSLOT + wave * 2048;
@@ -1023,7 +1041,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3(const stzs_conv_args a) {
             bool rok;
             if (FLAT) {
                 const long R = row0 + r;
-                const long bb = R / a.T_in;
+                const long bb = rowdiv(R, a.T_in, invTi, nR + BT < (1L << 22));
                 rok = R < nR;
                 off = bb * a.bsx + (R - bb * a.T_in) * a.ldx;
             } else {

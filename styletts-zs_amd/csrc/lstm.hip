@@ -78,23 +78,12 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     const int H = a.H, G4 = 4 * H;
     const int hp = H + 8;
     constexpr int NH = PR ? 2 : 1;  // slab row = hi[H] (| lo[H])
-    // KS2 (bf16, H >= 64): the 8 waves are (gate, K half): each wave runs half of the K-steps for every row tile and
-    // the two halves' gate partials meet in two slabs, summed by the cell update (half the dependent MFMA chain per
-    // wave at batch 1, where one row tile leaves the second wave of each gate idle otherwise); else (precise, H = 32)
-    // two waves per gate split the row tiles
-    constexpr bool KS2 = !PR && NKS >= 2;
-    constexpr int NKW = KS2 ? NKS / 2 : NKS;  // K-steps per wave
     bf16_t* As = reinterpret_cast<bf16_t*>(smem);                                   // [NH][64][hp]
-    float* gs = reinterpret_cast<float*>(smem + ((NH * MROWS * hp * 2 + 15) & ~15)); // [KS2 ? 2 : 1][64][4*UNITS + 4]
+    float* gs = reinterpret_cast<float*>(smem + ((NH * MROWS * hp * 2 + 15) & ~15)); // [64][4*UNITS + 4]
     __shared__ int s_ok, s_last;
     const int gp = 4 * UNITS + 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int gate = wave & 3, mh = wave >> 2;  // (KS2: mh = the K half)
-    // a gate pre-activation summed over the K halves (half 0 first), before the input projection is added
-    auto gsum = [&](int i) -> float {
-        if constexpr (KS2) return gs[i] + gs[MROWS * gp + i];
-        else return gs[i];
-    };
+    const int gate = wave & 3, mh = wave >> 2;  // 8 waves: two per gate, each half of the row tiles
     const int p = blockIdx.x, dir = blockIdx.y, grp = blockIdx.z;
     const int P = H / UNITS;
     const int b0 = grp * MROWS;
@@ -114,15 +103,14 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
 
     // W_hh^T fragments of this wave's gate (g = wave) for the workgroup's 32 units, in registers
     const bf16_t* Wd = reinterpret_cast<const bf16_t*>(a.whhT) + (long)dir * (G4 / 16) * NKS * 512;
-    bf16x8 bw[2][NKW], bwl[PR ? 2 : 1][PR ? NKS : 1];
+    bf16x8 bw[2][NKS], bwl[PR ? 2 : 1][PR ? NKS : 1];
     const long lo_off = (long)2 * (G4 / 16) * NKS * 512;  // PR: the lo fragments follow both directions' hi ones
-    const int kw0 = KS2 ? mh * NKW : 0;  // this wave's first K-step
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int ct = (gate * H + p * UNITS) / 16 + c;
 #pragma unroll
-        for (int ks = 0; ks < NKW; ++ks) {
-            bw[c][ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)ct * NKS + kw0 + ks) * 512 + lane * 8);
+        for (int ks = 0; ks < NKS; ++ks) {
+            bw[c][ks] = *reinterpret_cast<const bf16x8*>(Wd + ((long)ct * NKS + ks) * 512 + lane * 8);
             if constexpr (PR) bwl[c][ks] = *reinterpret_cast<const bf16x8*>(Wd + lo_off + ((long)ct * NKS + ks) * 512 + lane * 8);
         }
     }
@@ -216,15 +204,14 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         __syncthreads();
         PROF(2)
         // ---- gates of this wave's gate g = wave for all rows: [64 x 32 units] ----
-        float* gsw = gs + (KS2 ? mh * MROWS * gp : 0);  // this wave's slab
 #pragma unroll
-        for (int mi = 0; mi < (KS2 ? 4 : 2); ++mi) {
-            const int mt = KS2 ? mi : mh * 2 + mi;
+        for (int mi = 0; mi < 2; ++mi) {
+            const int mt = mh * 2 + mi;
             if (mt >= nmt) break;
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int ks = 0; ks < NKW; ++ks) {
-                const int ao = (mt * 16 + (lane & 15)) * hp + (kw0 + ks) * 32 + 8 * (lane >> 4);
+            for (int ks = 0; ks < NKS; ++ks) {
+                const int ao = (mt * 16 + (lane & 15)) * hp + ks * 32 + 8 * (lane >> 4);
                 const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + ao);
                 if constexpr (PR) {  // h_lo W_hi + h_hi W_lo + h_hi W_hi (small terms first)
                     const bf16x8 afl = *reinterpret_cast<const bf16x8*>(As + MROWS * hp + ao);
@@ -239,8 +226,8 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = mt * 16 + (lane >> 4) * 4 + r;
-                gsw[row * gp + gate * UNITS + (lane & 15)] = acc0[r];
-                gsw[row * gp + gate * UNITS + 16 + (lane & 15)] = acc1[r];
+                gs[row * gp + gate * UNITS + (lane & 15)] = acc0[r];
+                gs[row * gp + gate * UNITS + 16 + (lane & 15)] = acc1[r];
             }
         }
         __syncthreads();
@@ -252,7 +239,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
             // g = 0 lane gathers f / g / o by DPP and updates the cell; even units publish {tag, h_u, h_u+1} granules
             if (tid < nrows * 128) {
                 const int row = tid >> 7, u = (tid >> 2) & 31, g = tid & 3;
-                const float pre = gsum(row * gp + g * UNITS + u) + gxs;
+                const float pre = gs[row * gp + g * UNITS + u] + gxs;
                 const float act = g == 2 ? fast_tanh(pre) : fast_sigmoid(pre);
                 const float fg = dpp_f<0x55>(act), gt = dpp_f<0xAA>(act), og = dpp_f<0xFF>(act);  // quad lanes 1, 2, 3
                 c1 = cell_c(act, fg, gt, c1);  // (meaningful in the g = 0 lane)
@@ -274,9 +261,9 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         float hv[CPT];
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
-            const int gr = crow * gp + cu0 + j;
-            const float gi = gsum(gr) + gx[0][j], gf = gsum(gr + UNITS) + gx[1][j], gg = gsum(gr + 2 * UNITS) + gx[2][j],
-                        go = gsum(gr + 3 * UNITS) + gx[3][j];
+            const float* gr = gs + crow * gp + cu0 + j;
+            const float gi = gr[0] + gx[0][j], gf = gr[UNITS] + gx[1][j], gg = gr[2 * UNITS] + gx[2][j],
+                        go = gr[3 * UNITS] + gx[3][j];
             if constexpr (PR) {
                 const float ig = acc_sigmoid(gi), fg = acc_sigmoid(gf), og = acc_sigmoid(go);
                 c[j] = fg * c[j] + ig * tanhf(gg);
@@ -386,9 +373,7 @@ extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     if (a->precise && (a->ldy % 4 || a->bsy % 4)) return STZS_ESHAPE;
     const int hp = a->H + 8;
     const int nh = a->precise ? 2 : 1;
-    // A tile(s) + the gate slab(s): two (one per K half) in the bf16 form when H >= 64 (lstm_xchg KS2)
-    const int nslab = (!a->precise && a->H >= 64) ? 2 : 1;
-    const size_t lds = ((nh * MROWS * hp * 2 + 15) & ~15) + (size_t)nslab * MROWS * (4 * UNITS + 4) * 4;
+    const size_t lds = ((nh * MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4;
     dim3 grid(P, a->ndir, groups);
     switch (a->H / 32) {
 #define STZS_LSTM_CASE(n)                                                                                   \

@@ -54,7 +54,7 @@ LATENCY_TE_SPLITK = 4
 # split-K slices of the decoder / predictor AdaIN-block convs (their generic-layout copies, BlkW.conv1s / conv2s) in
 # the batch-1 latency engine: at 200-400 frames a decoder conv is 16 tiles x 108 K-steps on 16 CUs; 0 = off
 BLK_SPLITK = 0
-LATENCY_BLK_SPLITK = 4
+LATENCY_BLK_SPLITK = 8
 
 
 _ES = {L.F32: 4, L.BF16: 2, L.F8: 1}
