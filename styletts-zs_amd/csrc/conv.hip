@@ -641,7 +641,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
         const int r = o >> 6, p = (o >> 4) & 3;
         long R = row0 + r;
         R = R < nR ? R : nR - 1;
-        const long bb = R / a.T_in;
+        const long bb = rowdiv(R, a.T_in, 1.f / (float)a.T_in, nR < (1L << 22));
         asrc[i] = (bb * a.bsx + (R - bb * a.T_in) * a.ldx) * ESZ + ((p ^ gswz(r)) << 4);
     }
     auto fill = [&](int k) {
