@@ -171,7 +171,7 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
     for (int v0 = 0; v0 < BTM * (BCO / 8); v0 += EB * NTHR) {
         long pb[EB], pt[EB];
         bool pv[EB];
-        float rr[EB][8], ai[EB][8];
+        float rr[EB][8], ai[EB][8], gvv[EB][8];
 #pragma unroll
         for (int i = 0; i < EB; ++i) {
             const int tl = ((v0 + tid) >> 4) + i * (NTHR >> 4);
@@ -198,8 +198,19 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
             pt[i] = t;
             pv[i] = ok;
             if constexpr (VEC) {
-                if constexpr (HR) load8(Rp + bc * a.bsr + (tc / a.res_tdiv) * a.ldr + cc, rr[i]);
+                // (res_tdiv 1 but for the upsampling AdaIN blocks: a uniform test instead of a 64-bit division per row)
+                const long tr = a.res_tdiv == 1 ? tc : (long)((int)tc / a.res_tdiv);
+                if constexpr (HR) load8(Rp + bc * a.bsr + tr * a.ldr + cc, rr[i]);
                 if constexpr (HA) load8(AI + bc * a.bsa + tc * a.lda + cc, ai[i]);
+            }
+            if (FLAT && a.gate) {  // DiT gate of this row's utterance, in flight with the residual rows
+                const float* gp = a.gate + bc * a.gate_bs;
+                if (gate_vec && co + 8 <= a.Co) {
+                    load8(gp + co, gvv[i]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) gvv[i][j] = gp[min(co + j, a.Co - 1)];
+                }
             }
         }
 #pragma unroll
@@ -207,22 +218,13 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
             if (!pv[i]) continue;
             const int tl = ((v0 + tid) >> 4) + i * (NTHR >> 4);
             const long bb = pb[i], t = pt[i];
-            float u[8], gv[8];
-            if (FLAT && a.gate) {  // DiT gate of this row's utterance: two 16-B loads when aligned
-                const float* gp = a.gate + bb * a.gate_bs;
-                if (gate_vec && co + 8 <= a.Co) {
-                    load8(gp + co, gv);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) gv[j] = gp[min(co + j, a.Co - 1)];
-                }
-            }
+            float u[8];
             const float* er = ep + tl * EP_PITCH + cv * 8;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 float x = epi_act<EACT>(er[j] + kb[j], a.epi_slope);
                 if (FLAT) {
-                    if (a.gate) x *= gv[j];
+                    if (a.gate) x *= gvv[i][j];
                 } else {
                     x *= kg[j];
                 }

@@ -32,7 +32,8 @@ if "--build" in sys.argv:  # the whole library (conv.hip calls into the other ke
         return o
     with cf.ThreadPoolExecutor(max_workers=8) as ex:
         objs = list(ex.map(one, B.sources()))
-    subprocess.check_call([B.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", SO])
+    subprocess.check_call([B.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", SO + ".tmp"])
+    os.replace(SO + ".tmp", SO)  # (a copy of the tree never sees a partial library)
     sys.exit(0)
 
 import torch  # noqa: E402
