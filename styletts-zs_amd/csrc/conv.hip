@@ -320,9 +320,22 @@ STZS_DEV void epilogue_act(const stzs_conv_args& a, const float* ep, const float
 
 template <int BTM>
 STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK);
-template <typename TOut, bool FLAT, int BTM = BT>
+// EP: the epilogue variant compiled into the calling kernel.  -1: all of them behind runtime tests (the conv kernels);
+// 0..15: ONE vectorised variant, HR = bit 0, HA = bit 1, activation index (ep_act) = bits 2-3 (the GEMM kernels:
+// with all twenty variants inlined a gemm_glds instance was ~73 k instructions and its epilogue ran from a cold
+// instruction cache)
+template <typename TOut, bool FLAT, int BTM = BT, int EP = -1>
 STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0,
                      int by);
+constexpr int ep_act(int i) { return i == 0 ? STZS_ACT_NONE : (i == 1 ? STZS_ACT_GELU : (i == 2 ? STZS_ACT_SILU : STZS_ACT_LEAKY)); }
+// the EP index of a launch (-1: no specialised variant)
+inline int ep_index(const stzs_conv_args& a, bool vec) {
+    if (!vec) return -1;
+    const int ai = a.epi_act == STZS_ACT_NONE ? 0 : a.epi_act == STZS_ACT_GELU ? 1 : a.epi_act == STZS_ACT_SILU ? 2
+                 : a.epi_act == STZS_ACT_LEAKY ? 3 : -1;
+    if (ai < 0) return -1;
+    return (a.res ? 1 : 0) | (a.acc_in ? 2 : 0) | (ai << 2);
+}
 
 // 8-wide vector epilogue legal (every output / residual / accumulate row 16-B aligned)
 __host__ __device__ inline bool epi_vec(const stzs_conv_args& a) {
@@ -539,7 +552,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
 #else
 #define GPROF_E(i)
 #endif
-template <typename TOut, bool FLAT, int BTM>
+template <typename TOut, bool FLAT, int BTM, int EP>
 STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int bq, int t0, long row0,
                      int by) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -565,7 +578,9 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigne
     }
     __syncthreads();
     GPROF_E(6)
-    if (epi_vec(a)) {
+    if constexpr (EP >= 0) {
+        epilogue<TOut, FLAT, true, (EP & 1) != 0, (EP & 2) != 0, ep_act(EP >> 2), BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
+    } else if (epi_vec(a)) {
         if (a.res && a.acc_in) epilogue_act<TOut, FLAT, true, true, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
         else if (a.res) epilogue_act<TOut, FLAT, true, true, false, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
         else if (a.acc_in) epilogue_act<TOut, FLAT, true, false, true, BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
@@ -609,7 +624,7 @@ STZS_DEV bool splitk_combine(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4],
 #else
 #define GPROF(i)
 #endif
-template <typename TOut, int BTM, bool F8, int SK = 1>
+template <typename TOut, int BTM, bool F8, int SK = 1, int EP = -1>
 __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     GPROF(0)
     constexpr int MT = BTM / 32;           // 16-row tiles per wave (2 x 2 waves)
@@ -747,7 +762,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
     if constexpr (SK > 1) {
         if (!splitk_combine<BTM, SK>(a, acc, smem)) return;
     }
-    finish<TOut, true, BTM>(a, acc, smem, 0, 0, row0, by);
+    finish<TOut, true, BTM, EP>(a, acc, smem, 0, 0, row0, by);
 #ifdef STZS_GEMM_PROF
     GPROF(3)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1125,6 +1140,18 @@ size_t lds_bytes(int rows_in, int cic) {
     return main > epi ? main : epi;
 }
 
+// the gemm_glds instance with the launch's epilogue variant compiled in (EP, finish)
+template <typename TOut, int BTM, bool F8, int SK>
+void (*pick_gemm(int ep))(stzs_conv_args) {
+    switch (ep) {
+#define STZS_EPK(e) case e: return gemm_glds<TOut, BTM, F8, SK, e>;
+        STZS_EPK(0) STZS_EPK(1) STZS_EPK(2) STZS_EPK(3) STZS_EPK(4) STZS_EPK(5) STZS_EPK(6) STZS_EPK(7)
+        STZS_EPK(8) STZS_EPK(9) STZS_EPK(10) STZS_EPK(11) STZS_EPK(12) STZS_EPK(13) STZS_EPK(14) STZS_EPK(15)
+#undef STZS_EPK
+        default: return gemm_glds<TOut, BTM, F8, SK, -1>;
+    }
+}
+
 template <typename TIn, typename TOut, bool F8 = false>
 int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     const bool flat = (a.ks == 1 && a.stride == 1 && a.pad == 0 && a.ups == 0 && a.pro_mode == STZS_PRO_NONE &&
@@ -1144,13 +1171,14 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
         size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
         const size_t lr = 4 * (size_t)(small ? gslot<64>() : gslot<128>());
         lg = lg > lr ? lg : lr;
-        auto kg = small ? gemm_glds<TOut, 64, F8> : gemm_glds<TOut, 128, F8>;
+        const int ep = ep_index(a, epi_vec(a));
+        auto kg = small ? pick_gemm<TOut, 64, F8, 1>(ep) : pick_gemm<TOut, 128, F8, 1>(ep);
         if (a.splitk > 1) {  // split-K: 64-row tiles at every row count (the K order must not depend on M)
             const int NK = a.ci_pad / 32;
             if (F8 || (a.splitk != 2 && a.splitk != 4) || NK % a.splitk || !a.splitk_ws || !a.splitk_ctr ||
                 !stzs_aligned(a.splitk_ws, 16) || !stzs_aligned(a.splitk_ctr, 4))
                 return STZS_EINVAL;
-            if constexpr (!F8) kg = a.splitk == 2 ? gemm_glds<TOut, 64, false, 2> : gemm_glds<TOut, 64, false, 4>;
+            if constexpr (!F8) kg = a.splitk == 2 ? pick_gemm<TOut, 64, false, 2>(ep) : pick_gemm<TOut, 64, false, 4>(ep);
             small = true;
             grid.z = (unsigned)a.splitk;
             lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
