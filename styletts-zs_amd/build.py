@@ -28,10 +28,11 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=
 # harmonic-source STFT built with them failed 104 of 512 swept two-shard passes, the same code with only its 7 swapped
 # operands pre-swapped by two v_mov_b32 (everything else still packed) 0 of 512 (tools/pk_bisect.py,
 # profiles/r04_*_pk_bisect*.log).  tests/test_isa_audit.py fails the build if any kernel of the
-# library contains the pattern; conv.hip's epilogues / prologues and source.hip's STFT sums are where hipcc made it
+# library contains the pattern; the conv / GEMM epilogues and prologues (conv.hip, gemm.hip, convx.hip: one file until r04)
+# and source.hip's STFT sums are where hipcc made it
 # (and the r04 warp-specialised MRF conv's staging transform, since removed).
 NO_PK = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
-FILE_FLAGS = {"source.hip": NO_PK, "conv.hip": NO_PK}
+FILE_FLAGS = {"source.hip": NO_PK, "conv.hip": NO_PK, "gemm.hip": NO_PK, "convx.hip": NO_PK}
 
 
 def sources():
