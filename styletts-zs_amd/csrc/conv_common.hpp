@@ -372,7 +372,7 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigne
                 ep[(wt * (BTM / 2) + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
     if (a.flags & 4) return;
     GPROF_E(5)
-    float* c_bias = ep + BT * EP_PITCH;       // [BCO] bias, [BCO] gate (conv mode: one utterance)
+    float* c_bias = ep + BTM * EP_PITCH;      // [BCO] bias, [BCO] gate (conv mode: one utterance)
     float* c_gate = c_bias + BCO;
     if (tid < BCO) {
         const int n = by * BCO + tid;

@@ -37,8 +37,15 @@ STZS_DEV bool splitk_combine(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4],
 #else
 #define GPROF(i)
 #endif
+// LDS of one workgroup: the K-step ring (4 slots) aliased with the epilogue's fp32 tile + bias / gate rows (a linear
+// has no channel statistics).  64-row tiles: 48 KB -> three workgroups per CU (<= 136 VGPRs); 128-row: 68.6 KB -> two.
+template <int BTM>
+constexpr size_t gemm_lds() {
+    const size_t ring = 4 * (size_t)gslot<BTM>(), epi = (size_t)BTM * EP_PITCH * 4 + 2 * BCO * 4;
+    return ring > epi ? ring : epi;
+}
 template <typename TOut, int BTM, bool F8, int SK = 1, int EP = -1>
-__global__ __launch_bounds__(NTHR, 2) void gemm_glds(const stzs_conv_args a) {
+__global__ __launch_bounds__(NTHR, BTM == 64 ? 3 : 2) void gemm_glds(const stzs_conv_args a) {
     GPROF(0)
     constexpr int MT = BTM / 32;           // 16-row tiles per wave (2 x 2 waves)
     constexpr int GS = gslot<BTM>();
@@ -247,12 +254,18 @@ void (*pick_gemm(int ep))(stzs_conv_args) {
 template <typename TOut, bool F8>
 int gemm_launch(const stzs_conv_args& a, hipStream_t s) {
     dim3 grid((unsigned)(((long)a.B * a.T_out + BT - 1) / BT), a.co_pad / BCO);
-    // 64-row tiles when 128-row tiles would leave the GPU under-filled (< 2 workgroups per CU)
-    const int n_cu = stzs_cu_count();
-    bool small = (long)grid.x * grid.y < 2L * n_cu;
-    size_t lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
-    const size_t lr = 4 * (size_t)(small ? gslot<64>() : gslot<128>());
-    lg = lg > lr ? lg : lr;
+    // tile height by wave quantisation: 128-row tiles run two workgroups per CU, 64-row tiles three; a 64-row tile
+    // costs ~0.6 of a 128-row one (the fill and the epilogue do not halve).  STZS_GEMM_TILE=64|128 forces one.
+    const long n_cu = stzs_cu_count();
+    const long n128 = (long)grid.x * grid.y, n64 = (((long)a.B * a.T_out + 63) / 64) * grid.y;
+    const long r128 = (n128 + 2 * n_cu - 1) / (2 * n_cu), r64 = (n64 + 3 * n_cu - 1) / (3 * n_cu);
+    bool small = 6 * r64 < 10 * r128;
+    static const int force = [] {
+        const char* e = getenv("STZS_GEMM_TILE");
+        return e ? atoi(e) : 0;
+    }();
+    if (force == 64 || force == 128) small = force == 64;
+    size_t lg = small ? gemm_lds<64>() : gemm_lds<128>();
     const int ep = ep_index(a, epi_vec(a));
     auto kg = small ? pick_gemm<TOut, 64, F8, 1>(ep) : pick_gemm<TOut, 128, F8, 1>(ep);
     if (a.splitk > 1) {  // split-K: 64-row tiles at every row count (the K order must not depend on M)
@@ -263,8 +276,7 @@ int gemm_launch(const stzs_conv_args& a, hipStream_t s) {
         if constexpr (!F8) kg = a.splitk == 2 ? pick_gemm<TOut, 64, false, 2>(ep) : pick_gemm<TOut, 64, false, 4>(ep);
         small = true;
         grid.z = (unsigned)a.splitk;
-        lg = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
-        lg = lg > 4 * (size_t)gslot<64>() ? lg : 4 * (size_t)gslot<64>();
+        lg = gemm_lds<64>();
     }
     if (small) grid.x = (unsigned)(((long)a.B * a.T_out + 63) / 64);
     (void)hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);

@@ -10,10 +10,11 @@ namespace stzs_ln {
 template <int MAXV>
 STZS_DEV void store_f8_row(f8_t* Y, float (&v)[MAXV][8], int nv, int lane, float amax, float* scale);
 
-// normalise, modulate, activate and store row r whose values are in registers (lane holds the 8-value
-// vectors lane + 64 i)
-template <typename TO, int MAXV>
-STZS_DEV void ln_row_finish(const stzs_rowln_args& a, long r, int lane, float (&v)[MAXV][8]) {
+// the LayerNorm of one register-resident row in three steps (lane holds the 8-value vectors lane + 64 i): statistics,
+// the modulation vectors of the row's group, the finished vectors -- stzs_row_layernorm runs them back to back,
+// csrc/lnrows.hip takes the statistics of many rows before their (shared) modulation vectors arrive.  Same arithmetic.
+template <int MAXV>
+STZS_DEV void ln_row_stats(const stzs_rowln_args& a, int lane, const float (&v)[MAXV][8], float& mu, float& rstd) {
     const int nv = a.C >> 3;
     float s = 0.f;
 #pragma unroll
@@ -21,7 +22,7 @@ STZS_DEV void ln_row_finish(const stzs_rowln_args& a, long r, int lane, float (&
         if (lane + i * 64 < nv)
 #pragma unroll
             for (int j = 0; j < 8; ++j) s += v[i][j];
-    const float mu = wave_sum(s) / a.C;
+    mu = wave_sum(s) / a.C;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
@@ -34,37 +35,66 @@ STZS_DEV void ln_row_finish(const stzs_rowln_args& a, long r, int lane, float (&
             }
         }
     }
-    const float rstd = 1.f / sqrtf(wave_sum(q) / a.C + a.eps);
-    const long grp = r / a.gdiv;
-    TO* Y = reinterpret_cast<TO*>(a.y) + r * a.ldy;
-    // modulation rows as 32-B vectors (gs, bs and the bases are multiples of 8 floats: checked on the host)
-    const float* Gr = a.G ? a.G + grp * a.gs : nullptr;
-    const float* Br = a.Bt ? a.Bt + grp * a.bs : nullptr;
-    constexpr bool F8 = sizeof(TO) == 1;
-    float amax = 0.f;
+    rstd = 1.f / sqrtf(wave_sum(q) / a.C + a.eps);
+}
+
+// modulation vectors (G, Bt rows of group grp) of this lane's channel vectors; absent ones are left unset
+template <int MAXV>
+STZS_DEV void ln_mod_load(const stzs_rowln_args& a, long grp, int lane, float (&g)[MAXV][8], float (&bt)[MAXV][8]) {
+    const int nv = a.C >> 3;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
         const int vi = lane + i * 64;
         if (vi < nv) {
-            float g[8], bt[8], o[8];
-            if (Gr) load8(Gr + vi * 8, g);
-            if (Br) load8(Br + vi * 8, bt);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float gg = a.gadd + (Gr ? g[j] : 0.f);
-                o[j] = act_apply(a.act, (v[i][j] - mu) * rstd * gg + (Br ? bt[j] : 0.f), a.slope, 1.f);
-            }
-            if constexpr (F8) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    v[i][j] = o[j];
-                    amax = fmaxf(amax, fabsf(o[j]));
-                }
-            } else {
-                store8(Y + vi * 8, o);
-            }
+            if (a.G) load8(a.G + grp * a.gs + vi * 8, g[i]);
+            if (a.Bt) load8(a.Bt + grp * a.bs + vi * 8, bt[i]);
         }
     }
+}
+
+// put(i, vi, o) receives each finished 8-value vector (register slot i, vector vi): the global store of
+// stzs_row_layernorm, or csrc/lnrows.hip's LDS operand image
+template <int MAXV, typename Put>
+STZS_DEV void ln_row_out(const stzs_rowln_args& a, int lane, const float (&v)[MAXV][8], float mu, float rstd,
+                         const float (&g)[MAXV][8], const float (&bt)[MAXV][8], Put put) {
+    const int nv = a.C >> 3;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        const int vi = lane + i * 64;
+        if (vi < nv) {
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float gg = a.gadd + (a.G ? g[i][j] : 0.f);
+                o[j] = act_apply(a.act, (v[i][j] - mu) * rstd * gg + (a.Bt ? bt[i][j] : 0.f), a.slope, 1.f);
+            }
+            put(i, vi, o);
+        }
+    }
+}
+
+// normalise, modulate, activate and store row r whose values are in registers (lane holds the 8-value
+// vectors lane + 64 i)
+template <typename TO, int MAXV>
+STZS_DEV void ln_row_finish(const stzs_rowln_args& a, long r, int lane, float (&v)[MAXV][8]) {
+    const int nv = a.C >> 3;
+    TO* Y = reinterpret_cast<TO*>(a.y) + r * a.ldy;
+    // (modulation rows as 32-B vectors: gs, bs and the bases are multiples of 8 floats, checked on the host)
+    constexpr bool F8 = sizeof(TO) == 1;
+    float amax = 0.f, mu, rstd, g[MAXV][8], bt[MAXV][8];
+    ln_row_stats<MAXV>(a, lane, v, mu, rstd);
+    ln_mod_load<MAXV>(a, r / a.gdiv, lane, g, bt);
+    ln_row_out<MAXV>(a, lane, v, mu, rstd, g, bt, [&](int i, int vi, const float* o) {
+        if constexpr (F8) {  // (slot i was consumed above: overwritten with its result)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                v[i][j] = o[j];
+                amax = fmaxf(amax, fabsf(o[j]));
+            }
+        } else {
+            store8(Y + vi * 8, o);
+        }
+    });
     if constexpr (F8) store_f8_row(reinterpret_cast<f8_t*>(Y), v, nv, lane, amax, a.y_scale + r);
 }
 

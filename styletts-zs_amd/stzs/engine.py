@@ -209,6 +209,9 @@ class StyleTTSZS:
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
         # STZS_SMALL_ROWS=0 turns it off.
         self.small_rows = os.environ.get("STZS_SMALL_ROWS", "1") != "0"
+        # with the denoiser linears on the small-M rows form (dn_rows): each adaLN / affine LayerNorm fused into the
+        # one linear that reads it (stzs_ln_linear, csrc/lnrows.hip) instead of its own launch.  STZS_LN_FUSE=0: off
+        self.ln_fuse = os.environ.get("STZS_LN_FUSE", "1") != "0"
         # the last generator stage's noise conv fused into its ConvTranspose (bf16 engines); STZS_UPS_NOISE=0: off
         self.ups_noise_fused = os.environ.get("STZS_UPS_NOISE", "1") != "0"
         # the first stage's strided noise conv on super-rows of the harmonic source (register-direct kernel, bf16
@@ -303,13 +306,15 @@ class StyleTTSZS:
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
-             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, splitk=0, rows=0, attn=None,
-             what="conv"):
+             T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, pre_ln=None, splitk=0, rows=0,
+             attn=None, what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
         output fused into the conv epilogue (per-tile partials) + one small finalize launch.
         post_ln (stzs_rowln_args) / attn ((q, k, v, o) Acts): the LayerNorm / attention that consumes y, launched
         behind the linear.  (r03 also ran them, and the sampler's CFG + Euler step, inside the small-M linear's launch
-        by its last-arriving workgroups: bit-identical but slower at batch 1, removed in r04 -- DESIGN.md §5.)"""
+        by its last-arriving workgroups: bit-identical but slower at batch 1, removed in r04 -- DESIGN.md §5.)
+        pre_ln (stzs_rowln_args): the LayerNorm whose output x is, launched before the linear -- or, on the small-M
+        rows form, fused into it (stzs_ln_linear, csrc/lnrows.hip: the normalised rows never leave the chip)."""
         W = self.W
         a = L.ConvArgs()
         a.x, a.w, a.y = x.ptr, self._t(cw.w).data_ptr(), y.ptr
@@ -407,6 +412,15 @@ class StyleTTSZS:
                   self.buf(stats_key + ".r", (y.B, Cc), torch.float32))
         tm = self.timer
         launch = lambda: self.lib.stzs_conv1d(C.byref(a), self.stream())
+        fused = False
+        if pre_ln is not None:
+            nk = cw.ci_pad // 32
+            fused = bool(a.flags & L.CONV_ROWS) and a.splitk <= 1 and res is None and gate is None and \
+                st is None and pre_ln.C == cw.Ci == cw.ci_pad and nk in (4, 8, 16, 32) and pre_ln.out_dtype == L.BF16
+            if fused:
+                launch = lambda: self.lib.stzs_ln_linear(C.byref(a), C.byref(pre_ln), self.stream())
+            else:
+                self._call(self.lib.stzs_row_layernorm, pre_ln, what + ".ln", cost=_ln_cost(pre_ln))
         if tm is not None and (tm["all"] or what in tm["tags"]):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -423,7 +437,12 @@ class StyleTTSZS:
             opnd = lambda v: v.B * v.T * v.C * v.t.element_size() if v is not None else 0
             byt = x.B * x.T * x.C * x.t.element_size() + y.B * a.T_out * (cw.ups or 1) * cw.Co * y.t.element_size() + \
                 opnd(res) + opnd(acc_in) + wbytes
+            if fused:  # the LayerNorm's input rows instead of x
+                byt += pre_ln.R * pre_ln.C * (4 if pre_ln.in_dtype == L.F32 else 2) - x.B * x.T * x.C * x.t.element_size()
             tm["rec"].append((what, e0, e1, flops, byt, (cw.ks, dil, a.T_out, cw.Co), self.stage))
+        elif fused:
+            self.launches += 1
+            L.check(launch(), what)
         else:
             self._call(self.lib.stzs_conv1d, a, what)
         if post_ln is not None:  # the LayerNorm that consumes this linear's output (stzs_rowln_args)
@@ -825,7 +844,8 @@ class StyleTTSZS:
         else:
             ain, sin, sfx = an, None, ""
         # adaLN / LayerNorm rows of this step: ln1_l, ca_ln_l, ln2_l for every layer, then lnf; each one
-        # after the first is launched right behind the residual linear that produces its input (post_ln).
+        # after the first is launched right behind the residual linear that produces its input (post_ln), or on the
+        # rows form runs inside the linear that reads it (pre_ln, stzs_ln_linear).
         # (Fusing them into that linear's epilogue -- last-arriving tile of a row block, sc1 hand-off --
         # was tried: bit-identical but 1.6x slower at batch 1, the block's rows then normalise on one CU.)
         lns = []
@@ -838,31 +858,36 @@ class StyleTTSZS:
                                      y_scale=sin))
         fb = fmodx[0, i * R].data_ptr()
         lns.append(self._ln_args(h, an, G=fb + d * fsz, gs=2 * d, Bt=fb, bs=2 * d, gdiv=Ls))
-        self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, rows=rk.get("inp", 0), post_ln=lns[0], what="dn.in")
+        # on the rows form each LayerNorm runs inside the linear that reads it (pre_ln) instead of behind its producer
+        fl = bool(rk) and self.ln_fuse
+        post = lambda k: None if fl else lns[k]
+        pre = lambda k: lns[k] if fl else None
+        self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, rows=rk.get("inp", 0), post_ln=post(0), what="dn.in")
         sk = {} if (f8 or self.adt == torch.float32) else self.dn_splitk
         for l, lw in enumerate(W.dn_layers):
             mb = modx[l, i * R].data_ptr()
             self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, splitk=sk.get("qkv", 0), rows=rk.get("qkv", 0),
-                      attn=(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o), what="qkv")
+                      pre_ln=pre(3 * l), attn=(qkv.sl(0, d), qkv.sl(d, d), qkv.sl(2 * d, d), o), what="qkv")
             xo, so = (o8, s_o) if f8 else (o, None)
             if f8:
                 self.quant(o, o8, s_o)
             self.conv(lw["o" + sfx], xo, h, res=h, gate=mb + 2 * d * fsz, gate_bs=6 * d, x_scale=so,
-                      post_ln=lns[3 * l + 1], splitk=sk.get("o", 0), rows=rk.get("o", 0), what="sa_o")
+                      post_ln=post(3 * l + 1), splitk=sk.get("o", 0), rows=rk.get("o", 0), what="sa_o")
             self.conv(lw["q" + sfx], ain, q, x_scale=sin, splitk=sk.get("q", 0), rows=rk.get("q", 0),
-                      attn=(q, kv[l].sl(0, d), kv[l].sl(d, d), o), what="ca_q")
+                      pre_ln=pre(3 * l + 1), attn=(q, kv[l].sl(0, d), kv[l].sl(d, d), o), what="ca_q")
             if f8:
                 self.quant(o, o8, s_o)
-            self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=lns[3 * l + 2], splitk=sk.get("co", 0),
+            self.conv(lw["co" + sfx], xo, h, res=h, x_scale=so, post_ln=post(3 * l + 2), splitk=sk.get("co", 0),
                       rows=rk.get("co", 0), what="ca_o")
             self.conv(lw["ff1" + sfx], ain, ff, epi_act=L.ACT_GELU, x_scale=sin, splitk=sk.get("ff1", 0),
-                      rows=rk.get("ff1", 0), what="ff1")
+                      rows=rk.get("ff1", 0), pre_ln=pre(3 * l + 2), what="ff1")
             xf, sf = (ff8, s_ff) if f8 else (ff, None)
             if f8:
                 self.quant(ff, ff8, s_ff)
             self.conv(lw["ff2" + sfx], xf, h, res=h, gate=mb + 5 * d * fsz, gate_bs=6 * d, x_scale=sf,
-                      post_ln=lns[3 * l + 3], splitk=sk.get("ff2", 0), rows=rk.get("ff2", 0), what="ff2")
-        self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], rows=rk.get("out", 0), what="dn.out")
+                      post_ln=post(3 * l + 3), splitk=sk.get("ff2", 0), rows=rk.get("ff2", 0), what="ff2")
+        self.conv(W.dn_out, an, D, alpha=co["c_out"], acc_in=xa, beta=co["c_skip"], rows=rk.get("out", 0),
+                  pre_ln=pre(len(lns) - 1), what="dn.out")
 
     def _ln_args(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=0.0, y_scale=None):
         """stzs_rowln_args of a modulated LayerNorm x -> y (launched by stzs_row_layernorm behind the linear that

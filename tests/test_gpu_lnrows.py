@@ -1,0 +1,186 @@
+"""The LayerNorm-fed small-M linear (csrc/lnrows.hip, stzs_ln_linear): the batch-1 denoiser's adaLN / affine
+LayerNorms fused into the one linear that reads each.
+
+* the on-chip operand image is exactly stzs_row_layernorm's output: with an identity weight and fp32 output the fused
+  launch returns the unfused LayerNorm's bf16 rows bit for bit (MFMA of x * 1 + zeros is exact);
+* against torch fp32 on the unfused LayerNorm's bf16 rows for every denoiser shape (qkv, the cross-attention query,
+  GELU ffn1, dn.out with alpha / acc_in / beta): max-rel 1e-2 for bf16 outputs, 1e-5 for fp32 (fp32 accumulation in
+  another order, output rounding);
+* batch invariance: rows of a 200-row launch == the same rows inside a 6 400-row launch, bit for bit;
+* the latency engine with the fusion on vs off: the synthesised style codes agree to bf16 level.
+"""
+import ctypes as C
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(gpu_device):
+    from stzs.engine import StyleTTSZS
+    from stzs.params import init_params
+    from stzs.spec import SPEC_TINY
+    return StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, 0), device=gpu_device)
+
+
+def _weights(eng, w, b):
+    from stzs.weights import Arena, pack_conv
+    A = Arena()
+    cw = pack_conv(A, "g", w, b)
+    A.finalize(eng.device)
+    cw.w, cw.b = A[cw.w], A[cw.b]
+    return cw
+
+
+def _ln(eng, h, G, Bt, gs, bs, gdiv, gadd=0.0):
+    """stzs_rowln_args of a modulated LayerNorm of the rows of h into bf16 (the unfused form's output buffer)"""
+    from stzs.engine import Act
+    R, T, Cc = h.shape
+    y = Act(torch.zeros(R, T, Cc, device=h.device, dtype=torch.bfloat16))
+    a = eng._ln_args(Act(h), y, G=G.data_ptr() if G is not None else None, gs=gs,
+                     Bt=Bt.data_ptr() if Bt is not None else None, bs=bs, gdiv=gdiv, gadd=gadd)
+    return a, y
+
+
+def _unfused_ln(eng, a, y):
+    from stzs import _lib as L
+    L.check(eng.lib.stzs_row_layernorm(C.byref(a), eng.stream()), "ln")
+    torch.cuda.synchronize()
+    return y.t.clone()
+
+
+def _fused(eng, cw, ln, x_act, N, odt, act, acc=None, alpha=1.0, beta=0.0):
+    """y = linear(LN rows) through engine.conv(pre_ln=...) on the rows form"""
+    from stzs import _lib as L
+    from stzs.engine import Act
+    B, T = x_act.B, x_act.T
+    y = Act(torch.zeros(B, T, N, device=eng.device, dtype=odt))
+    n0 = eng.launches
+    eng.conv(cw, x_act, y, epi_act=act, acc_in=acc, alpha=alpha, beta=beta, rows=1, pre_ln=ln, what="lnrows")
+    torch.cuda.synchronize()
+    assert eng.launches == n0 + 1, "the LayerNorm must run inside the linear's launch"
+    return y.t.clone()
+
+
+def _inputs(dev, R, T, Cc, seed, groups):
+    g = torch.Generator().manual_seed(seed)
+    h = (torch.randn(R, T, Cc, generator=g) * 2 + 0.3).to(dev)
+    G = (torch.randn(groups, Cc, generator=g) * 0.2).to(dev)
+    Bt = (torch.randn(groups, Cc, generator=g) * 0.1).to(dev)
+    return h, G, Bt
+
+
+@pytest.mark.parametrize("Cc", [128, 512, 1024])
+@pytest.mark.parametrize("affine", [False, True])
+def test_operand_image_is_row_layernorm(eng, Cc, affine):
+    """identity weight, fp32 out: the fused launch returns the unfused LayerNorm's bf16 values exactly"""
+    from stzs.engine import Act
+    dev = eng.device
+    R, T = 2, 100
+    h, G, Bt = _inputs(dev, R, T, Cc, Cc + affine, R)
+    if affine:  # ln_g / ln_b: one vector for every row
+        ln, yln = _ln(eng, h, G[0], Bt[0], 0, 0, 1)
+    else:  # adaLN: per-utterance rows (gdiv = T)
+        ln, yln = _ln(eng, h, G, Bt, Cc, Cc, T, gadd=1.0)
+    ref = _unfused_ln(eng, ln, yln).float()
+    cw = _weights(eng, torch.eye(Cc), torch.zeros(Cc))
+    y = _fused(eng, cw, ln, yln, Cc, torch.float32, 0)
+    assert torch.equal(y, ref)
+
+
+CASES = [  # name, K, N, out dtype, act, acc_in
+    ("qkv", 512, 1536, torch.bfloat16, "none", False),
+    ("ca_q", 512, 512, torch.bfloat16, "none", False),
+    ("ff1", 512, 2048, torch.bfloat16, "gelu", False),
+    ("out", 512, 256, torch.float32, "none", True),
+    ("k256", 256, 384, torch.bfloat16, "silu", False),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_ln_linear_vs_torch(eng, case):
+    from stzs import _lib as L
+    from stzs.engine import Act
+    name, K, N, odt, act, acc = case
+    dev = eng.device
+    R, T = 2, 100
+    h, G, Bt = _inputs(dev, R, T, K, K + N, R)
+    ln, yln = _ln(eng, h, G, Bt, K, K, T, gadd=1.0)
+    a_ref = _unfused_ln(eng, ln, yln).float().cpu()
+    g = torch.Generator().manual_seed(N)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g) * 0.1
+    cw = _weights(eng, w, b)
+    ai = torch.randn(R, T, N, generator=g).to(odt) if acc else None
+    ea = {"none": L.ACT_NONE, "gelu": L.ACT_GELU, "silu": L.ACT_SILU}[act]
+    y = _fused(eng, cw, ln, yln, N, odt, ea, acc=Act(ai.to(dev)) if acc else None, alpha=0.75 if acc else 1.0,
+               beta=1.25 if acc else 0.0).float().cpu()
+    ref = a_ref @ w.to(torch.bfloat16).float().t() + b
+    if act == "gelu":
+        ref = torch.nn.functional.gelu(ref)
+    elif act == "silu":
+        ref = torch.nn.functional.silu(ref)
+    if acc:
+        ref = ref * 0.75 + 1.25 * ai.float()
+    tol = 1e-2 if odt == torch.bfloat16 else 1e-5
+    err = ((y - ref).abs().max() / ref.abs().max()).item()
+    assert err < tol, (name, err)
+
+
+def test_ln_linear_batch_invariant(eng):
+    """rows 0..199 of a 6 400-row launch == the same 200 rows launched alone"""
+    dev = eng.device
+    K, N, T = 512, 1536, 100
+    h, G, Bt = _inputs(dev, 64, T, K, 7, 64)
+    ln_big, y_big = _ln(eng, h, G, Bt, K, K, T, gadd=1.0)
+    g = torch.Generator().manual_seed(3)
+    cw = _weights(eng, torch.randn(N, K, generator=g) / math.sqrt(K), torch.randn(N, generator=g) * 0.1)
+    big = _fused(eng, cw, ln_big, y_big, N, torch.bfloat16, 0)
+    ln_s, y_s = _ln(eng, h[:2].contiguous(), G[:2].contiguous(), Bt[:2].contiguous(), K, K, T, gadd=1.0)
+    small = _fused(eng, cw, ln_s, y_s, N, torch.bfloat16, 0)
+    assert torch.equal(big[:2], small)
+
+
+def test_ln_linear_rejects(eng):
+    """shapes the fused form does not take are refused before any launch (the engine then runs the two launches)"""
+    from stzs import _lib as L
+    from stzs.engine import Act
+    dev = eng.device
+    h, G, Bt = _inputs(dev, 2, 100, 512, 1, 2)
+    ln, yln = _ln(eng, h, G, Bt, 512, 512, 100)
+    cw = _weights(eng, torch.randn(256, 512), torch.zeros(256))
+    a = L.ConvArgs()
+    a.x, a.w, a.y = yln.ptr, cw.w.data_ptr(), yln.ptr
+    a.B, a.T_in, a.T_out, a.Ci, a.Co, a.ks, a.ci_pad, a.co_pad, a.cic = 2, 100, 100, 512, 256, 1, 512, 256, 64
+    a.ldx, a.bsx, a.ldy, a.bsy, a.in_dtype, a.out_dtype, a.alpha = 512, 51200, 512, 51200, L.BF16, L.BF16, 1.0
+    ln.C = 256  # LayerNorm width != K
+    assert eng.lib.stzs_ln_linear(C.byref(a), C.byref(ln), eng.stream()) == L.ESHAPE
+    ln.C, ln.out_dtype = 512, L.F32  # the operand must be the bf16 rounding
+    assert eng.lib.stzs_ln_linear(C.byref(a), C.byref(ln), eng.stream()) == L.EDTYPE
+
+
+def test_latency_engine_fused_vs_unfused(gpu_device):
+    """configs[1] on the batch-1 latency engine with the LayerNorms fused vs launched: one LayerNorm launch fewer per
+    DiT LayerNorm, same style codes to bf16 level (the oracle parity of the fused engine: tests/test_gpu_configs.py)"""
+    import bench
+    from stzs.engine import StyleTTSZS, latency_engine
+    from stzs.params import init_params
+    from stzs.spec import SPEC_V0
+    S = SPEC_V0
+    base = StyleTTSZS(S, init_params(S, seed=0), device=gpu_device)
+    tok, ref, eps, dur = bench.make_inputs(S, 1, seed=1000)
+    outs, launches = [], []
+    for fuse in (False, True):
+        e = latency_engine(S, base.W, base.device)
+        e.ln_fuse = fuse
+        n0 = e.launches
+        out = e.synth(tok, ref, steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG, noise=eps, durations=dur, seeds=[7])
+        launches.append(e.launches - n0)
+        outs.append(out["codes"].float().cpu())
+    nln = bench.STEPS_LATENCY * (3 * S.dn_layers + 1)
+    assert launches[0] - launches[1] == nln, launches
+    err = ((outs[0] - outs[1]).norm() / outs[0].norm()).item()
+    assert err < 1e-2, err
