@@ -208,10 +208,10 @@ typedef struct stzs_rowln_args {
 int stzs_row_layernorm(const stzs_rowln_args* a, void* stream);
 /* the LayerNorm that feeds a small-M linear, fused into it (csrc/lnrows.hip; the configs[1] batch-1 denoiser's
  * adaLN / affine LayerNorms, each read by one linear): y = epilogue(A W^T) with A = the bf16 rows stzs_row_layernorm(ln)
- * would store (same row arithmetic; ln->y is not written).  a: a linear (ks 1, no prologue, no residual / gate /
- * split-K / fp8) on STZS_PACK_KSTEP bf16 weights with Ci = ci_pad = ln->C in {128, 256, 512, 1024}; a->x unused,
- * ln->R = B * T_in rows of ln->x (f32 | bf16), ln->out_dtype = STZS_BF16.  Epilogue: bias, epi_act NONE | GELU | SILU,
- * alpha, beta * acc_in; y bf16 | f32.  Per output element one sequential K chain (batch-invariant). */
+ * would store (its statistics summed per 16-lane group: within one bf16 ulp; ln->y is not written).  a: a linear
+ * (ks 1, no prologue, no residual / gate / split-K / fp8) on STZS_PACK_KSTEP bf16 weights with Ci = ci_pad = ln->C in
+ * {128, 256, 512}; a->x unused, ln->R = B * T_in rows of ln->x (f32 | bf16), ln->out_dtype = STZS_BF16, ln->act
+ * NONE.  Epilogue: bias, epi_act NONE | GELU | SILU, alpha, beta * acc_in; y bf16 | f32.  Per output element one sequential K chain (batch-invariant). */
 int stzs_ln_linear(const stzs_conv_args* a, const stzs_rowln_args* ln, void* stream);
 
 /* per-row fp8 quantisation with a power-of-two row scale (exact scaling, as MX block scales):

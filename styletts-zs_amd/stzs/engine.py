@@ -416,7 +416,8 @@ class StyleTTSZS:
         if pre_ln is not None:
             nk = cw.ci_pad // 32
             fused = bool(a.flags & L.CONV_ROWS) and a.splitk <= 1 and res is None and gate is None and \
-                st is None and pre_ln.C == cw.Ci == cw.ci_pad and nk in (4, 8, 16, 32) and pre_ln.out_dtype == L.BF16
+                st is None and pre_ln.C == cw.Ci == cw.ci_pad and nk in (4, 8, 16) and pre_ln.out_dtype == L.BF16 and \
+                pre_ln.act == L.ACT_NONE
             if fused:
                 launch = lambda: self.lib.stzs_ln_linear(C.byref(a), C.byref(pre_ln), self.stream())
             else:
