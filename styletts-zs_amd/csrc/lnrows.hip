@@ -118,6 +118,90 @@ __global__ __launch_bounds__(NTHR) void ln_rows(const stzs_conv_args a, const st
     }
 }
 
+// The plain small-M linear on the same 16-row x 64-column workgroup (stzs_ln_linear with ln = NULL; the batch-1
+// denoiser's attention output projections and input projection, the per-utterance linears): A fragments straight
+// from the x rows into registers (bf16, or fp32 x pro_cscale rounded to bf16 as csrc/rows.hip), every K-step of both
+// operands in flight from entry, no LDS; the epilogue adds the FLAT DiT gate and the residual.
+template <typename TI, typename TOut, int NK, int EACT>
+__global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int T = a.T_in, nR = a.B * T;
+    const int r0 = blockIdx.y * LR_ROWS;
+    const int ct = blockIdx.x * 4 + wave;
+    if (ct * 16 >= a.Co) return;  // (wave-uniform; no barrier in this kernel)
+    const int cot = ct >> 3, rr = (ct & 7) * 16 + (lane & 15);
+    const unsigned char* Wb = reinterpret_cast<const unsigned char*>(a.w) + ((int64_t)cot * NK * 128 + rr) * 64 +
+                              (((lane >> 4) ^ gswz(rr)) << 4);
+    uint4 br[NK];
+#pragma unroll
+    for (int j = 0; j < NK; ++j) br[j] = *reinterpret_cast<const uint4*>(Wb + (int64_t)j * 128 * 64);
+    const float invT = 1.f / (float)T;
+    int Ra = r0 + (lane & 15);  // this lane's A row; k offset 8 (lane >> 4) in every K-step
+    Ra = Ra < nR ? Ra : nR - 1;
+    const long ba = rowdiv(Ra, T, invT, true);
+    const TI* X = reinterpret_cast<const TI*>(a.x) + ba * a.bsx + (Ra - ba * T) * a.ldx + (lane >> 4) * 8;
+    typename Raw<TI>::T ar[NK];
+#pragma unroll
+    for (int j = 0; j < NK; ++j) ar[j] = Raw<TI>::load(X + j * 32);
+    // every load issued before the first MFMA (hipcc otherwise interleaves them to save registers)
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+        bf16x8 fa;
+        if constexpr (sizeof(TI) == 2) {
+            fa = __builtin_bit_cast(bf16x8, ar[j]);
+        } else {
+            float v[8];
+            Raw<TI>::cvt(ar[j], v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= a.pro_cscale;
+            fa = __builtin_bit_cast(bf16x8, pack8(v));
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, __builtin_bit_cast(bf16x8, br[j]), acc, 0, 0, 0);
+    }
+    // ---- epilogue (csrc/rows.hip's order: act(v + bias), gate, + residual, alpha, + beta acc_in) ----
+    const int n = ct * 16 + (lane & 15);
+    if (n >= a.Co) return;
+    const float bias = a.bias ? a.bias[n] : 0.f;
+    const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
+    const TOut* AI = reinterpret_cast<const TOut*>(a.acc_in);
+    TOut* Y = reinterpret_cast<TOut*>(a.y);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int R = r0 + (lane >> 4) * 4 + i;
+        if (R >= nR) continue;
+        const long bb = rowdiv(R, T, invT, true);
+        const long t = R - bb * T;
+        float x = epi_act<EACT>(acc[i] + bias, a.epi_slope);
+        if (a.gate) x *= a.gate[bb * a.gate_bs + n];
+        if (Rp) x += DT<TOut>::ld(Rp + bb * a.bsr + t * a.ldr + n);
+        x *= a.alpha;
+        if (AI) x += a.beta * DT<TOut>::ld(AI + bb * a.bsa + t * a.lda + n);
+        DT<TOut>::st(Y + bb * a.bsy + t * a.ldy + n, x);
+    }
+}
+
+template <typename TI, typename TOut, int NK>
+void* pick_plain_act(int act) {
+    switch (act) {
+        case STZS_ACT_GELU: return (void*)rows16<TI, TOut, NK, STZS_ACT_GELU>;
+        case STZS_ACT_SILU: return (void*)rows16<TI, TOut, NK, STZS_ACT_SILU>;
+        case STZS_ACT_NONE: return (void*)rows16<TI, TOut, NK, STZS_ACT_NONE>;
+        default: return nullptr;
+    }
+}
+
+template <typename TI, typename TOut>
+void* pick_plain(int nk, int act) {
+    switch (nk) {
+        case 4: return pick_plain_act<TI, TOut, 4>(act);
+        case 8: return pick_plain_act<TI, TOut, 8>(act);
+        case 16: return pick_plain_act<TI, TOut, 16>(act);
+        default: return nullptr;
+    }
+}
+
 template <typename TI, typename TOut, int NK>
 void* pick_act(int act) {
     switch (act) {
@@ -140,8 +224,37 @@ void* pick(int nk, int act) {
 
 }  // namespace
 
+static int plain_launch(const stzs_conv_args* a, hipStream_t s) {
+    if (!a->x) return STZS_EINVAL;
+    const bool lin = a->ks == 1 && a->stride == 1 && a->pad == 0 && a->ups == 0 && a->T_in == a->T_out &&
+                     a->pro_mode == STZS_PRO_NONE && a->pro_act == STZS_ACT_NONE && !a->stat_part && !a->x_scale &&
+                     a->splitk <= 1 && (!a->res || a->res_tdiv == 1);
+    if (!lin || (a->flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 | STZS_CONV_W_F32 | STZS_CONV_W_X3 |
+                             STZS_CONV_W_FRAG32 | STZS_CONV_UPS_NOISE)))
+        return STZS_EINVAL;
+    const int nk = a->ci_pad / 32;
+    if (a->B <= 0 || a->T_in <= 0 || a->Co <= 0 || a->Co > a->co_pad || a->co_pad % 128 || a->Ci > a->ci_pad ||
+        a->ci_pad % 32 || (nk != 4 && nk != 8 && nk != 16) || (long)a->B * a->T_in >= (1 << 22) - LR_ROWS)
+        return STZS_ESHAPE;
+    // A rows are read over [0, ci_pad) in 16-B (bf16) / 32-B (fp32) pieces
+    if (a->ldx < a->ci_pad || a->ldx % 8 || a->bsx % 8 || !stzs_aligned(a->x, 16)) return STZS_ESHAPE;
+    void* k = nullptr;
+    if (a->in_dtype == STZS_BF16 && a->pro_cscale != 1.f) return STZS_EINVAL;
+    if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) k = pick_plain<bf16_t, bf16_t>(nk, a->epi_act);
+    else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) k = pick_plain<bf16_t, float>(nk, a->epi_act);
+    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32) k = pick_plain<float, float>(nk, a->epi_act);
+    else return STZS_EDTYPE;
+    if (!k) return STZS_EINVAL;
+    dim3 grid((unsigned)((a->Co + 63) / 64), (unsigned)(((long)a->B * a->T_in + LR_ROWS - 1) / LR_ROWS));
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(stzs_conv_args)>(k), grid, dim3(NTHR), 0, s, *a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
 extern "C" int stzs_ln_linear(const stzs_conv_args* a, const stzs_rowln_args* ln, void* stream) {
-    if (!a || !ln || !a->w || !a->y || !ln->x) return STZS_EINVAL;
+    if (!a || !a->w || !a->y) return STZS_EINVAL;
+    if (!ln) return plain_launch(a, reinterpret_cast<hipStream_t>(stream));
+    if (!ln->x) return STZS_EINVAL;
     const bool lin = a->ks == 1 && a->stride == 1 && a->pad == 0 && a->ups == 0 && a->T_in == a->T_out &&
                      a->pro_mode == STZS_PRO_NONE && a->pro_act == STZS_ACT_NONE && !a->stat_part && !a->x_scale &&
                      !a->res && !a->gate && a->splitk <= 1;

@@ -212,6 +212,9 @@ class StyleTTSZS:
         # with the denoiser linears on the small-M rows form (dn_rows): each adaLN / affine LayerNorm fused into the
         # one linear that reads it (stzs_ln_linear, csrc/lnrows.hip) instead of its own launch.  STZS_LN_FUSE=0: off
         self.ln_fuse = os.environ.get("STZS_LN_FUSE", "1") != "0"
+        # one-slice rows-form linears with K <= 512 on the 16-row register-direct form (csrc/lnrows.hip rows16: every
+        # K-step of both operands in flight, no cross-wave reduction).  STZS_ROWS16=0: csrc/rows.hip for all of them
+        self.rows16 = os.environ.get("STZS_ROWS16", "1") != "0"
         # the last generator stage's noise conv fused into its ConvTranspose (bf16 engines); STZS_UPS_NOISE=0: off
         self.ups_noise_fused = os.environ.get("STZS_UPS_NOISE", "1") != "0"
         # the first stage's strided noise conv on super-rows of the harmonic source (register-direct kernel, bf16
@@ -422,6 +425,12 @@ class StyleTTSZS:
                 launch = lambda: self.lib.stzs_ln_linear(C.byref(a), C.byref(pre_ln), self.stream())
             else:
                 self._call(self.lib.stzs_row_layernorm, pre_ln, what + ".ln", cost=_ln_cost(pre_ln))
+        # a one-slice rows-form linear with K <= 512 on the 16-row register-direct form (stzs_ln_linear, ln = NULL)
+        r16 = (pre_ln is None and self.rows16 and bool(a.flags & L.CONV_ROWS) and a.splitk <= 1 and st is None and
+               cw.ci_pad // 32 in (4, 8, 16) and (res is None or res_tdiv == 1) and x.ptr % 16 == 0 and
+               x.ld % 8 == 0 and x.bs % 8 == 0)
+        if r16:
+            launch = lambda: self.lib.stzs_ln_linear(C.byref(a), None, self.stream())
         if tm is not None and (tm["all"] or what in tm["tags"]):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -441,7 +450,7 @@ class StyleTTSZS:
             if fused:  # the LayerNorm's input rows instead of x
                 byt += pre_ln.R * pre_ln.C * (4 if pre_ln.in_dtype == L.F32 else 2) - x.B * x.T * x.C * x.t.element_size()
             tm["rec"].append((what, e0, e1, flops, byt, (cw.ks, dil, a.T_out, cw.Co), self.stage))
-        elif fused:
+        elif fused or r16:
             self.launches += 1
             L.check(launch(), what)
         else:
