@@ -132,17 +132,20 @@ __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
     const int cot = ct >> 3, rr = (ct & 7) * 16 + (lane & 15);
     const unsigned char* Wb = reinterpret_cast<const unsigned char*>(a.w) + ((int64_t)cot * NK * 128 + rr) * 64 +
                               (((lane >> 4) ^ gswz(rr)) << 4);
-    uint4 br[NK];
-#pragma unroll
-    for (int j = 0; j < NK; ++j) br[j] = *reinterpret_cast<const uint4*>(Wb + (int64_t)j * 128 * 64);
+    // K-steps in flight per wave: all of them up to 16 (fp32 A: 8), then a ring refilled as each is consumed
+    constexpr int CH = NK < (sizeof(TI) == 2 ? 16 : 8) ? NK : (sizeof(TI) == 2 ? 16 : 8);
     const float invT = 1.f / (float)T;
     int Ra = r0 + (lane & 15);  // this lane's A row; k offset 8 (lane >> 4) in every K-step
     Ra = Ra < nR ? Ra : nR - 1;
     const long ba = rowdiv(Ra, T, invT, true);
     const TI* X = reinterpret_cast<const TI*>(a.x) + ba * a.bsx + (Ra - ba * T) * a.ldx + (lane >> 4) * 8;
-    typename Raw<TI>::T ar[NK];
+    uint4 br[CH];
+    typename Raw<TI>::T ar[CH];
 #pragma unroll
-    for (int j = 0; j < NK; ++j) ar[j] = Raw<TI>::load(X + j * 32);
+    for (int j = 0; j < CH; ++j) {
+        br[j] = *reinterpret_cast<const uint4*>(Wb + (int64_t)j * 128 * 64);
+        ar[j] = Raw<TI>::load(X + j * 32);
+    }
     // every load issued before the first MFMA (hipcc otherwise interleaves them to save registers)
     __builtin_amdgcn_sched_barrier(0);
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -150,15 +153,20 @@ __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
     for (int j = 0; j < NK; ++j) {
         bf16x8 fa;
         if constexpr (sizeof(TI) == 2) {
-            fa = __builtin_bit_cast(bf16x8, ar[j]);
+            fa = __builtin_bit_cast(bf16x8, ar[j % CH]);
         } else {
             float v[8];
-            Raw<TI>::cvt(ar[j], v);
+            Raw<TI>::cvt(ar[j % CH], v);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] *= a.pro_cscale;
             fa = __builtin_bit_cast(bf16x8, pack8(v));
         }
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, __builtin_bit_cast(bf16x8, br[j]), acc, 0, 0, 0);
+        const bf16x8 fb = __builtin_bit_cast(bf16x8, br[j % CH]);
+        if (j + CH < NK) {
+            br[j % CH] = *reinterpret_cast<const uint4*>(Wb + (int64_t)(j + CH) * 128 * 64);
+            ar[j % CH] = Raw<TI>::load(X + (j + CH) * 32);
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc, 0, 0, 0);
     }
     // ---- epilogue (csrc/rows.hip's order: act(v + bias), gate, + residual, alpha, + beta acc_in) ----
     const int n = ct * 16 + (lane & 15);
@@ -198,6 +206,8 @@ void* pick_plain(int nk, int act) {
         case 4: return pick_plain_act<TI, TOut, 4>(act);
         case 8: return pick_plain_act<TI, TOut, 8>(act);
         case 16: return pick_plain_act<TI, TOut, 16>(act);
+        case 32: return pick_plain_act<TI, TOut, 32>(act);
+        case 64: return pick_plain_act<TI, TOut, 64>(act);
         default: return nullptr;
     }
 }
@@ -234,7 +244,8 @@ static int plain_launch(const stzs_conv_args* a, hipStream_t s) {
         return STZS_EINVAL;
     const int nk = a->ci_pad / 32;
     if (a->B <= 0 || a->T_in <= 0 || a->Co <= 0 || a->Co > a->co_pad || a->co_pad % 128 || a->Ci > a->ci_pad ||
-        a->ci_pad % 32 || (nk != 4 && nk != 8 && nk != 16) || (long)a->B * a->T_in >= (1 << 22) - LR_ROWS)
+        a->ci_pad % 32 || (nk != 4 && nk != 8 && nk != 16 && nk != 32 && nk != 64) ||
+        (long)a->B * a->T_in >= (1 << 22) - LR_ROWS)
         return STZS_ESHAPE;
     // A rows are read over [0, ci_pad) in 16-B (bf16) / 32-B (fp32) pieces
     if (a->ldx < a->ci_pad || a->ldx % 8 || a->bsx % 8 || !stzs_aligned(a->x, 16)) return STZS_ESHAPE;

@@ -212,9 +212,10 @@ class StyleTTSZS:
         # with the denoiser linears on the small-M rows form (dn_rows): each adaLN / affine LayerNorm fused into the
         # one linear that reads it (stzs_ln_linear, csrc/lnrows.hip) instead of its own launch.  STZS_LN_FUSE=0: off
         self.ln_fuse = os.environ.get("STZS_LN_FUSE", "1") != "0"
-        # one-slice rows-form linears with K <= 512 on the 16-row register-direct form (csrc/lnrows.hip rows16: every
-        # K-step of both operands in flight, no cross-wave reduction).  STZS_ROWS16=0: csrc/rows.hip for all of them
+        # rows-form linears with K <= rows16_maxk on the 16-row register-direct form (csrc/lnrows.hip rows16: up to 16
+        # K-steps of both operands in flight, no cross-wave reduction, no K slices).  STZS_ROWS16=0: csrc/rows.hip
         self.rows16 = os.environ.get("STZS_ROWS16", "1") != "0"
+        self.rows16_maxk = int(os.environ.get("STZS_ROWS16_MAXK", "512"))  # (ffn2, K 2048: rows.hip Z 4 measured as fast, r04_t)
         # the last generator stage's noise conv fused into its ConvTranspose (bf16 engines); STZS_UPS_NOISE=0: off
         self.ups_noise_fused = os.environ.get("STZS_UPS_NOISE", "1") != "0"
         # the first stage's strided noise conv on super-rows of the harmonic source (register-direct kernel, bf16
@@ -425,11 +426,13 @@ class StyleTTSZS:
                 launch = lambda: self.lib.stzs_ln_linear(C.byref(a), C.byref(pre_ln), self.stream())
             else:
                 self._call(self.lib.stzs_row_layernorm, pre_ln, what + ".ln", cost=_ln_cost(pre_ln))
-        # a one-slice rows-form linear with K <= 512 on the 16-row register-direct form (stzs_ln_linear, ln = NULL)
-        r16 = (pre_ln is None and self.rows16 and bool(a.flags & L.CONV_ROWS) and a.splitk <= 1 and st is None and
-               cw.ci_pad // 32 in (4, 8, 16) and (res is None or res_tdiv == 1) and x.ptr % 16 == 0 and
-               x.ld % 8 == 0 and x.bs % 8 == 0)
+        # a rows-form linear with K <= rows16_maxk on the 16-row register-direct form (stzs_ln_linear, ln = NULL; its
+        # K slices, if any, dropped: one sequential chain per element)
+        r16 = (pre_ln is None and self.rows16 and bool(a.flags & L.CONV_ROWS) and st is None and
+               cw.ci_pad // 32 in (4, 8, 16, 32, 64) and cw.ci_pad <= self.rows16_maxk and
+               (res is None or res_tdiv == 1) and x.ptr % 16 == 0 and x.ld % 8 == 0 and x.bs % 8 == 0)
         if r16:
+            a.splitk = 0
             launch = lambda: self.lib.stzs_ln_linear(C.byref(a), None, self.stream())
         if tm is not None and (tm["all"] or what in tm["tags"]):
             e0 = torch.cuda.Event(enable_timing=True)

@@ -3,8 +3,9 @@
 Against torch fp32 on the same bf16 operands (max-rel over the outputs: fp32 accumulation in a different order,
 bf16 output rounding -> 1e-2 for bf16 outputs, 1e-5 for fp32 outputs), for every denoiser linear shape and epilogue
 (GELU ffn1, gated residual o / ffn2 in fp32, c_out / c_skip dn.out with accumulate-input, fp32-input dn.in with
-cscale) and every K split Z; batch invariance (rows of a 100-row launch == the same rows inside a 6 400-row launch,
-bit for bit); re-runs bit-identical (the split-K tickets are left zeroed).
+cscale) and every K split Z, on both small-M forms (rows.hip, lnrows.hip rows16); batch invariance (rows of a
+100-row launch == the same rows inside a 6 400-row launch, bit for bit); re-runs bit-identical (the split-K tickets
+are left zeroed).
 """
 import math
 
@@ -14,12 +15,16 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def eng(gpu_device):
+@pytest.fixture(scope="module", params=["rows", "rows16"])
+def eng(request, gpu_device):
+    """both small-M forms: csrc/rows.hip (K slices Z) and the 16-row register-direct csrc/lnrows.hip rows16 (which
+    the engine takes for K <= rows16_maxk, ignoring Z)"""
     from stzs.engine import StyleTTSZS
     from stzs.params import init_params
     from stzs.spec import SPEC_TINY
-    return StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, 0), device=gpu_device)
+    e = StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, 0), device=gpu_device)
+    e.rows16 = request.param == "rows16"
+    return e
 
 
 CASES = [  # name, K, N, in dtype, out dtype, act, gated residual, acc_in, cscale
