@@ -119,26 +119,31 @@ __global__ __launch_bounds__(NTHR) void ln_rows(const stzs_conv_args a, const st
 }
 
 // The plain small-M linear on the same 16-row x 64-column workgroup (stzs_ln_linear with ln = NULL; the batch-1
-// denoiser's attention output projections and input projection, the per-utterance linears): A fragments straight
-// from the x rows into registers (bf16, or fp32 x pro_cscale rounded to bf16 as csrc/rows.hip), every K-step of both
-// operands in flight from entry, no LDS; the epilogue adds the FLAT DiT gate and the residual.
-template <typename TI, typename TOut, int NK, int EACT>
+// denoiser's attention output projections, ffn2 and input projection, the per-utterance linears): A fragments
+// straight from the x rows into registers (bf16, or fp32 x pro_cscale rounded to bf16 as csrc/rows.hip), up to 16
+// K-steps of both operands in flight, no LDS; the epilogue adds the FLAT DiT gate and the residual.
+// SPLIT (splitk = Z in {2, 4}): workgroup z runs K-steps [z NKS, (z+1) NKS) and hands its fp32 partials to the tile's
+// last arriver as csrc/rows.hip does (16-B write-through stores, drain, barrier, agent-scope ticket; the last arriver
+// sums the Z slabs in slice order with sc1 loads): the value does not depend on the arrival order or the row count.
+template <typename TI, typename TOut, int NKS, int EACT, bool SPLIT>
 __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int T = a.T_in, nR = a.B * T;
     const int r0 = blockIdx.y * LR_ROWS;
     const int ct = blockIdx.x * 4 + wave;
-    if (ct * 16 >= a.Co) return;  // (wave-uniform; no barrier in this kernel)
-    const int cot = ct >> 3, rr = (ct & 7) * 16 + (lane & 15);
-    const unsigned char* Wb = reinterpret_cast<const unsigned char*>(a.w) + ((int64_t)cot * NK * 128 + rr) * 64 +
-                              (((lane >> 4) ^ gswz(rr)) << 4);
+    if (!SPLIT && ct * 16 >= a.Co) return;  // (wave-uniform; no barrier without K slices)
+    const int ctc = ct * 16 < a.Co ? ct : 0;  // (with K slices every wave reaches the barriers)
+    const int NK = a.ci_pad / 32, kz = SPLIT ? (int)blockIdx.z * NKS : 0;
+    const int cot = ctc >> 3, rr = (ctc & 7) * 16 + (lane & 15);
+    const unsigned char* Wb = reinterpret_cast<const unsigned char*>(a.w) +
+                              (((int64_t)cot * NK + kz) * 128 + rr) * 64 + (((lane >> 4) ^ gswz(rr)) << 4);
     // K-steps in flight per wave: all of them up to 16 (fp32 A: 8), then a ring refilled as each is consumed
-    constexpr int CH = NK < (sizeof(TI) == 2 ? 16 : 8) ? NK : (sizeof(TI) == 2 ? 16 : 8);
+    constexpr int CH = NKS < (sizeof(TI) == 2 ? 16 : 8) ? NKS : (sizeof(TI) == 2 ? 16 : 8);
     const float invT = 1.f / (float)T;
     int Ra = r0 + (lane & 15);  // this lane's A row; k offset 8 (lane >> 4) in every K-step
     Ra = Ra < nR ? Ra : nR - 1;
     const long ba = rowdiv(Ra, T, invT, true);
-    const TI* X = reinterpret_cast<const TI*>(a.x) + ba * a.bsx + (Ra - ba * T) * a.ldx + (lane >> 4) * 8;
+    const TI* X = reinterpret_cast<const TI*>(a.x) + ba * a.bsx + (Ra - ba * T) * a.ldx + (lane >> 4) * 8 + kz * 32;
     uint4 br[CH];
     typename Raw<TI>::T ar[CH];
 #pragma unroll
@@ -150,7 +155,7 @@ __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
     __builtin_amdgcn_sched_barrier(0);
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < NK; ++j) {
+    for (int j = 0; j < NKS; ++j) {
         bf16x8 fa;
         if constexpr (sizeof(TI) == 2) {
             fa = __builtin_bit_cast(bf16x8, ar[j % CH]);
@@ -162,11 +167,41 @@ __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
             fa = __builtin_bit_cast(bf16x8, pack8(v));
         }
         const bf16x8 fb = __builtin_bit_cast(bf16x8, br[j % CH]);
-        if (j + CH < NK) {
+        if (j + CH < NKS) {
             br[j % CH] = *reinterpret_cast<const uint4*>(Wb + (int64_t)(j + CH) * 128 * 64);
             ar[j % CH] = Raw<TI>::load(X + (j + CH) * 32);
         }
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc, 0, 0, 0);
+    }
+    if constexpr (SPLIT) {
+        __shared__ int s_last;
+        const int Z = gridDim.z, z = blockIdx.z;
+        constexpr int SLAB = NTHR * 16;  // one f32x4 per thread
+        const int64_t tile = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        unsigned char* base = reinterpret_cast<unsigned char*>(a.splitk_ws) + tile * (int64_t)Z * SLAB;
+        const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(base, 0, Z * SLAB, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), wr, z * SLAB + tid * 16, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            typedef __attribute__((address_space(1))) unsigned int gu32;
+            gu32* ctr = (gu32*)(a.splitk_ctr + tile);
+            const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old == (unsigned)(Z - 1);
+            if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = last;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        u32x4 pv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)  // every slab (its own too) by sc1 loads, all in flight
+            if (q < Z) pv[q] = __builtin_amdgcn_raw_buffer_load_b128(wr, q * SLAB + tid * 16, 0, 16);
+        acc = __builtin_bit_cast(f32x4, pv[0]);
+#pragma unroll
+        for (int q = 1; q < 4; ++q)  // slice order
+            if (q < Z) acc += __builtin_bit_cast(f32x4, pv[q]);
+        if (ct * 16 >= a.Co) return;
     }
     // ---- epilogue (csrc/rows.hip's order: act(v + bias), gate, + residual, alpha, + beta acc_in) ----
     const int n = ct * 16 + (lane & 15);
@@ -190,24 +225,35 @@ __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
     }
 }
 
-template <typename TI, typename TOut, int NK>
+// the split form's slab bytes: ceil(M / 16) x ceil(Co / 64) tiles x Z slices x 4 KB (at most
+// stzs_conv_rows_workspace(M, Co, Z): rows16 is a valid user of the rows.hip workspace and counters)
+template <typename TI, typename TOut, int NKS, bool SPLIT>
 void* pick_plain_act(int act) {
     switch (act) {
-        case STZS_ACT_GELU: return (void*)rows16<TI, TOut, NK, STZS_ACT_GELU>;
-        case STZS_ACT_SILU: return (void*)rows16<TI, TOut, NK, STZS_ACT_SILU>;
-        case STZS_ACT_NONE: return (void*)rows16<TI, TOut, NK, STZS_ACT_NONE>;
+        case STZS_ACT_GELU: return (void*)rows16<TI, TOut, NKS, STZS_ACT_GELU, SPLIT>;
+        case STZS_ACT_SILU: return (void*)rows16<TI, TOut, NKS, STZS_ACT_SILU, SPLIT>;
+        case STZS_ACT_NONE: return (void*)rows16<TI, TOut, NKS, STZS_ACT_NONE, SPLIT>;
         default: return nullptr;
     }
 }
 
+// nks: K-steps per slice; split: Z > 1 (slices of 4 / 8 / 16 K-steps)
 template <typename TI, typename TOut>
-void* pick_plain(int nk, int act) {
-    switch (nk) {
-        case 4: return pick_plain_act<TI, TOut, 4>(act);
-        case 8: return pick_plain_act<TI, TOut, 8>(act);
-        case 16: return pick_plain_act<TI, TOut, 16>(act);
-        case 32: return pick_plain_act<TI, TOut, 32>(act);
-        case 64: return pick_plain_act<TI, TOut, 64>(act);
+void* pick_plain(int nks, bool split, int act) {
+    if (split) {
+        switch (nks) {
+            case 4: return pick_plain_act<TI, TOut, 4, true>(act);
+            case 8: return pick_plain_act<TI, TOut, 8, true>(act);
+            case 16: return pick_plain_act<TI, TOut, 16, true>(act);
+            default: return nullptr;
+        }
+    }
+    switch (nks) {
+        case 4: return pick_plain_act<TI, TOut, 4, false>(act);
+        case 8: return pick_plain_act<TI, TOut, 8, false>(act);
+        case 16: return pick_plain_act<TI, TOut, 16, false>(act);
+        case 32: return pick_plain_act<TI, TOut, 32, false>(act);
+        case 64: return pick_plain_act<TI, TOut, 64, false>(act);
         default: return nullptr;
     }
 }
@@ -238,25 +284,29 @@ static int plain_launch(const stzs_conv_args* a, hipStream_t s) {
     if (!a->x) return STZS_EINVAL;
     const bool lin = a->ks == 1 && a->stride == 1 && a->pad == 0 && a->ups == 0 && a->T_in == a->T_out &&
                      a->pro_mode == STZS_PRO_NONE && a->pro_act == STZS_ACT_NONE && !a->stat_part && !a->x_scale &&
-                     a->splitk <= 1 && (!a->res || a->res_tdiv == 1);
+                     (a->splitk <= 1 || a->splitk == 2 || a->splitk == 4) && (!a->res || a->res_tdiv == 1);
     if (!lin || (a->flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 | STZS_CONV_W_F32 | STZS_CONV_W_X3 |
                              STZS_CONV_W_FRAG32 | STZS_CONV_UPS_NOISE)))
         return STZS_EINVAL;
-    const int nk = a->ci_pad / 32;
+    const int nk = a->ci_pad / 32, Z = a->splitk > 1 ? a->splitk : 1, nks = nk / Z;
+    const bool split = Z > 1;
     if (a->B <= 0 || a->T_in <= 0 || a->Co <= 0 || a->Co > a->co_pad || a->co_pad % 128 || a->Ci > a->ci_pad ||
-        a->ci_pad % 32 || (nk != 4 && nk != 8 && nk != 16 && nk != 32 && nk != 64) ||
+        a->ci_pad % 32 || nk % Z || (split ? (nks != 4 && nks != 8 && nks != 16)
+                                           : (nks != 4 && nks != 8 && nks != 16 && nks != 32 && nks != 64)) ||
         (long)a->B * a->T_in >= (1 << 22) - LR_ROWS)
         return STZS_ESHAPE;
+    if (split && (!a->splitk_ws || !a->splitk_ctr || !stzs_aligned(a->splitk_ws, 16) || !stzs_aligned(a->splitk_ctr, 4)))
+        return STZS_EINVAL;
     // A rows are read over [0, ci_pad) in 16-B (bf16) / 32-B (fp32) pieces
     if (a->ldx < a->ci_pad || a->ldx % 8 || a->bsx % 8 || !stzs_aligned(a->x, 16)) return STZS_ESHAPE;
     void* k = nullptr;
     if (a->in_dtype == STZS_BF16 && a->pro_cscale != 1.f) return STZS_EINVAL;
-    if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) k = pick_plain<bf16_t, bf16_t>(nk, a->epi_act);
-    else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) k = pick_plain<bf16_t, float>(nk, a->epi_act);
-    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32) k = pick_plain<float, float>(nk, a->epi_act);
+    if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) k = pick_plain<bf16_t, bf16_t>(nks, split, a->epi_act);
+    else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) k = pick_plain<bf16_t, float>(nks, split, a->epi_act);
+    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32) k = pick_plain<float, float>(nks, split, a->epi_act);
     else return STZS_EDTYPE;
     if (!k) return STZS_EINVAL;
-    dim3 grid((unsigned)((a->Co + 63) / 64), (unsigned)(((long)a->B * a->T_in + LR_ROWS - 1) / LR_ROWS));
+    dim3 grid((unsigned)((a->Co + 63) / 64), (unsigned)(((long)a->B * a->T_in + LR_ROWS - 1) / LR_ROWS), (unsigned)Z);
     hipLaunchKernelGGL(reinterpret_cast<void (*)(stzs_conv_args)>(k), grid, dim3(NTHR), 0, s, *a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;

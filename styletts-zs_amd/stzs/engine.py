@@ -215,7 +215,10 @@ class StyleTTSZS:
         # rows-form linears with K <= rows16_maxk on the 16-row register-direct form (csrc/lnrows.hip rows16: up to 16
         # K-steps of both operands in flight, no cross-wave reduction, no K slices).  STZS_ROWS16=0: csrc/rows.hip
         self.rows16 = os.environ.get("STZS_ROWS16", "1") != "0"
-        self.rows16_maxk = int(os.environ.get("STZS_ROWS16_MAXK", "512"))  # (ffn2, K 2048: rows.hip Z 4 measured as fast, r04_t)
+        self.rows16_split = os.environ.get("STZS_ROWS16_SPLIT", "1") != "0"  # (the Z-slice form: batch-1 ffn2)
+        # (unsliced up to K 512: ffn2, K 2048, as one 64-K-step chain measured no faster than rows.hip Z 4, r04_t;
+        # with its 4 slices on the split form it is, r04_x)
+        self.rows16_maxk = int(os.environ.get("STZS_ROWS16_MAXK", "512"))
         # the last generator stage's noise conv fused into its ConvTranspose (bf16 engines); STZS_UPS_NOISE=0: off
         self.ups_noise_fused = os.environ.get("STZS_UPS_NOISE", "1") != "0"
         # the first stage's strided noise conv on super-rows of the harmonic source (register-direct kernel, bf16
@@ -426,13 +429,17 @@ class StyleTTSZS:
                 launch = lambda: self.lib.stzs_ln_linear(C.byref(a), C.byref(pre_ln), self.stream())
             else:
                 self._call(self.lib.stzs_row_layernorm, pre_ln, what + ".ln", cost=_ln_cost(pre_ln))
-        # a rows-form linear with K <= rows16_maxk on the 16-row register-direct form (stzs_ln_linear, ln = NULL; its
-        # K slices, if any, dropped: one sequential chain per element)
+        # a rows-form linear on the 16-row register-direct form (stzs_ln_linear, ln = NULL): K <= rows16_maxk as one
+        # sequential chain per element (its K slices dropped), or with its Z in {2, 4} slices of 4..16 K-steps
+        nk = cw.ci_pad // 32
         r16 = (pre_ln is None and self.rows16 and bool(a.flags & L.CONV_ROWS) and st is None and
-               cw.ci_pad // 32 in (4, 8, 16, 32, 64) and cw.ci_pad <= self.rows16_maxk and
                (res is None or res_tdiv == 1) and x.ptr % 16 == 0 and x.ld % 8 == 0 and x.bs % 8 == 0)
+        r16_split = r16 and self.rows16_split and a.splitk in (2, 4) and nk % a.splitk == 0 and \
+            nk // a.splitk in (4, 8, 16)
+        r16 = r16_split or (r16 and nk in (4, 8, 16, 32, 64) and cw.ci_pad <= self.rows16_maxk)
         if r16:
-            a.splitk = 0
+            if not r16_split:
+                a.splitk = 0
             launch = lambda: self.lib.stzs_ln_linear(C.byref(a), None, self.stream())
         if tm is not None and (tm["all"] or what in tm["tags"]):
             e0 = torch.cuda.Event(enable_timing=True)
