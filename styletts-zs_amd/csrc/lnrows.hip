@@ -326,7 +326,8 @@ extern "C" int stzs_ln_linear(const stzs_conv_args* a, const stzs_rowln_args* ln
     // the linear's K is the LayerNorm's row: C = Ci = ci_pad, 4 / 8 / 16 K-steps
     const int C = ln->C, nk = C / 32;
     if (C != a->Ci || C != a->ci_pad || C % 32 || (nk != 4 && nk != 8 && nk != 16)) return STZS_ESHAPE;
-    if ((long)ln->R != (long)a->B * a->T_in || ln->R >= (1 << 22) - LR_ROWS || ln->ldx % 8 || ln->gdiv <= 0)
+    if ((long)ln->R != (long)a->B * a->T_in || ln->R >= (1 << 22) - LR_ROWS || ln->ldx % 8 || ln->gdiv <= 0 ||
+        !stzs_aligned(ln->x, 16))
         return STZS_ESHAPE;
     if ((ln->G && (ln->gs % 8 || !stzs_aligned(ln->G, 32))) || (ln->Bt && (ln->bs % 8 || !stzs_aligned(ln->Bt, 32))))
         return STZS_ESHAPE;

@@ -424,7 +424,7 @@ class StyleTTSZS:
             nk = cw.ci_pad // 32
             fused = bool(a.flags & L.CONV_ROWS) and a.splitk <= 1 and res is None and gate is None and \
                 st is None and pre_ln.C == cw.Ci == cw.ci_pad and nk in (4, 8, 16) and pre_ln.out_dtype == L.BF16 and \
-                pre_ln.act == L.ACT_NONE
+                pre_ln.act == L.ACT_NONE and (pre_ln.x or 0) % 16 == 0 and pre_ln.ldx % 8 == 0
             if fused:
                 launch = lambda: self.lib.stzs_ln_linear(C.byref(a), C.byref(pre_ln), self.stream())
             else:
