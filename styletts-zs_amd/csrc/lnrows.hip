@@ -225,8 +225,6 @@ __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
     }
 }
 
-// the split form's slab bytes: ceil(M / 16) x ceil(Co / 64) tiles x Z slices x 4 KB (at most
-// stzs_conv_rows_workspace(M, Co, Z): rows16 is a valid user of the rows.hip workspace and counters)
 template <typename TI, typename TOut, int NKS, bool SPLIT>
 void* pick_plain_act(int act) {
     switch (act) {
@@ -280,6 +278,8 @@ void* pick(int nk, int act) {
 
 }  // namespace
 
+// (the K-slice form's slabs: ceil(M / 16) x ceil(Co / 64) tiles x Z x 4 KB, never more than
+// stzs_conv_rows_workspace(M, Co, Z); its tickets: one per tile, fewer than that workspace's)
 static int plain_launch(const stzs_conv_args* a, hipStream_t s) {
     if (!a->x) return STZS_EINVAL;
     const bool lin = a->ks == 1 && a->stride == 1 && a->pad == 0 && a->ups == 0 && a->T_in == a->T_out &&
