@@ -213,7 +213,7 @@ int stzs_row_layernorm(const stzs_rowln_args* a, void* stream);
  * {128, 256, 512}; a->x unused, ln->R = B * T_in rows of ln->x (f32 | bf16), ln->out_dtype = STZS_BF16, ln->act
  * NONE.  Epilogue: bias, epi_act NONE | GELU | SILU, alpha, beta * acc_in; y bf16 | f32.  Per output element one
  * sequential K chain (batch-invariant).
- * ln = NULL: the plain small-M linear on the same 16-row x 64-column workgroups (A = the x rows: bf16, or fp32 scaled
+ * ln = NULL: the plain small-M linear on 16-row workgroups of 16 columns (64 with K slices; A = the x rows: bf16, or fp32 scaled
  * by pro_cscale and rounded to bf16; ci_pad / 32 in {4, 8, 16, 32, 64}; x 16-B aligned, ldx / bsx multiples of 8;
  * epilogue adds the FLAT gate and the residual).  splitk = Z in {2, 4} with ci_pad / 32 / Z in {4, 8, 16}: K slices
  * handed to each tile's last arriver through splitk_ws (stzs_conv_rows_workspace(rows, Co, Z) bytes suffice) and

@@ -118,19 +118,19 @@ __global__ __launch_bounds__(NTHR) void ln_rows(const stzs_conv_args a, const st
     }
 }
 
-// The plain small-M linear on the same 16-row x 64-column workgroup (stzs_ln_linear with ln = NULL; the batch-1
+// The plain small-M linear on 16-row workgroups of WPG 16-column tiles (stzs_ln_linear with ln = NULL; the batch-1
 // denoiser's attention output projections, ffn2 and input projection, the per-utterance linears): A fragments
 // straight from the x rows into registers (bf16, or fp32 x pro_cscale rounded to bf16 as csrc/rows.hip), up to 16
 // K-steps of both operands in flight, no LDS; the epilogue adds the FLAT DiT gate and the residual.
 // SPLIT (splitk = Z in {2, 4}): workgroup z runs K-steps [z NKS, (z+1) NKS) and hands its fp32 partials to the tile's
 // last arriver as csrc/rows.hip does (16-B write-through stores, drain, barrier, agent-scope ticket; the last arriver
 // sums the Z slabs in slice order with sc1 loads): the value does not depend on the arrival order or the row count.
-template <typename TI, typename TOut, int NKS, int EACT, bool SPLIT>
+template <typename TI, typename TOut, int NKS, int EACT, bool SPLIT, int WPG = 4>
 __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int T = a.T_in, nR = a.B * T;
     const int r0 = blockIdx.y * LR_ROWS;
-    const int ct = blockIdx.x * 4 + wave;
+    const int ct = blockIdx.x * WPG + wave;  // (WPG waves per workgroup, one 16-column tile each)
     if (!SPLIT && ct * 16 >= a.Co) return;  // (wave-uniform; no barrier without K slices)
     const int ctc = ct * 16 < a.Co ? ct : 0;  // (with K slices every wave reaches the barriers)
     const int NK = a.ci_pad / 32, kz = SPLIT ? (int)blockIdx.z * NKS : 0;
@@ -225,19 +225,35 @@ __global__ __launch_bounds__(NTHR) void rows16(const stzs_conv_args a) {
     }
 }
 
-template <typename TI, typename TOut, int NKS, bool SPLIT>
+template <typename TI, typename TOut, int NKS, bool SPLIT, int WPG = 4>
 void* pick_plain_act(int act) {
     switch (act) {
-        case STZS_ACT_GELU: return (void*)rows16<TI, TOut, NKS, STZS_ACT_GELU, SPLIT>;
-        case STZS_ACT_SILU: return (void*)rows16<TI, TOut, NKS, STZS_ACT_SILU, SPLIT>;
-        case STZS_ACT_NONE: return (void*)rows16<TI, TOut, NKS, STZS_ACT_NONE, SPLIT>;
+        case STZS_ACT_GELU: return (void*)rows16<TI, TOut, NKS, STZS_ACT_GELU, SPLIT, WPG>;
+        case STZS_ACT_SILU: return (void*)rows16<TI, TOut, NKS, STZS_ACT_SILU, SPLIT, WPG>;
+        case STZS_ACT_NONE: return (void*)rows16<TI, TOut, NKS, STZS_ACT_NONE, SPLIT, WPG>;
         default: return nullptr;
     }
 }
 
 // nks: K-steps per slice; split: Z > 1 (slices of 4 / 8 / 16 K-steps)
 template <typename TI, typename TOut>
-void* pick_plain(int nks, bool split, int act) {
+void* pick_plain(int nks, bool split, int act, int wpg) {
+    if (wpg == 2 && !split) {  // 2-wave, 32-column workgroups
+        switch (nks) {
+            case 4: return pick_plain_act<TI, TOut, 4, false, 2>(act);
+            case 8: return pick_plain_act<TI, TOut, 8, false, 2>(act);
+            case 16: return pick_plain_act<TI, TOut, 16, false, 2>(act);
+            default: return nullptr;
+        }
+    }
+    if (wpg == 1 && !split) {  // one-wave, 16-column workgroups (the default)
+        switch (nks) {
+            case 4: return pick_plain_act<TI, TOut, 4, false, 1>(act);
+            case 8: return pick_plain_act<TI, TOut, 8, false, 1>(act);
+            case 16: return pick_plain_act<TI, TOut, 16, false, 1>(act);
+            default: return nullptr;
+        }
+    }
     if (split) {
         switch (nks) {
             case 4: return pick_plain_act<TI, TOut, 4, true>(act);
@@ -301,13 +317,22 @@ static int plain_launch(const stzs_conv_args* a, hipStream_t s) {
     if (a->ldx < a->ci_pad || a->ldx % 8 || a->bsx % 8 || !stzs_aligned(a->x, 16)) return STZS_ESHAPE;
     void* k = nullptr;
     if (a->in_dtype == STZS_BF16 && a->pro_cscale != 1.f) return STZS_EINVAL;
-    if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) k = pick_plain<bf16_t, bf16_t>(nks, split, a->epi_act);
-    else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) k = pick_plain<bf16_t, float>(nks, split, a->epi_act);
-    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32) k = pick_plain<float, float>(nks, split, a->epi_act);
+    // waves (16-column tiles) per workgroup of the unsliced form: 1 (STZS_ROWS16_WPG = 1 | 2 | 4; the sliced form: 4).
+    // More, smaller workgroups: batch-1 p50 6.83 (4) -> 6.65 (2) -> 6.52 ms (1), profiles/r04_af_lat.log, r04_ag_lat.log
+    static const int env_wpg = [] {
+        const char* e = getenv("STZS_ROWS16_WPG");
+        const int v = e ? atoi(e) : 1;
+        return v == 2 || v == 4 ? v : 1;
+    }();
+    const int wpg = (!split && nks <= 16) ? env_wpg : 4;
+    if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_BF16) k = pick_plain<bf16_t, bf16_t>(nks, split, a->epi_act, wpg);
+    else if (a->in_dtype == STZS_BF16 && a->out_dtype == STZS_F32) k = pick_plain<bf16_t, float>(nks, split, a->epi_act, wpg);
+    else if (a->in_dtype == STZS_F32 && a->out_dtype == STZS_F32) k = pick_plain<float, float>(nks, split, a->epi_act, wpg);
     else return STZS_EDTYPE;
     if (!k) return STZS_EINVAL;
-    dim3 grid((unsigned)((a->Co + 63) / 64), (unsigned)(((long)a->B * a->T_in + LR_ROWS - 1) / LR_ROWS), (unsigned)Z);
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(stzs_conv_args)>(k), grid, dim3(NTHR), 0, s, *a);
+    dim3 grid((unsigned)((a->Co + 16 * wpg - 1) / (16 * wpg)), (unsigned)(((long)a->B * a->T_in + LR_ROWS - 1) / LR_ROWS),
+              (unsigned)Z);
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(stzs_conv_args)>(k), grid, dim3(64 * wpg), 0, s, *a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }
