@@ -137,12 +137,8 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * Same prologue / epilogue contract as STZS_CONV_W_LANE16 with ks in {3, 7, 11} (Snake) or ks = 3
  * (LeakyReLU / identity), Co % 8 == 0; bit-identical results, no weight ring and no K-loop barrier. */
 #define STZS_CONV_W_FRAG32 256
-/* flags bit (FRAG32 weights): run the k3 single-chunk RESIDUAL convs on the persistent LDS-DMA-pipelined kernel
- * (csrc/mrfp.hip) instead of the one-tile-per-workgroup register-direct one (csrc/mrfv.hip); bit-identical
- * results.  Opt-in: per launch it is faster (stage-1 c2 324 vs 352 us, c2 + accumulate 298 vs 351 us), but in
- * the two-stream bench the step time is unchanged and its resident persistent workgroups can hold back the
- * co-resident LSTM launch of the concurrent stream. */
-#define STZS_CONV_MRF_PIPE 512
+/* (512: formerly STZS_CONV_MRF_PIPE, the persistent k3 MRF form of rounds 2-4 -- removed in round 5, no end-to-end
+ * gain; the bit stays unused) */
 /* flags: PRECISE split-operand form (csrc/conv.hip conv_x3).  w = two bf16 K-step streams (hi = bf16(w),
  * then lo = bf16(w - hi)), each [co_pad/128][ci_pad/32 * ks][128][32] in the STZS_PACK_KSTEP swizzle with
  * cic = 32 (stzs/weights.py kstep_stream_x3); activations are split the same way when staged, and every
@@ -153,7 +149,8 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * pro_cscale and rounded to bf16) x rows, STZS_PACK_KSTEP weights; every workgroup owns 16 output columns, all rows of
  * a 64/128-row block and 1/Z of K, operands loaded straight into MFMA fragments.  splitk = Z in {0, 1} (off) or any Z
  * with ci_pad / 32 = 4 Z {1, 2, 4, 8, 16}: the Z slices hand their fp32 partials to the tile's last arriver through
- * splitk_ws (stzs_conv_rows_workspace bytes) and splitk_ctr (one zeroed uint32 per tile, left zeroed).  Epilogue:
+ * splitk_ws (stzs_conv_rows_workspace bytes: the larger of this layout and stzs_ln_linear's K-slice layout) and
+ * splitk_ctr (one zeroed uint32 per tile, left zeroed).  Epilogue:
  * bias, epi_act NONE | GELU | SILU, FLAT gate, residual, alpha, beta * acc_in.  The per-element summation order depends on
  * K and Z only (batch-invariant).  Replaces gemm_glds for 100-row linears whose 8-32 tiles would stream all of K
  * through 8-32 CUs (SURVEY §8(a) a2 at B = 1). */
@@ -169,6 +166,8 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * 128 output channels per workgroup instead of its default wide form (256 per workgroup: every staged input row
  * transformed once per 256 channels instead of once per 128).  Bit-identical either way; an A/B switch. */
 #define STZS_CONV_MRFV_NARROW 8192
+/* bytes of splitk_ws for a K-sliced small-M linear over `rows` rows, Co columns, kgroups slices: covers both the
+ * csrc/rows.hip form (STZS_CONV_ROWS) and the 16-row K-slice form of stzs_ln_linear (ln = NULL, splitk in {2, 4}) */
 size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
 

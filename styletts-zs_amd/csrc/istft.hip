@@ -82,7 +82,12 @@ __global__ __launch_bounds__(256) void istft_kernel(const IstftJob a) {
 #pragma unroll
         for (int k = 0; k < nb; ++k) {
             const float mag = __expf(row[k]);
-            const float ph = __sinf(row[nb + k]);
+            // phase = sin(x) for an unbounded conv_post output x: reduced to [-pi, pi] first (two-constant Cody-Waite,
+            // exact k 2pi_hi for |x| < 2^17), since v_sin's accuracy falls off with |x|
+            const float xv = row[nb + k];
+            const float kq = rintf(xv * 0.159154943091895336f);
+            const float xr = fmaf(-kq, -1.7484555e-7f, fmaf(-kq, 6.28318548202514648f, xv));
+            const float ph = __sinf(xr);
             re[k] = mag * __cosf(ph);
             im[k] = mag * __sinf(ph);
         }

@@ -294,8 +294,8 @@ void* pick(int nk, int act) {
 
 }  // namespace
 
-// (the K-slice form's slabs: ceil(M / 16) x ceil(Co / 64) tiles x Z x 4 KB, never more than
-// stzs_conv_rows_workspace(M, Co, Z); its tickets: one per tile, fewer than that workspace's)
+// (the K-slice form's slabs: ceil(M / 16) x ceil(Co / 64) tiles x Z x 4 KB, which stzs_conv_rows_workspace(M, Co, Z)
+// covers (it returns the larger of this layout and csrc/rows.hip's); its tickets: one per tile)
 static int plain_launch(const stzs_conv_args* a, hipStream_t s) {
     if (!a->x) return STZS_EINVAL;
     const bool lin = a->ks == 1 && a->stride == 1 && a->pad == 0 && a->ups == 0 && a->T_in == a->T_out &&

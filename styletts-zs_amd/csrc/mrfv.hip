@@ -369,7 +369,6 @@ void (*pick(int ks, bool one, bool al, bool wide))(stzs_conv_args) {
 
 }  // namespace
 
-int stzs_mrfp_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrfp.hip (1: not applicable)
 int stzs_ups_conv_launch(const stzs_conv_args& a, hipStream_t s);   // csrc/ups.hip (polyphase ConvTranspose)
 
 // internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32 weights
@@ -383,10 +382,6 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
     if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
-    {  // STZS_CONV_MRF_PIPE: the k3 single-chunk residual convs on the persistent LDS-DMA-pipelined form (mrfp.hip)
-        const int r = stzs_mrfp_conv_launch(a, s);
-        if (r != 1) return r;
-    }
     const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + CS_BYTES;
     void (*k)(stzs_conv_args) = nullptr;
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;

@@ -276,7 +276,12 @@ extern "C" size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgr
     const int mt = rows_mt(rows);
     const long nblk = (rows + 16 * mt - 1) / (16 * mt);
     const long tiles = nblk * ((Co + 15) / 16);
-    return kgroups > 1 ? (size_t)tiles * kgroups * mt * 64 * 16 : 0;
+    if (kgroups <= 1) return 0;
+    const size_t rows_form = (size_t)tiles * kgroups * mt * 64 * 16;
+    // the K-slice form of csrc/lnrows.hip (rows16 split, stzs_ln_linear with ln = NULL) writes one 4-KB slab per
+    // (16-row x 64-column tile, slice): larger than this file's layout when Co % 64 is in (0, 48]
+    const size_t r16 = (size_t)((rows + 15) / 16) * ((Co + 63) / 64) * kgroups * 4096;
+    return rows_form > r16 ? rows_form : r16;
 }
 
 // validates the linear and launches

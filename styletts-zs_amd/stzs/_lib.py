@@ -23,7 +23,6 @@ CONV_W_FRAG32 = 256  # include/stzs.h STZS_CONV_W_FRAG32
 CONV_W_F32 = 64  # include/stzs.h STZS_CONV_W_F32 (fp32-MFMA conv_f32)
 CONV_W_X3 = 1024  # include/stzs.h STZS_CONV_W_X3 (precise mode: split-operand bf16x3 conv_x3)
 CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD remap)
-CONV_MRF_PIPE = 512  # include/stzs.h STZS_CONV_MRF_PIPE (k3 residual MRF convs on csrc/mrfp.hip, opt-in)
 CONV_ROWS = 2048  # include/stzs.h STZS_CONV_ROWS (small-M linear on the whole chip, csrc/rows.hip)
 CONV_UPS_NOISE = 4096  # include/stzs.h STZS_CONV_UPS_NOISE (ConvTranspose + fused 1x1 noise conv, csrc/ups.hip)
 CONV_MRFV_NARROW = 8192  # include/stzs.h STZS_CONV_MRFV_NARROW (register-direct MRF conv at 128 channels per workgroup)

@@ -224,7 +224,7 @@ class StyleTTSZS:
         # the first stage's strided noise conv on super-rows of the harmonic source (register-direct kernel, bf16
         # engines); STZS_NOISE_SUPER=0: the stride-6 conv_mfma form
         self.noise_super = os.environ.get("STZS_NOISE_SUPER", "1") != "0"
-        # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_MRF_PIPE = 512)
+        # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_LINEAR_IDS = 128)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
         # graph-replayed); check_status() reads it and raises
@@ -424,7 +424,11 @@ class StyleTTSZS:
             nk = cw.ci_pad // 32
             fused = bool(a.flags & L.CONV_ROWS) and a.splitk <= 1 and res is None and gate is None and \
                 st is None and pre_ln.C == cw.Ci == cw.ci_pad and nk in (4, 8, 16) and pre_ln.out_dtype == L.BF16 and \
-                pre_ln.act == L.ACT_NONE and (pre_ln.x or 0) % 16 == 0 and pre_ln.ldx % 8 == 0
+                pre_ln.act == L.ACT_NONE and (pre_ln.x or 0) % 16 == 0 and pre_ln.ldx % 8 == 0 and \
+                pre_ln.gdiv > 0 and pre_ln.R < (1 << 22) - 16 and \
+                (not pre_ln.G or (pre_ln.gs % 8 == 0 and pre_ln.G % 32 == 0)) and \
+                (not pre_ln.Bt or (pre_ln.bs % 8 == 0 and pre_ln.Bt % 32 == 0))
+            # (every condition stzs_ln_linear checks, csrc/lnrows.hip: a shape it refuses takes the two launches)
             if fused:
                 launch = lambda: self.lib.stzs_ln_linear(C.byref(a), C.byref(pre_ln), self.stream())
             else:
@@ -1296,7 +1300,8 @@ class StyleTTSZS:
         a.B, a.R, a.C, a.in_dtype, a.out_dtype = nb, R, Cn, dti, dto
         self._call(self.lib.stzs_copy2d, a, "copy_windows")
 
-    def decode_chunked(self, pro: dict, codes: torch.Tensor, seeds, chunk: int, halo: int, batch_windows=True):
+    def decode_chunked(self, pro: dict, codes: torch.Tensor, seeds, chunk: int, halo: int, batch_windows=True,
+                       max_pass_rows: int = 64):
         """configs[4] CHUNKED streaming decoder (oracle/stzs_ref.py decode_chunked): each chunk of `chunk` aligned
         frames is decoded over its fixed-length window (chunk_windows) -- pre-blocks and generator on the window alone,
         AdaIN with WINDOW-local InstanceNorm statistics -- on the slice of the whole utterance's harmonic-source
@@ -1305,7 +1310,11 @@ class StyleTTSZS:
         with batch_windows every later window is then decoded in ONE pass, the windows as the rows of one batch
         (window-major, [window][utterance]): every decoder kernel is batch-invariant (per-utterance tiles and
         statistics), so this is bit-identical to decoding them one by one (batch_windows=False), in 3 passes' worth of
-        launches instead of one per chunk.  Yields (first_sample, wav chunk [B, n]) views of one [B, 600 T40] buffer."""
+        launches instead of one per chunk.  A pass holds at most max(B, max_pass_rows) window rows (windows x utterances):
+        a pass's audio is ready only when the whole pass is decoded and its activations scale with its rows, so at large
+        B or long targets the later windows go in several passes (time to the second chunk ~ one pass's decode; peak
+        activation memory ~ max_pass_rows windows).  Yields (first_sample, wav chunk [B, n]) views of one [B, 600 T40]
+        buffer."""
         S = self.spec
         enc_in, F0, Nn, T40 = pro["asr_buf"], pro["F0"], pro["N"], pro["T40"]
         B = enc_in.B
@@ -1319,7 +1328,12 @@ class StyleTTSZS:
         wins = self.chunk_windows(T40, chunk, halo)
         Wn = wins[0][3] - wins[0][2]
         Tfw = fpf * Wn + 1
-        groups = ([[0], list(range(1, len(wins)))] if batch_windows else [[k] for k in range(len(wins))])
+        if batch_windows:
+            per = max(1, max_pass_rows // max(B, 1))  # windows per pass after the first
+            rest = list(range(1, len(wins)))
+            groups = [[0]] + [rest[i:i + per] for i in range(0, len(rest), per)]
+        else:
+            groups = [[k] for k in range(len(wins))]
         groups = [g for g in groups if g]
         F0c, Nc = F0.contiguous(), Nn.contiguous()
         cdt = L.F32 if codes.dtype == torch.float32 else L.BF16

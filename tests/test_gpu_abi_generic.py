@@ -1,15 +1,24 @@
 """The generic tensor-descriptor C-ABI on the GPU (include/stzs.h, csrc/abi.hip): each operator, fed the C++
 packers' weights, against the engine path it restates natively (bit-identical: same kernels, same arguments,
-bit-identical packed bytes) or against the oracle formula."""
+bit-identical packed bytes) or against the oracle formula; the composite operators (denoiser_fwd, decoder_pre,
+f0n_predictor) both ways: bit-identical to the engine AND within the stage bounds of the fp32 oracle."""
 import ctypes as C
 
 import numpy as np
 import pytest
 import torch
 
+from refops import rel_err
 from stzs import _lib as L
 
 pytestmark = pytest.mark.gpu
+
+# oracle parity of the composite operators (rel-L2, teacher-forced inputs), the stage bounds of
+# tests/test_gpu_configs.py: a single NFE against the sampler's bound, F0 / N against the predictor's; decoder_pre
+# (the generator input, 5 AdaIN blocks at 1024 channels in bf16) against the decoder waveform's 1.05e-1 halved
+TOL_SAMPLER = 1e-2
+TOL_F0, TOL_N = 1e-4, 4.5e-2
+TOL_DEC_PRE = 5e-2
 
 
 def _call(op, ins, outs, p, ws_bytes=None):
@@ -369,6 +378,13 @@ def test_generic_denoiser_fwd(gpu_device, tiny, tiny_params, spec, src, cfg, sig
     rc, short = _run_generic("denoiser_fwd", ins, [D], p)
     assert rc == L.OK and short == L.ESHAPE
     assert torch.equal(D, want), (D - want).abs().max().item()
+    # ... and against the fp32 oracle directly (same bf16-rounded text rows): one NFE at the sampler's stage bound
+    from oracle import stzs_ref as R
+    kv, pool = R.denoiser_context(P, S, h.float().cpu(), prompt.cpu(), cfg)
+    ref = R.denoiser(P, S, x.cpu(), sigma, kv, pool)
+    e = rel_err(D.cpu(), ref)
+    print(f"stzs_denoiser_fwd {spec} cfg={cfg} sigma={sigma}: rel-L2 vs oracle {e:.2e}")
+    assert e < TOL_SAMPLER
 
 
 @pytest.mark.parametrize("spec,src", CASES_SRC)
@@ -400,6 +416,11 @@ def test_generic_decoder_pre(gpu_device, tiny, tiny_params, spec, src):
     rc, short = _run_generic("decoder_pre", ins, [out], p)
     assert rc == L.OK and short == L.ESHAPE
     assert torch.equal(out, want)
+    from oracle import stzs_ref as R
+    ref = R.decoder_pre(P, S, asr.float().cpu(), F0.cpu(), Nn.cpu(), codes.cpu()).transpose(1, 2)
+    e = rel_err(out.float().cpu(), ref)
+    print(f"stzs_decoder_pre {spec}: rel-L2 vs oracle {e:.2e}")
+    assert e < TOL_DEC_PRE
 
 
 @pytest.mark.parametrize("spec,src", CASES_SRC)
@@ -435,3 +456,8 @@ def test_generic_f0n_predictor(gpu_device, tiny, tiny_params, spec, src, B):
     rc, short = _run_generic("f0n_predictor", ins, [F0, Nn, status], p)
     assert rc == L.OK and short == L.ESHAPE and int(status.item()) == 0
     assert torch.equal(F0, F0w) and torch.equal(Nn, Nw)
+    from oracle import stzs_ref as R
+    rF, rN = R.f0n_predictor(P, S, en.float().cpu(), codes.cpu())
+    eF, eN = rel_err(F0.cpu(), rF), rel_err(Nn.cpu(), rN)
+    print(f"stzs_f0n_predictor {spec} B={B}: F0 rel-L2 vs oracle {eF:.2e}, N {eN:.2e}")
+    assert eF < TOL_F0 and eN < TOL_N

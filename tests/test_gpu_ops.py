@@ -303,7 +303,7 @@ MRF_CASES = [
     (3, 400, 1090, 256, 3, 1, "leaky", True, False, True, 2),    # decoder block conv2: Ci 1090 (9 chunks), x2 shortcut
     (4, 200, 200, 96, 3, 1, "leaky", False, False, True, 1),     # predictor block conv1 (2 chunks, 1 column tile)
     (2, 300, 130, 64, 3, 1, "none", False, False, True, 1),      # up-block conv1 after the dw-ConvT: no prologue
-    # k3, one 128-channel chunk: the persistent LDS-DMA-pipelined kernel (csrc/mrfp.hip) under FRAG32
+    # k3, one 128-channel chunk (the stage-1 register-direct form, three workgroups per CU)
     (16, 24001, 128, 128, 3, 1, "snake", False, False, True, 1),  # stage-1 c1 shape: 3008 tiles, ~12 per CU
     (5, 24001, 128, 128, 3, 5, "snake", True, True, False, 1),    # stage-1 last c2 (residual + accumulate)
     (7, 3001, 128, 128, 3, 3, "snake", True, False, True, 1),     # c2 + stats, ragged last tile (3001 % 128)
@@ -311,7 +311,6 @@ MRF_CASES = [
     (3, 500, 128, 64, 3, 1, "leaky", True, False, True, 1),       # Co 64 (half the column tile), LeakyReLU
     (2, 333, 128, 128, 3, 2, "none", False, False, True, 1),      # no prologue
 ]
-PIPE_CASES = [c for c in MRF_CASES if c[2] == 128 and c[4] == 3 and c[7]]  # residual forms (csrc/mrfp.hip)
 
 
 def _run_mrf(eng, case, form, flags=0, ref=True):
@@ -401,19 +400,6 @@ def test_mrf_wide_bit_identical(eng, case):
     from stzs import _lib as L
     a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_NARROW, ref=False)
     b, sb, _ = _run_mrf(eng, case, "frag32", ref=False)
-    assert torch.equal(a, b)
-    if sa is not None:
-        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
-
-
-@pytest.mark.parametrize("case", PIPE_CASES)
-def test_mrf_pipelined_bit_identical(eng, case):
-    """the persistent LDS-DMA-pipelined k3 kernel (csrc/mrfp.hip, STZS_CONV_MRF_PIPE) vs the one-tile-per-
-    workgroup register-direct kernel (csrc/mrfv.hip, the FRAG32 default): same staged operands, same K order,
-    same statistics grouping -> outputs and statistics bit-identical."""
-    from stzs import _lib as L
-    a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRF_PIPE)
-    b, sb, _ = _run_mrf(eng, case, "frag32")
     assert torch.equal(a, b)
     if sa is not None:
         assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])

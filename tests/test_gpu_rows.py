@@ -70,12 +70,20 @@ def _run(eng, cw, x, res, ai, gate, N, odt, act, cs, rows):
     return y.t.clone()
 
 
-@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("Z", [1, 2, 4])
+# partial column tiles (N not a multiple of 64): the inactive waves of a 64-column rows16 K-slice tile still load
+# tile 0's weights and meet the barriers, and the `ct * 16 >= Co` returns after the hand-off run
+PARTIAL = [
+    ("p80", 512, 80, torch.bfloat16, torch.bfloat16, "none", False, False, 1.0),
+    ("p200", 512, 200, torch.bfloat16, torch.float32, "none", True, False, 1.0),
+    ("p16", 2048, 16, torch.bfloat16, torch.float32, "none", True, False, 1.0),
+]
+# (K split must give every wave the same K-step count: (K / 32) % (4 Z) == 0)
+RZ = [(c, Z) for c in CASES + PARTIAL for Z in (1, 2, 4) if (c[1] // 32) % (4 * Z) == 0]
+
+
+@pytest.mark.parametrize("case,Z", RZ, ids=[f"{c[0]}-{Z}" for c, Z in RZ])
 def test_rows_vs_torch(eng, case, Z):
     name, K, N, idt, odt, act, gated, acc, cs = case
-    if (K // 32) % (4 * Z):
-        pytest.skip("K split must give every wave the same K-step count")
     w, b, cw, x, res, ai, gate = _setup(eng, K, N, idt, odt, gated, acc, 100, K + N + Z)
     y = _run(eng, cw, x, res, ai, gate, N, odt, act, cs, Z).float().cpu()
     xa = (x.float() * cs).to(torch.bfloat16).float()
@@ -106,3 +114,26 @@ def test_rows_batch_invariant(eng, case):
         small = _run(eng, cw, x[sl], res[sl] if res is not None else None, ai[sl] if ai is not None else None,
                      gate[sl], N, odt, act, cs, Z)
         assert torch.equal(small, big[sl]), (name, lo, hi)
+
+
+@pytest.mark.parametrize("N,M", [(16, 50), (16, 100), (80, 100), (200, 50)])
+def test_rows_split_workspace_exact(eng, N, M):
+    """a C-ABI caller that sizes splitk_ws by stzs_conv_rows_workspace(M, Co, Z) exactly: both K-slice forms
+    (csrc/rows.hip and the rows16 split form of csrc/lnrows.hip) stay inside it (a guard region behind the
+    workspace is untouched) for Co % 64 in (0, 48], where rows16's 4-KB-per-(16 x 64 tile) slabs outgrow rows.hip's
+    layout (the header promised this size, the engine was only safe by its 4-MB minimum scratch)."""
+    K, Z = 512, 2
+    w, b, cw, x, res, ai, gate = _setup(eng, K, N, torch.bfloat16, torch.float32, True, False, M, N + M)
+    nb = eng.lib.stzs_conv_rows_workspace(M, N, Z)
+    assert nb > 0 and nb % 4 == 0
+    guard = 1 << 16
+    store = torch.full((nb // 4 + guard,), 12345.0, device=eng.device)
+    orig = eng._scratch
+    eng._scratch = lambda name, n: store if name.startswith("rows_ws") else orig(name, n)
+    try:
+        y = _run(eng, cw, x, res, ai, gate, N, torch.float32, "none", 1.0, Z).float().cpu()
+    finally:
+        eng._scratch = orig
+    assert bool((store[nb // 4:] == 12345.0).all()), "slab writes past stzs_conv_rows_workspace bytes"
+    ref = (x.float() @ w.to(torch.bfloat16).float().t() + b) * gate[:, None, :] + res.float()
+    assert ((y - ref).abs().max() / ref.abs().max()).item() < 1e-5

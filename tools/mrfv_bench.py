@@ -1,5 +1,4 @@
-"""Register-direct MRF conv (csrc/mrfv.hip, STZS_CONV_W_FRAG32), the persistent LDS-DMA-pipelined k3 residual
-form (csrc/mrfp.hip, + STZS_CONV_MRF_PIPE) and the LDS-ring MRF conv (csrc/mrf.hip, STZS_CONV_W_LANE16) on the generator shapes: bit-identity of outputs and fused statistics, then time per launch.
+"""Register-direct MRF conv (csrc/mrfv.hip, STZS_CONV_W_FRAG32) and the LDS-ring MRF conv (csrc/mrf.hip, STZS_CONV_W_LANE16) on the generator shapes: bit-identity of outputs and fused statistics, then time per launch.
 
     python tools/mrfv_bench.py            (env: B=64, CASES=0,1,2,..., FLAGS=0, REPS=5)
 """
@@ -47,8 +46,9 @@ for (T, C, k, dil) in cases:
     for variant in ("c1", "c2", "c2acc"):
         outs = {}
         forms = [("lane16", c16, 0), ("mrfv", cfr, 0)]
-        # single-chunk: the persistent form; two chunks: the narrow (128 channels per workgroup) register-direct form
-        forms.append(("mrfp", cfr, L.CONV_MRF_PIPE) if C == 128 else ("mrfvN", cfr, L.CONV_MRFV_NARROW))
+        # two chunks: also the narrow (128 channels per workgroup) register-direct form
+        if C != 128:
+            forms.append(("mrfvN", cfr, L.CONV_MRFV_NARROW))
         for name, cw, fl in forms:
             y = Act(torch.zeros(B, T, C, device=dev, dtype=torch.bfloat16))
             kw = dict(pad=dil * (k - 1) // 2, dil=dil, pro=(mean, rstd, C, gb.data_ptr(), 2 * C, C),
