@@ -15,10 +15,10 @@ pytestmark = pytest.mark.gpu
 
 # oracle parity of the composite operators (rel-L2, teacher-forced inputs), the stage bounds of
 # tests/test_gpu_configs.py: a single NFE against the sampler's bound, F0 / N against the predictor's; decoder_pre
-# (the generator input, 5 AdaIN blocks at 1024 channels in bf16) against the decoder waveform's 1.05e-1 halved
+# (the generator input, 5 AdaIN blocks at 1024 channels in bf16) at ~2x its measured error
 TOL_SAMPLER = 1e-2
 TOL_F0, TOL_N = 1e-4, 4.5e-2
-TOL_DEC_PRE = 5e-2
+TOL_DEC_PRE = 1.5e-2  # (measured r05_a: v0 6.9e-3, tiny 3.6e-3)
 
 
 def _call(op, ins, outs, p, ws_bytes=None):

@@ -11,3 +11,5 @@ timeout -k 10 500 python bench.py > gpurun_out/bench_$tag.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_$tag.log
 bash tools/prof.sh prof_$tag
 python3 tools/roofline_check.py gpurun_out/prof_$tag/run_kernel_trace.csv gpurun_out/prof_$tag.log > gpurun_out/roofline_check_$tag.json && cat gpurun_out/roofline_check_$tag.json
+[ -n "$PMC" ] && bash tools/pmc_bench.sh $tag
+exit 0

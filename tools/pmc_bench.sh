@@ -10,5 +10,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python3 bench.py --steps 1 --warmup 1 --no-cpu --no-latency --no-longform --no-precise --no-graph > $out/$c.log 2>&1 || { echo "PMC $c failed"; tail -5 $out/$c.log; exit 1; }
 done
 # written under gpurun_out/ so it travels back; copy it into profiles/ to publish it to bench.py
-# the 36 MRF resblock convs of a step: stage 0 on mrf_conv (mrf.hip), stage 1 on mrfv_conv (mrfv.hip), Snake prologue
-python3 tools/pmc_traffic.py $out "mrf_conv<2|mrfv_conv<2" > $out/${tag}_pmc_mrf.json && cat $out/${tag}_pmc_mrf.json
+# the 36 MRF resblock convs of a step (mrfv_conv, Snake prologue), per shape against their algorithmic bytes
+python3 tools/pmc_traffic.py $out "mrfv_conv<2" > $out/${tag}_pmc_mrf.json && cat $out/${tag}_pmc_mrf.json
