@@ -140,13 +140,14 @@ def longform(S, P, dev, runs=7):
     dur = torch.tensor([[3, 2] * (T // 2)], dtype=torch.int32).to(dev)
     nf = int(40 * 30)
 
-    def timed(halo):
+    def timed(halo, eng=None):
+        eng = e8 if eng is None else eng
         first, total = [], []
         for i in range(runs + 1):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             n = 0
-            for j, (_, w) in enumerate(e8.synth_stream(tok, ref, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps,
+            for j, (_, w) in enumerate(eng.synth_stream(tok, ref, steps=STEPS_THROUGHPUT, cfg_scale=CFG, noise=eps,
                                                        durations=dur, seeds=[3], n_frames=nf, chunk_s=1.0,
                                                        check=False, chunked_halo=halo)):
                 if j == 0:
@@ -164,12 +165,24 @@ def longform(S, P, dev, runs=7):
     f_c, t_c = timed(CHUNK_HALO)
     lstm_to = int(int(e8.status.item()) != 0)
     del e8
+    # the long-form mode at tolerance: fp8 sampler, precise text encoder / prosody predictor / decoder
+    # (StyleTTSZS(precise=True, fp8_denoiser=True); tests/test_gpu_stream.py::test_longform_30s_precise_prosody)
+    ep = StyleTTSZS(S, P, device=dev, precise=True, fp8_denoiser=True)
+    f_p, t_p = timed(None, ep)
+    lstm_to += int(int(ep.status.item()) != 0)
+    del ep
+    torch.cuda.empty_cache()
     return dict(lstm_timeouts=lstm_to, config="configs[4]: batch 1, 30-s target, 2-step CFG-5, fp8 e4m3 denoiser linears, "
                        "streaming iSTFT in 1-s chunks, eager", audio_s=30.0,
                 p50_first_chunk_ms=f_w, p50_total_ms=t_w, realtime_factor=round(30.0 / (t_w * 1e-3), 1),
                 chunked=dict(halo_frames=CHUNK_HALO, p50_first_chunk_ms=f_c, p50_total_ms=t_c,
                              note="chunked decoder (engine.decode_chunked): 1-s chunks decoded over +-halo windows with "
-                                  "window-local statistics; parity vs oracle decode_chunked (tests/test_gpu_stream.py)"))
+                                  "window-local statistics; parity vs oracle decode_chunked (tests/test_gpu_stream.py)"),
+                precise_prosody=dict(p50_first_chunk_ms=f_p, p50_total_ms=t_p,
+                                     realtime_factor=round(30.0 / (t_p * 1e-3), 1),
+                                     note="fp8 denoiser sampler, precise (split-operand, fp32 activations) text encoder, "
+                                          "prosody predictor and decoder: the configs[4] mode whose 30-s log-mel L1 "
+                                          "vs the oracle is flat per 5-s window (tests/test_gpu_stream.py)"))
 
 
 def gpu_ahead(ms=60.0):

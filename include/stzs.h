@@ -166,6 +166,14 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * 128 output channels per workgroup instead of its default wide form (256 per workgroup: every staged input row
  * transformed once per 256 channels instead of once per 128).  Bit-identical either way; an A/B switch. */
 #define STZS_CONV_MRFV_NARROW 8192
+/* flags: PRECISE register-direct form of the FRAG32 convs (csrc/mrfx.hip): the split-operand arithmetic of
+ * STZS_CONV_W_X3 (w * z = wl * zh + wh * zl + wh * zh, fp32 accumulate) with the data movement of STZS_CONV_W_FRAG32.
+ * w = per 32-wide K-step (loop order [co_pad/128][ci_pad/128][ks][4]) the hi then the lo fragment block
+ * [2][4 waves][2][64 lanes][8] bf16 of the STZS_CONV_W_FRAG32 layout (same frag32 row permutation; stzs/weights.py
+ * frag32x3_stream, STZS_PACK_FRAG32X3).  cic = 128, ks in {3, 7, 11} (Snake) or 3 (LeakyReLU / identity, no
+ * accumulate input), stride 1, fp32 x / y / res / acc_in (32-B aligned rows), Co % 8 == 0; the InstanceNorm
+ * statistics are those of the stored fp32 values. */
+#define STZS_CONV_W_FRAG32X3 16384
 /* bytes of splitk_ws for a K-sliced small-M linear over `rows` rows, Co columns, kgroups slices: covers both the
  * csrc/rows.hip form (STZS_CONV_ROWS) and the 16-row K-slice form of stzs_ln_linear (ln = NULL, splitk in {2, 4}) */
 size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);
@@ -518,7 +526,8 @@ typedef struct stzs_params_t {
 
 /* packed weight forms (host-side packers; stzs/weights.py pack_conv restated in C++) */
 enum { STZS_PACK_KSTEP = 0, STZS_PACK_LANE16 = 1, STZS_PACK_FRAG32 = 2, STZS_PACK_NARROW32 = 3,
-       STZS_PACK_X3 = 4 /* precise mode: hi | lo split streams, 32-channel K-steps (STZS_CONV_W_X3) */ };
+       STZS_PACK_X3 = 4 /* precise mode: hi | lo split streams, 32-channel K-steps (STZS_CONV_W_X3) */,
+       STZS_PACK_FRAG32X3 = 5 /* precise mode, register-direct: hi | lo FRAG32 blocks per K-step (STZS_CONV_W_FRAG32X3) */ };
 /* bytes of the packed bf16 form of a Conv1d weight [Co][Ci][ks] (ups = 0) or ConvTranspose1d weight [Ci][Co][2 ups]
  * (ups > 0, polyphase); 0 if the form does not apply to the shape */
 size_t stzs_pack_conv_size(int Co, int Ci, int ks, int ups, int form);

@@ -53,6 +53,9 @@ extern "C" size_t stzs_pack_conv_size(int Co, int Ci, int ks, int ups, int form)
                        ? (size_t)g.ks * g.co_pad * g.ci_pad * 2 : 0;
         case STZS_PACK_NARROW32: return (!ups && g.cic == 128 && Co <= 32) ? (size_t)g.ks * 32 * g.ci_pad * 2 : 0;
         case STZS_PACK_X3: return 2 * (size_t)g.ks * g.co_pad * g.ci_pad * 2;
+        case STZS_PACK_FRAG32X3:  // the precise register-direct convs (csrc/mrfx.hip): plain k 3 / 7 / 11 convs
+            return (!ups && g.cic == 128 && Co % 8 == 0 && (ks == 3 || ks == 7 || ks == 11))
+                       ? 2 * (size_t)g.ks * g.co_pad * g.ci_pad * 2 : 0;
         default: return 0;
     }
 }
@@ -98,21 +101,27 @@ extern "C" int stzs_pack_conv(const float* w, int Co, int Ci, int ks, int ups, i
                                 for (int e = 0; e < 8; ++e) o[n++] = h_bf16(W(tap, col, cc * g.cic + kq * 32 + c * 8 + e));
                             }
                         }
-    } else if (form == STZS_PACK_FRAG32) {
-        // [cot][chunk][tap][kq][w][nt][g][i][8]: packed row w*32 + nt*16 + i (frag32-permuted), channels kq*32 + 8g
+    } else if (form == STZS_PACK_FRAG32 || form == STZS_PACK_FRAG32X3) {
+        // [cot][chunk][tap][kq]([hl])[w][nt][g][i][8]: packed row w*32 + nt*16 + i (frag32-permuted), channels
+        // kq*32 + 8g; FRAG32X3: per K-step the hi block (bf16(w)) then the lo block (bf16(w - hi))
+        const int nhl = form == STZS_PACK_FRAG32X3 ? 2 : 1;
         size_t n = 0;
         for (int cot = 0; cot < ncot; ++cot)
             for (int cc = 0; cc < nchunk; ++cc)
                 for (int tap = 0; tap < g.ks; ++tap)
                     for (int kq = 0; kq < 4; ++kq)
-                        for (int wv = 0; wv < 4; ++wv)
-                            for (int nt = 0; nt < 2; ++nt)
-                                for (int gg = 0; gg < 4; ++gg)
-                                    for (int i = 0; i < 16; ++i) {
-                                        const int col = cot * 128 + frag32_row(wv * 32 + nt * 16 + i);
-                                        for (int e = 0; e < 8; ++e)
-                                            o[n++] = h_bf16(W(tap, col, cc * 128 + kq * 32 + gg * 8 + e));
-                                    }
+                        for (int hl = 0; hl < nhl; ++hl)
+                            for (int wv = 0; wv < 4; ++wv)
+                                for (int nt = 0; nt < 2; ++nt)
+                                    for (int gg = 0; gg < 4; ++gg)
+                                        for (int i = 0; i < 16; ++i) {
+                                            const int col = cot * 128 + frag32_row(wv * 32 + nt * 16 + i);
+                                            for (int e = 0; e < 8; ++e) {
+                                                const float v = W(tap, col, cc * 128 + kq * 32 + gg * 8 + e);
+                                                const uint16_t hi = h_bf16(v);
+                                                o[n++] = hl ? h_bf16(v - h_f32(hi)) : hi;
+                                            }
+                                        }
     } else {  // NARROW32: [cc][tap][kq][32 rows][4 positions x 8], rows narrow32-permuted, same swizzle
         size_t n = 0;
         for (int cc = 0; cc < nchunk; ++cc)

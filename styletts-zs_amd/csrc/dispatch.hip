@@ -7,8 +7,23 @@
 int stzs_conv1d_core(const stzs_conv_args* a, void* stream);           // csrc/conv.hip
 int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/mrfv.hip
 int stzs_rows_gemm_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/rows.hip
+int stzs_mrfx_conv_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/mrfx.hip
 
 extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
+    if (a && (a->flags & STZS_CONV_W_FRAG32X3)) {  // the precise register-direct form
+        if (!a->x || !a->w || !a->y) return STZS_EINVAL;
+        if (a->flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 | STZS_CONV_W_F32 | STZS_CONV_W_X3 | STZS_CONV_A_DMA |
+                        STZS_CONV_W_FRAG32 | STZS_CONV_ROWS | STZS_CONV_UPS_NOISE))
+            return STZS_EINVAL;
+        if (a->B <= 0 || a->T_in <= 0 || a->T_out <= 0 || a->Ci <= 0 || a->Co <= 0 || a->dil <= 0) return STZS_ESHAPE;
+        if (a->ci_pad < a->Ci || a->co_pad < a->Co || a->ldx < ((a->Ci + 7) / 8) * 8) return STZS_ESHAPE;
+        if (!stzs_aligned(a->w, 16)) return STZS_EINVAL;
+        if (a->pro_mode == STZS_PRO_ADAIN && (!a->pro_mean || !a->pro_rstd || !a->pro_gb)) return STZS_EINVAL;
+        if (a->in_dtype == STZS_F8 || a->x_scale) return STZS_EDTYPE;
+        if (a->splitk > 1) return STZS_EINVAL;
+        if (a->stat_part && !stzs_aligned(a->stat_part, 8)) return STZS_EINVAL;
+        return stzs_mrfx_conv_launch(*a, reinterpret_cast<hipStream_t>(stream));
+    }
     if (a && (a->flags & STZS_CONV_W_FRAG32)) {
         if (!a->x || !a->w || !a->y) return STZS_EINVAL;
         if (a->flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 | STZS_CONV_W_F32 | STZS_CONV_A_DMA))

@@ -134,16 +134,23 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
             }
             auto stage = [&](auto full_tag) {
                 constexpr bool FULL = decltype(full_tag)::value;
-                float4 raw[SB][2];
+                // row vectors loaded per group: all of them when the accumulators are not live (one chunk), half
+                // otherwise (the multi-chunk forms stage chunk 2 beside 64 live accumulators)
+                constexpr int G = NCH == 1 ? SB : (SB + 1) / 2;
+                float4 raw[G][2];
+                auto load_group = [&](int i0) {
 #pragma unroll
-                for (int i = 0; i < SB; ++i) {  // 32-bit offsets from the utterance base (SGPR)
-                    int tin = t0 - a.pad + rsub + 16 * i;
-                    if constexpr (!FULL) tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
-                    const unsigned off = (unsigned)(tin * (int)a.ldx + cl) * 4u;
-                    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(X) + off);
-                    raw[i][0] = p[0];
-                    raw[i][1] = p[1];
-                }
+                    for (int i = 0; i < G; ++i) {  // 32-bit offsets from the utterance base (SGPR)
+                        if (i0 + i >= SB) break;
+                        int tin = t0 - a.pad + rsub + 16 * (i0 + i);
+                        if constexpr (!FULL) tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+                        const unsigned off = (unsigned)(tin * (int)a.ldx + cl) * 4u;
+                        const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(X) + off);
+                        raw[i][0] = p[0];
+                        raw[i][1] = p[1];
+                    }
+                };
+                load_group(0);
                 __syncthreads();  // constants visible
                 float ksc[8], ksh[8], kar[8], kia[8];
 #pragma unroll
@@ -158,9 +165,11 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
                 const float slope = a.pro_slope;
 #pragma unroll
                 for (int i = 0; i < SB; ++i) {
+                    if (i > 0 && i % G == 0) load_group(i);
                     const int r = rsub + 16 * i;
-                    const float xin[8] = {raw[i][0].x, raw[i][0].y, raw[i][0].z, raw[i][0].w,
-                                          raw[i][1].x, raw[i][1].y, raw[i][1].z, raw[i][1].w};
+                    const int ig = i % G;
+                    const float xin[8] = {raw[ig][0].x, raw[ig][0].y, raw[ig][0].z, raw[ig][0].w,
+                                          raw[ig][1].x, raw[ig][1].y, raw[ig][1].z, raw[ig][1].w};
                     float z[8];
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
@@ -197,12 +206,16 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
         }
         __syncthreads();
         // K loop: no barrier.  K-step s = tap * 4 + kq reads input rows t + tap dil, channels kq * 32 ..
+        // (the lane index laundered per chunk: otherwise hipcc hoists all NKC fragment offsets out of the chunk loop
+        // of the multi-chunk forms and keeps them live -- 15-27 VGPRs spilled at k7 / k11)
+        int lr = lane & 15;
+        asm volatile("" : "+v"(lr));
         auto kloop = [&](auto first_tag) {
             constexpr bool FIRST = decltype(first_tag)::value;
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
             auto frag_off = [&](int s) {  // byte offset of this lane's B fragment (row tile 0) at K-step s
                 const int tap = s >> 2, kq = s & 3;
-                const int r = (lane & 15) + tap * dil;
+                const int r = lr + tap * dil;
                 return r * PX + ((((kq << 2) + g4) ^ (r & 15)) << 4);
             };
             {

@@ -26,6 +26,7 @@ CONV_LINEAR_IDS = 128  # include/stzs.h STZS_CONV_LINEAR_IDS (diagnostic: no XCD
 CONV_ROWS = 2048  # include/stzs.h STZS_CONV_ROWS (small-M linear on the whole chip, csrc/rows.hip)
 CONV_UPS_NOISE = 4096  # include/stzs.h STZS_CONV_UPS_NOISE (ConvTranspose + fused 1x1 noise conv, csrc/ups.hip)
 CONV_MRFV_NARROW = 8192  # include/stzs.h STZS_CONV_MRFV_NARROW (register-direct MRF conv at 128 channels per workgroup)
+CONV_W_FRAG32X3 = 16384  # include/stzs.h STZS_CONV_W_FRAG32X3 (precise register-direct MRF conv, csrc/mrfx.hip)
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -166,7 +167,7 @@ class Params(C.Structure):
     _fields_ = [("i", i32 * 16), ("f", f32 * 8)]
 
 
-PACK_KSTEP, PACK_LANE16, PACK_FRAG32, PACK_NARROW32, PACK_X3 = 0, 1, 2, 3, 4
+PACK_KSTEP, PACK_LANE16, PACK_FRAG32, PACK_NARROW32, PACK_X3, PACK_FRAG32X3 = 0, 1, 2, 3, 4, 5
 GENERIC_OPS = ["cfg_euler_step", "duration_head", "length_regulate", "sine_gen", "conv_post_istft", "bilstm",
                "conv_transpose_up", "mrf_resblock", "denoiser_fwd", "decoder_pre", "f0n_predictor"]
 # input-list layouts of the composite generic operators (include/stzs.h STZS_DN_* / STZS_DP_* / STZS_FN_*)

@@ -171,21 +171,27 @@ class StyleTTSZS:
         self.spec = spec
         self.fp8_denoiser = fp8_denoiser
         precise_decoder = precise_decoder or precise
-        assert not (precise and fp8_denoiser), "precise mode keeps every linear at ~fp32 accuracy"
         self.precise = precise_decoder
         self.precise_all = precise
+        # precise + fp8_denoiser: the configs[4] long-form mode -- the style sampler on the fp8 denoiser (bf16
+        # activations), text encoder / prosody predictor / decoder precise (the F0 phase the harmonic source
+        # integrates over 30 s needs the predictor's fp32-level F0: DESIGN.md §3)
+        self.lowp_dn = bool(precise and fp8_denoiser)
         self.dec_dt = torch.float32 if precise_decoder else torch.bfloat16
-        self.adt = torch.float32 if precise else torch.bfloat16  # text / sampler / predictor activations
+        self.adt = torch.float32 if precise else torch.bfloat16  # text / predictor activations
+        self.sdt = torch.bfloat16 if self.lowp_dn else self.adt  # style-sampler activations
         self.device = torch.device(device)
         self.lib = L.load()
         L.check(self.lib.stzs_init(self.device.index or 0), "stzs_init")
         if packed is not None:
             assert packed.spec == spec and packed.arena.buf.device == self.device and \
-                packed.precise == precise_decoder and packed.precise_all == precise, \
+                packed.precise == precise_decoder and packed.precise_all == precise and \
+                getattr(packed, "lowp_denoiser", False) == self.lowp_dn, \
                 "packed model: spec / device / precise mode differ"
             self.W = packed
         else:
-            self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder, precise_all=precise)
+            self.W = PackedModel(spec, params, self.device, fill=fill, precise=precise_decoder, precise_all=precise,
+                                 lowp_denoiser=self.lowp_dn)
         self._bufs = {}
         self._retired = []
         self._consts = {}
@@ -224,6 +230,9 @@ class StyleTTSZS:
         # the first stage's strided noise conv on super-rows of the harmonic source (register-direct kernel, bf16
         # engines); STZS_NOISE_SUPER=0: the stride-6 conv_mfma form
         self.noise_super = os.environ.get("STZS_NOISE_SUPER", "1") != "0"
+        # precise mode: the FRAG32 convs (MRF, AdaIN-block k3) on the split-operand register-direct kernel
+        # (csrc/mrfx.hip) instead of the LDS-ring conv_x3; STZS_MRFX=0: conv_x3
+        self.mrfx = os.environ.get("STZS_MRFX", "1") != "0"
         # diagnostic conv flag bits ORed into every stzs_conv1d call (e.g. STZS_CONV_LINEAR_IDS = 128)
         self.conv_flags = int(os.environ.get("STZS_CONV_FLAGS", "0"), 0)
         # device status word collecting the LSTM exchange's spin-timeout flag over every launch (eager or
@@ -360,7 +369,14 @@ class StyleTTSZS:
                 and cscale == 1.0 and x.t.dtype in (torch.bfloat16, torch.float8_e4m3fn)
                 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
-        if cw.wx3 is not None:  # precise mode: split bf16 operands (csrc/conv.hip conv_x3)
+        if (getattr(cw, "fx3", None) is not None and self.mrfx and x.t.dtype == torch.float32 and
+                y.t.dtype == torch.float32 and stride == 1 and not cw.ups and epi_act == L.ACT_NONE and gate is None and
+                (pro_act == L.ACT_SNAKE or (cw.ks == 3 and acc_in is None)) and
+                (res is None or res.t.dtype == torch.float32) and x.ptr % 32 == 0 and y.ptr % 32 == 0):
+            # precise mode, register-direct: split bf16 operands on the mrfv data movement (csrc/mrfx.hip)
+            a.w, a.cic = self._t(cw.fx3).data_ptr(), 128
+            flags = (flags & ~8) | L.CONV_W_FRAG32X3
+        elif cw.wx3 is not None:  # precise mode: split bf16 operands (csrc/conv.hip conv_x3)
             a.w, a.cic = self._t(cw.wx3).data_ptr(), 32
             flags = (flags & ~8) | L.CONV_W_X3
         elif cw.w32 is not None:  # fp32 operands on fp32 MFMA (csrc/conv.hip conv_f32)
@@ -749,6 +765,10 @@ class StyleTTSZS:
         cfg = cfg_scale != 1.0
         R = 2 * B if cfg else B
         sig = sigma_schedule(S, steps)
+        if h_txt.t.dtype != self.sdt:  # (the long-form mode: precise fp32 text rows into the bf16 / fp8 sampler)
+            hs = self.act("dn.h_txt", B, h_txt.T, h_txt.C, self.sdt)
+            self.copy2d(h_txt, hs, h_txt.T, h_txt.C)
+            h_txt = hs
         st = self.denoiser_prepare(h_txt, prompt, sig[:steps], cfg)
         x = self.buf("dn.x", (R, S.L_s, S.code_dim), torch.float32)
         N = S.L_s * S.code_dim
@@ -783,14 +803,14 @@ class StyleTTSZS:
         Ls, d, cd = S.L_s, S.dn_d, S.code_dim
         Lc = T + Ls
         steps = len(sigmas)
-        ctx = self.act("dn.ctx", R, Lc, d, self.adt)
+        ctx = self.act("dn.ctx", R, Lc, d, self.sdt)
         # ctx_txt rows: the conv writes T rows per utterance into a buffer of Lc rows per utterance
         self._conv_rows(W.dn_ctx_txt, h_txt, ctx.t, 0, 0, "dn.ctx_txt")
         pa = Act(prompt)
         self._conv_rows(W.dn_ctx_prm, pa, ctx.t, 0, T, "dn.ctx_prm")
         if cfg:
             self._conv_rows(W.dn_ctx_txt, h_txt, ctx.t, B, 0, "dn.ctx_txt.u")
-            f32 = self.adt == torch.float32
+            f32 = self.sdt == torch.float32
             nul = Act(W.t(W.dn_ctx_null32 if f32 else W.dn_ctx_null)[None])
             dst = Act(ctx.t[B:]).rows(0, B)
             a = L.CopyArgs()
@@ -809,7 +829,7 @@ class StyleTTSZS:
             self._call(self.lib.stzs_copy2d, a, "pool_null")
         kv = []
         for l, lw in enumerate(W.dn_layers):
-            kvl = self.act(f"dn.kv{l}", R, Lc, 2 * d, self.adt)
+            kvl = self.act(f"dn.kv{l}", R, Lc, 2 * d, self.sdt)
             self.conv(lw["kv"], ctx, kvl, what=f"dn.kv{l}")
             kv.append(kvl)
         # sigma embeddings for all steps
@@ -822,7 +842,7 @@ class StyleTTSZS:
         temb = self.act("dn.temb", 1, steps, d, torch.float32)
         self.conv(W.dn_t0, Act(fo), t0, epi_act=L.ACT_SILU, rows=self._rows_z(W.dn_t0), what="dn.t0")
         self.conv(W.dn_t1, t0, temb, rows=self._rows_z(W.dn_t1), what="dn.t1")
-        cb = self.buf("dn.cb", (steps * R, d), self.adt)
+        cb = self.buf("dn.cb", (steps * R, d), self.sdt)
         mod = self.buf("dn.mod", (steps * R, 6 * d), torch.float32)
         fmod = self.buf("dn.fmod", (steps * R, 2 * d), torch.float32)
         modx = self.buf("dn.modx", (S.dn_layers, steps * R, 6 * d), torch.float32)
@@ -846,11 +866,11 @@ class StyleTTSZS:
         R, kv, modx, fmodx = st["R"], st["kv"], st["modx"], st["fmodx"]
         Ls, d = S.L_s, S.dn_d
         h = self.act("dn.h", R, Ls, d, torch.float32)
-        an = self.act("dn.a", R, Ls, d, self.adt)
-        qkv = self.act("dn.qkv", R, Ls, 3 * d, self.adt)
-        o = self.act("dn.o", R, Ls, d, self.adt)
-        q = self.act("dn.q", R, Ls, d, self.adt)
-        ff = self.act("dn.ff", R, Ls, S.dn_ffn, self.adt)
+        an = self.act("dn.a", R, Ls, d, self.sdt)
+        qkv = self.act("dn.qkv", R, Ls, 3 * d, self.sdt)
+        o = self.act("dn.o", R, Ls, d, self.sdt)
+        q = self.act("dn.q", R, Ls, d, self.sdt)
+        ff = self.act("dn.ff", R, Ls, S.dn_ffn, self.sdt)
         pos = Act(W.t(W.dn_pos)[None])
         fsz = 4
         f8 = self.fp8_denoiser
@@ -862,7 +882,7 @@ class StyleTTSZS:
             s_o = self.buf("dn.o8s", (R * Ls,), torch.float32)
             s_ff = self.buf("dn.ff8s", (R * Ls,), torch.float32)
         co = edm_coeffs(S, st["sig"][i])
-        rk = {} if (f8 or self.adt == torch.float32) else self.dn_rows
+        rk = {} if (f8 or self.sdt == torch.float32) else self.dn_rows
         if f8:
             ain, sin, sfx = an8, s_an, "8"
         else:
@@ -887,7 +907,7 @@ class StyleTTSZS:
         post = lambda k: None if fl else lns[k]
         pre = lambda k: lns[k] if fl else None
         self.conv(W.dn_in, xa, h, cscale=co["c_in"], res=pos, rows=rk.get("inp", 0), post_ln=post(0), what="dn.in")
-        sk = {} if (f8 or self.adt == torch.float32) else self.dn_splitk
+        sk = {} if (f8 or self.sdt == torch.float32) else self.dn_splitk
         for l, lw in enumerate(W.dn_layers):
             mb = modx[l, i * R].data_ptr()
             self.conv(lw["qkv" + sfx], ain, qkv, x_scale=sin, splitk=sk.get("qkv", 0), rows=rk.get("qkv", 0),

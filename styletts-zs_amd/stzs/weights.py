@@ -49,6 +49,7 @@ class ConvW:
     w32: Optional[object] = None  # fp32 K-step stream (STZS_CONV_W_F32, conv_f32), unpermuted
     frag32: bool = False  # fragment-order packing of the register-direct MRF kernel (STZS_CONV_W_FRAG32)
     wx3: Optional[object] = None  # precise mode: hi | lo bf16 K-step streams (STZS_CONV_W_X3, conv_x3), unpermuted
+    fx3: Optional[object] = None  # precise mode, register-direct: hi | lo FRAG32 blocks per K-step (STZS_CONV_W_FRAG32X3)
     nz32: Optional[object] = None  # fused noise conv (STZS_CONV_UPS_NOISE): its fp32 weights [Co][32]
 
 
@@ -161,6 +162,17 @@ def frag32_stream(wp: torch.Tensor) -> torch.Tensor:
     return t.reshape(co_pad // 128, -1, 8).contiguous()
 
 
+def frag32x3_stream(wp: torch.Tensor) -> torch.Tensor:
+    """[ks, co_pad, ci_pad] fp32 (rows already frag32-permuted) -> [co_pad/128, NK * 1024, 8] bf16: per 32-wide
+    K-step (the frag32_stream order) the hi fragment block [4 waves][2][64 lanes][8] of bf16(w), then the lo block of
+    bf16(w - hi) -- one K-step of both halves adjacent for the precise register-direct kernel (csrc/mrfx.hip,
+    include/stzs.h STZS_CONV_W_FRAG32X3)."""
+    hi, lo = split_bf16(wp)
+    h = frag32_stream(hi.float()).view(wp.shape[1] // 128, -1, 512, 8)
+    l = frag32_stream(lo.float()).view(wp.shape[1] // 128, -1, 512, 8)
+    return torch.stack([h, l], 2).reshape(wp.shape[1] // 128, -1, 8).to(torch.bfloat16)
+
+
 def narrow32_stream(wp: torch.Tensor, cic: int) -> torch.Tensor:
     """[ks, 32, ci_pad] -> [NK, 32, 32] K-steps for the narrow conv (csrc/mrf.hip narrow_conv): packed row
     rr = nt*16 + g*4 + r holds output channel g*8 + nt*4 + r; 16-B chunks XOR-swizzled as kstep_stream."""
@@ -215,7 +227,9 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, frag32_perm()].reshape(ks, co_pad, ci_pad)
         wn = A.add(name + ".wfr", frag32_stream(wp).to(torch.bfloat16))
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, w32=w32, frag32=True, wx3=wx3)
+        # the precise register-direct form (csrc/mrfx.hip) of the plain convs
+        fx3 = A.add(name + ".wfx3", frag32x3_stream(wp)) if (x3 and not ups) else None
+        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, w32=w32, frag32=True, wx3=wx3, fx3=fx3)
     if lane16:
         assert cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
@@ -435,10 +449,12 @@ def pack_blk(A: Arena, P, name, up=False, x3=False) -> BlkW:
 class PackedModel:
     """All hot-path weights of spec v0 in kernel layouts, resident in one device arena."""
 
-    def __init__(self, spec: Spec, P, device, fill=True, precise=False, precise_all=False):
+    def __init__(self, spec: Spec, P, device, fill=True, precise=False, precise_all=False, lowp_denoiser=False):
         """precise: also pack the split-operand (hi | lo) streams of every decoder conv (StyleTTSZS(
         precise_decoder=True)); precise_all: of every conv, linear and LSTM of the pipeline except the
-        reference-prompt front end, whose output is quantised to discrete codes (StyleTTSZS(precise=True))."""
+        reference-prompt front end, whose output is quantised to discrete codes (StyleTTSZS(precise=True)).
+        lowp_denoiser (with precise_all): the denoiser's linears without the split streams -- the configs[4]
+        long-form mode StyleTTSZS(precise=True, fp8_denoiser=True): fp8 sampler, precise text / prosody / decoder."""
         S = self.spec = spec
         xd = precise or precise_all
         xa = precise_all
@@ -468,28 +484,30 @@ class PackedModel:
         self.pe_vq = A.add("pe.vq", P["pe.vq"].float())  # [G][K][dg] codebooks (stzs_code_quantize)
         # --- denoiser ---
         L = lambda n: pack_conv(A, n, P[n + ".w"], P[n + ".b"], x3=xa)
-        self.dn_in = L("dn.in_proj")
+        xdn = xa and not lowp_denoiser
+        Ld = lambda n: pack_conv(A, n, P[n + ".w"], P[n + ".b"], x3=xdn)
+        self.dn_in = Ld("dn.in_proj")
         self.dn_pos = A.add("dn.pos", P["dn.pos"].float())
-        self.dn_t0, self.dn_t1 = L("dn.t_mlp0"), L("dn.t_mlp1")
-        self.dn_pool = L("dn.pool_proj")
-        self.dn_ctx_txt, self.dn_ctx_prm = L("dn.ctx_txt"), L("dn.ctx_prm")
-        self.dn_ada = L("dn.ada")
+        self.dn_t0, self.dn_t1 = Ld("dn.t_mlp0"), Ld("dn.t_mlp1")
+        self.dn_pool = Ld("dn.pool_proj")
+        self.dn_ctx_txt, self.dn_ctx_prm = Ld("dn.ctx_txt"), Ld("dn.ctx_prm")
+        self.dn_ada = Ld("dn.ada")
         self.dn_table = A.add("dn.ada_table", P["dn.ada_table"].float())
-        self.dn_final_ada = L("dn.final_ada")
-        self.dn_out = L("dn.out")
+        self.dn_final_ada = Ld("dn.final_ada")
+        self.dn_out = Ld("dn.out")
         # constant unconditional-branch context: null codes through ctx_prm / pool_proj (fp32, once)
         null = P["dn.null_codes"].float()
         ctx_null = null @ P["dn.ctx_prm.w"].t() + P["dn.ctx_prm.b"]
         pool_null = null.mean(0) @ P["dn.pool_proj.w"].t() + P["dn.pool_proj.b"]
         self.dn_ctx_null = A.add("dn.ctx_null", ctx_null.to(torch.bfloat16))
         self.dn_pool_null = A.add("dn.pool_null", pool_null.float())
-        self.dn_ctx_null32 = A.add("dn.ctx_null32", ctx_null.float()) if xa else None
+        self.dn_ctx_null32 = A.add("dn.ctx_null32", ctx_null.float()) if xdn else None
         self.dn_layers = []
         for l in range(S.dn_layers):
             p = f"dn.l{l}"
             self.dn_layers.append(dict(
-                qkv=L(p + ".sa_qkv"), o=L(p + ".sa_o"), q=L(p + ".ca_q"), kv=L(p + ".ca_kv"), co=L(p + ".ca_o"),
-                ff1=L(p + ".ff1"), ff2=L(p + ".ff2"),
+                qkv=Ld(p + ".sa_qkv"), o=Ld(p + ".sa_o"), q=Ld(p + ".ca_q"), kv=Ld(p + ".ca_kv"), co=Ld(p + ".ca_o"),
+                ff1=Ld(p + ".ff1"), ff2=Ld(p + ".ff2"),
                 ln_g=A.add(p + ".ca_ln.g", P[p + ".ca_ln.g"]), ln_b=A.add(p + ".ca_ln.b", P[p + ".ca_ln.b"])))
             # fp8 e4m3fn copies of the per-layer linears (configs[4]: StyleTTSZS(fp8_denoiser=True))
             for key, n in (("qkv", ".sa_qkv"), ("o", ".sa_o"), ("q", ".ca_q"), ("co", ".ca_o"), ("ff1", ".ff1"),
@@ -581,6 +599,7 @@ class PackedModel:
         self.device = device
         self.precise = precise
         self.precise_all = precise_all
+        self.lowp_denoiser = bool(lowp_denoiser and precise_all)
 
     def t(self, name):
         return self.arena[name]

@@ -62,6 +62,27 @@ def test_pack_conv_x3_matches_python(Co, Ci, ks, ups):
     assert out.tobytes() == want
 
 
+@pytest.mark.parametrize("Co,Ci,ks", [(128, 128, 3), (256, 256, 11), (176, 256, 7), (64, 130, 3)])
+def test_pack_conv_frag32x3_matches_python(Co, Ci, ks):
+    """the precise register-direct split stream (hi | lo FRAG32 blocks per K-step, csrc/mrfx.hip) bit-identical to
+    stzs/weights.py frag32x3_stream."""
+    from stzs.weights import Arena, pack_conv
+    lib = L.load()
+    g = torch.Generator().manual_seed(Co + 5 * Ci + ks)
+    w = torch.randn(Co, Ci, ks, generator=g) / math.sqrt(Ci * ks)
+    A = Arena()
+    cw = pack_conv(A, "t", w, None, frag32=True, x3=True)
+    A.finalize("cpu")
+    want = A[cw.fx3].contiguous().view(torch.uint8).numpy().tobytes()
+    n = lib.stzs_pack_conv_size(Co, Ci, ks, 0, L.PACK_FRAG32X3)
+    assert n == len(want)
+    out = np.zeros(n, dtype=np.uint8)
+    wc = np.ascontiguousarray(w.numpy(), dtype=np.float32)
+    assert lib.stzs_pack_conv(wc.ctypes.data, Co, Ci, ks, 0, L.PACK_FRAG32X3, out.ctypes.data) == L.OK
+    assert out.tobytes() == want
+    assert lib.stzs_pack_conv_size(22, 128, 7, 0, L.PACK_FRAG32X3) == 0  # Co % 8
+
+
 def test_pack_lstm_x3_matches_python(tiny_params):
     from stzs.weights import Arena, pack_lstm
     lib = L.load()

@@ -12,6 +12,7 @@ teacher-forced decoder log-mel L1 <= 1e-3 (north star) and waveform rel-L2 <= 1e
 inputs at v0, and a 4-utterance 2-step batch) log-mel L1 <= 1e-3 (north star), prompt codes teacher-forced
 (the bf16 front end's output is a discrete decision, as durations elsewhere).
 """
+import ctypes as C
 import math
 
 import pytest
@@ -157,6 +158,120 @@ def test_conv_x3_kernel(gpu_device, B, T, Ci, Co, k, dil, stride, ups, act):
     e = max_rel(out, ref)
     print("conv_x3", B, T, Ci, Co, k, dil, stride, ups, act, f"{e:.2e}")
     assert e < 4e-5
+
+
+# the precise register-direct conv (csrc/mrfx.hip, STZS_CONV_W_FRAG32X3): B, T, Ci, Co, k, dil, act, residual,
+# accumulate, statistics, res_tdiv -- stage-1 shapes (one 128-channel chunk; 128-row tiles up to a 146-row halo, 64-row
+# tiles beyond: k7 d5, k11 d3 / d5), stage-0 shapes (two chunks), the AdaIN-block k3 forms (LeakyReLU / identity,
+# Ci 1090 = 9 chunks with Ci < ci_pad, x2 shortcut residual), ragged last tiles, Co < co_pad
+MRFX_CASES = [
+    (3, 1000, 128, 128, 3, 1, "snake", False, False, True, 1),
+    (2, 777, 128, 128, 7, 3, "snake", True, False, True, 1),     # 146-row halo: the largest 128-row tile
+    (2, 1001, 128, 128, 7, 5, "snake", True, True, False, 1),    # 64-row tiles, residual + accumulate
+    (2, 500, 128, 128, 11, 5, "snake", False, False, True, 1),   # 64-row tiles, 178-row halo -> 114
+    (3, 333, 128, 128, 11, 1, "snake", True, True, True, 1),
+    (2, 400, 256, 256, 11, 3, "snake", True, False, True, 1),    # stage-0 width: 2 chunks, 64-row tiles
+    (2, 400, 256, 256, 3, 1, "snake", True, True, True, 1),
+    (1, 129, 256, 176, 7, 1, "snake", False, False, True, 1),    # ragged: 1 valid row in the 2nd tile; Co < co_pad
+    (3, 400, 1090, 256, 3, 1, "leaky", True, False, True, 2),    # decoder block conv2: 9 chunks, x2 shortcut
+    (2, 300, 130, 64, 3, 1, "none", False, False, True, 1),      # up-block conv1 after the dw-ConvT: no prologue
+]
+
+
+@pytest.mark.parametrize("case", MRFX_CASES)
+def test_mrfx_kernel(gpu_device, case):
+    """the precise register-direct conv (csrc/mrfx.hip) with the AdaIN + Snake / LeakyReLU / identity prologue,
+    residual (at t / res_tdiv) / alpha / accumulate epilogue and fused statistics vs an fp64 torch reference of the
+    same conv (prologue in fp64 too): max-abs 4e-5 of max|ref| (the conv_x3 bound: split products drop al*bl, ~2^-16
+    relative each; the Snake's hardware sine is fp32-level); statistics of the stored fp32 output 1e-5.  Also against
+    conv_x3 on the same operands (same arithmetic, another K order): 4e-5."""
+    from stzs import _lib as L
+    from stzs.engine import Act, StyleTTSZS
+    from stzs.params import init_params
+    from stzs.spec import SPEC_TINY
+    from stzs.weights import Arena, pack_conv
+    B, T, Ci, Co, k, dil, act, hr, ha, st, tdiv = case
+    eng = StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, seed=0), device=gpu_device)
+    g = torch.Generator().manual_seed(B * T + Ci + k + dil)
+    pad = dil * (k - 1) // 2
+    x = torch.randn(B, T, Ci, generator=g)
+    w = torch.randn(Co, Ci, k, generator=g) / math.sqrt(Ci * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    mean = torch.randn(B, Ci, generator=g) * 0.1
+    rstd = torch.rand(B, Ci, generator=g) + 0.5
+    gb = torch.randn(B, 2 * Ci, generator=g) * 0.2
+    alpha = torch.rand(Ci, generator=g) + 0.5
+    res = torch.randn(B, (T + tdiv - 1) // tdiv, Co, generator=g) if hr else None
+    acc = torch.randn(B, T, Co, generator=g) if ha else None
+    osc = 1 / 3 if ha else (0.7071 if hr else 1.0)
+    xd = x.double().transpose(1, 2)
+    if act != "none":
+        sc = ((1 + gb[:, :Ci].double()) * rstd.double())[:, :, None]
+        xd = xd * sc + (gb[:, Ci:].double()[:, :, None] - mean.double()[:, :, None] * sc)
+    if act == "snake":
+        a_ = alpha.double()[None, :, None]
+        xd = xd + torch.sin(a_ * xd) ** 2 / a_
+    elif act == "leaky":
+        xd = F.leaky_relu(xd, 0.2)
+    ref = F.conv1d(xd, w.double(), b.double(), padding=pad, dilation=dil).transpose(1, 2)
+    if hr:
+        ref = ref + res.double().repeat_interleave(tdiv, 1)[:, :T]
+    ref = ref * osc
+    if ha:
+        ref = ref + acc.double()
+    A = Arena()
+    cw = pack_conv(A, "t", w, b, frag32=True, x3=True)
+    A.finalize(gpu_device)
+    cw.w, cw.wx3, cw.fx3, cw.b = A[cw.w], A[cw.wx3], A[cw.fx3], A[cw.b]
+    ld = (Ci + 7) // 8 * 8
+    xt = torch.zeros(B, T, ld, device=gpu_device)
+    xt[:, :, :Ci] = x.to(gpu_device)
+    keep = [mean.to(gpu_device), rstd.to(gpu_device), gb.to(gpu_device), alpha.to(gpu_device)]
+    pro = None if act == "none" else (keep[0], keep[1], Ci, keep[2].data_ptr(), 2 * Ci, Ci)
+    pa = {"snake": L.ACT_SNAKE, "leaky": L.ACT_LEAKY, "none": L.ACT_NONE}[act]
+    outs = []
+    for mrfx in (True, False):
+        eng.mrfx = mrfx
+        y = Act(torch.zeros(B, T, Co, device=gpu_device))
+        rd = Act(res.to(gpu_device)) if hr else None
+        ad = Act(acc.to(gpu_device)) if ha else None
+        n0 = eng.launches
+        o = eng.conv(cw, Act(xt, 0, Ci), y, pad=pad, dil=dil, pro=pro, pro_act=pa, pro_slope=0.2,
+                     pro_alpha=keep[3] if act == "snake" else None, res=rd, res_tdiv=tdiv, alpha=osc, acc_in=ad,
+                     beta=1.0, stats_key="t.mrfx" if st else None, what="mrfx")
+        torch.cuda.synchronize()
+        outs.append((y.t.double().cpu(), (o[1][0].clone().cpu(), o[1][1].clone().cpu()) if st else None))
+    got, stats = outs[0]
+    e = max_rel(got, ref)
+    e_x3 = max_rel(got, outs[1][0])
+    print("mrfx", case, f"max-rel vs fp64 {e:.2e}, vs conv_x3 {e_x3:.2e}")
+    assert e < 4e-5 and e_x3 < 4e-5
+    if st:
+        m, r = stats
+        mr, vr = got.mean(1), got.var(1, unbiased=False)
+        assert float(((m.double() - mr).abs() / (mr.abs() + vr.sqrt())).max()) < 1e-5
+        assert max_rel(r.double(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
+
+
+def test_mrfx_is_the_precise_path(gpu_device):
+    """the precise engine routes its FRAG32 convs to the register-direct split-operand kernel: a stage-1 MRF conv shape
+    returns STZS_OK through STZS_CONV_W_FRAG32X3, and the form refuses bf16 operands (ESHAPE before any launch)."""
+    from stzs import _lib as L
+    lib = L.load()
+    a = L.ConvArgs()
+    x = torch.zeros(1, 300, 128, device=gpu_device)
+    y = torch.zeros(1, 300, 128, device=gpu_device)
+    wt = torch.zeros(3 * 4 * 1024 * 8, dtype=torch.bfloat16, device=gpu_device)
+    a.x, a.w, a.y = x.data_ptr(), wt.data_ptr(), y.data_ptr()
+    a.ldx, a.bsx, a.ldy, a.bsy = 128, 300 * 128, 128, 300 * 128
+    a.B, a.T_in, a.T_out, a.Ci, a.Co, a.ks, a.dil, a.stride, a.pad = 1, 300, 300, 128, 128, 3, 1, 1, 1
+    a.ci_pad, a.co_pad, a.cic, a.in_dtype, a.out_dtype = 128, 128, 128, L.F32, L.F32
+    a.pro_act, a.pro_cscale, a.alpha, a.flags = L.ACT_NONE, 1.0, 1.0, L.CONV_W_FRAG32X3
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.stzs_conv1d(C.byref(a), s) == L.OK
+    torch.cuda.synchronize()
+    a.in_dtype = L.BF16
+    assert lib.stzs_conv1d(C.byref(a), s) == L.ESHAPE
 
 
 def _lstm_ref64(x, P, name):
