@@ -53,8 +53,8 @@ extern "C" size_t stzs_pack_conv_size(int Co, int Ci, int ks, int ups, int form)
                        ? (size_t)g.ks * g.co_pad * g.ci_pad * 2 : 0;
         case STZS_PACK_NARROW32: return (!ups && g.cic == 128 && Co <= 32) ? (size_t)g.ks * 32 * g.ci_pad * 2 : 0;
         case STZS_PACK_X3: return 2 * (size_t)g.ks * g.co_pad * g.ci_pad * 2;
-        case STZS_PACK_FRAG32X3:  // the precise register-direct convs (csrc/mrfx.hip): plain k 3 / 7 / 11 convs
-            return (!ups && g.cic == 128 && Co % 8 == 0 && (ks == 3 || ks == 7 || ks == 11))
+        case STZS_PACK_FRAG32X3:  // the precise register-direct convs (csrc/mrfx.hip): k 3 / 7 / 11 convs, k 1 linears
+            return (!ups && g.cic == 128 && Co % 8 == 0 && (ks == 1 || ks == 3 || ks == 7 || ks == 11))
                        ? 2 * (size_t)g.ks * g.co_pad * g.ci_pad * 2 : 0;
         default: return 0;
     }

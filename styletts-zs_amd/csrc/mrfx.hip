@@ -363,6 +363,209 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// FLAT linears of the precise pipeline (ks 1, no prologue but pro_cscale): 128 consecutive rows of the [B * T] row
+// space per tile, the same split-operand K loop over 128-channel chunks (4 K-steps each), and the next chunk's fp32
+// rows loaded into registers while the current chunk's K loop runs (every row a tile stages is a whole 512-B row
+// piece: no halo).  Epilogue of the linears (csrc/conv_common.hpp epilogue, FLAT): bias, GELU / SiLU, the DiT gate of
+// the row's utterance, residual, alpha, beta * acc_in; fp32 out.
+template <int EACT, bool GATE, bool HR, bool HA>
+__global__ __launch_bounds__(NTH, 2) void mrfx_lin(const stzs_conv_args a) {
+    constexpr int BT = 128, MT = 8, NKC = 4, SB = 8;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* const thi = smem;
+    constexpr int lo_off = BT * PX;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nx = gridDim.x;
+    const int lin = (a.flags & STZS_CONV_LINEAR_IDS) ? blockIdx.y * nx + blockIdx.x
+                                                      : xcd_remap(blockIdx.y * nx + blockIdx.x, nx * gridDim.y);
+    const int by = lin / nx, bx = lin - by * nx;
+    const long nR = (long)a.B * a.T_in;
+    const long row0 = (long)bx * BT;
+    const int nchunk = a.ci_pad >> 7;
+    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + ((long)by * nchunk * NKC) * 1024 + wave * 128 + lane;
+    auto wload = [&](bf16x8 (&w)[4], int kk) {
+        const bf16x8* p = Wf + (long)kk * 1024;
+        w[0] = p[0];
+        w[1] = p[64];
+        w[2] = p[512];
+        w[3] = p[576];
+    };
+    const float* X = reinterpret_cast<const float*>(a.x);
+    const int cv = tid & 15, rsub = tid >> 4;
+    const int g4 = lane >> 4;
+    // the A rows: flat row R -> utterance R / T_in, step R % T_in (any batch stride); rows past nR are clamped here and
+    // zeroed in the transform
+    const float invTi = 1.f / (float)a.T_in;
+    unsigned xoff[SB];  // element offsets (the launcher checks B * bsx < 2^31)
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+        long R = row0 + rsub + 16 * i;
+        R = R < nR ? R : nR - 1;
+        const int q = (int)((float)(int)R * invTi);
+        int qq = q, rr = (int)R - q * a.T_in;
+        if (rr < 0) { --qq; rr += a.T_in; } else if (rr >= a.T_in) { ++qq; rr -= a.T_in; }
+        xoff[i] = (unsigned)(qq * (int)a.bsx + rr * (int)a.ldx);
+    }
+    float4 raw[SB][2];
+    auto load_chunk = [&](int cc) {
+        const int c = cc * 128 + cv * 8;
+        const int cl = c < a.Ci ? c : 0;
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+            const float4* p = reinterpret_cast<const float4*>(X + xoff[i] + cl);
+            raw[i][0] = p[0];
+            raw[i][1] = p[1];
+        }
+    };
+    f32x4 acc[2][MT];
+    bf16x8 wf[2][4];
+    bf16x8 xh[MT], xl[MT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    load_chunk(0);
+    const float csc = a.pro_cscale;
+    for (int cc = 0; cc < nchunk; ++cc) {
+        const int kb = cc * NKC;
+        wload(wf[0], kb);
+        __syncthreads();  // every wave is done reading the previous chunk's tiles
+        {
+            const bool c_ok = cc * 128 + cv * 8 < a.Ci;
+#pragma unroll
+            for (int i = 0; i < SB; ++i) {
+                const int r = rsub + 16 * i;
+                const bool ok = c_ok && row0 + r < nR;
+                const float xin[8] = {raw[i][0].x, raw[i][0].y, raw[i][0].z, raw[i][0].w,
+                                      raw[i][1].x, raw[i][1].y, raw[i][1].z, raw[i][1].w};
+                float z[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) z[j] = ok ? xin[j] * csc : 0.f;
+                uint4 hi, lo;
+                split8(z, hi, lo);
+                const int o = r * PX + ((cv ^ (r & 15)) << 4);
+                *reinterpret_cast<uint4*>(thi + o) = hi;
+                *reinterpret_cast<uint4*>(thi + lo_off + o) = lo;
+            }
+        }
+        if (cc + 1 < nchunk) load_chunk(cc + 1);  // the next chunk's rows fly during this chunk's K loop
+        __syncthreads();
+        int lr = lane & 15;
+        asm volatile("" : "+v"(lr));
+        auto frag_off = [&](int s) { return lr * PX + (((s << 2) + g4) ^ lr) * 16; };
+        {
+            const int o = frag_off(0);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                xh[mt] = *reinterpret_cast<const bf16x8*>(thi + o + mt * 16 * PX);
+                xl[mt] = *reinterpret_cast<const bf16x8*>(thi + lo_off + o + mt * 16 * PX);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NKC; ++s) {
+            if (s + 1 < NKC) wload(wf[(s + 1) & 1], kb + s + 1);
+            const int on = s + 1 < NKC ? frag_off(s + 1) : 0;
+            const bf16x8* w = wf[s & 1];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[j][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2 + j], xh[mt], acc[j][mt], 0, 0, 0);
+                    acc[j][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j], xl[mt], acc[j][mt], 0, 0, 0);
+                    acc[j][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j], xh[mt], acc[j][mt], 0, 0, 0);
+                }
+                if (s + 1 < NKC) {
+                    xh[mt] = *reinterpret_cast<const bf16x8*>(thi + on + mt * 16 * PX);
+                    xl[mt] = *reinterpret_cast<const bf16x8*>(thi + lo_off + on + mt * 16 * PX);
+                }
+            }
+            if (s + 1 < NKC) __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+                if (s + 1 < NKC) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (a.flags & 4) return;
+
+    // ---------------- epilogue: lane (g, n): flat row row0 + mt*16 + n, channels co0 .. co0 + 7 (fp32)
+    const int g = lane >> 4, n = lane & 15;
+    const int co0 = by * BCO + wave * 32 + g * 8;
+    if (co0 >= a.Co) return;
+    float bias[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[co0 + i] : 0.f;
+    const float invTo = 1.f / (float)a.T_out;
+    const bool gvec = GATE && (reinterpret_cast<uintptr_t>(a.gate) & 15) == 0 && a.gate_bs % 4 == 0;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const long R = row0 + mt * 16 + n;
+        if (R >= nR) continue;
+        const long q = (long)(int)((float)(int)R * invTo);
+        long b = q, t = R - q * a.T_out;
+        if (t < 0) { --b; t += a.T_out; } else if (t >= a.T_out) { ++b; t -= a.T_out; }
+        float v[8];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[nt * 4 + r] = acc[nt][mt][r] + bias[nt * 4 + r];
+        if constexpr (EACT == STZS_ACT_GELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = 0.5f * v[i] * (1.f + erff(v[i] * 0.70710678118654752f));
+        } else if constexpr (EACT == STZS_ACT_SILU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = v[i] / (1.f + expf(-v[i]));
+        }
+        if constexpr (GATE) {
+            const float* gp = a.gate + b * a.gate_bs + co0;
+            float gv[8];
+            if (gvec) {
+                load8(gp, gv);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) gv[i] = gp[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] *= gv[i];
+        }
+        if constexpr (HR) {
+            float f[8];
+            load8(reinterpret_cast<const float*>(a.res) + b * a.bsr + t * a.ldr + co0, f);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] += f[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] *= a.alpha;
+        if constexpr (HA) {
+            float f[8];
+            load8(reinterpret_cast<const float*>(a.acc_in) + b * a.bsa + t * a.lda + co0, f);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = fmaf(a.beta, f[i], v[i]);
+        }
+        store8(reinterpret_cast<float*>(a.y) + b * a.bsy + t * a.ldy + co0, v);
+    }
+}
+
+template <int EACT>
+void (*pick_lin_e(bool g, bool r, bool h))(stzs_conv_args) {
+    if (g) return r ? (h ? mrfx_lin<EACT, true, true, true> : mrfx_lin<EACT, true, true, false>)
+                    : (h ? mrfx_lin<EACT, true, false, true> : mrfx_lin<EACT, true, false, false>);
+    return r ? (h ? mrfx_lin<EACT, false, true, true> : mrfx_lin<EACT, false, true, false>)
+             : (h ? mrfx_lin<EACT, false, false, true> : mrfx_lin<EACT, false, false, false>);
+}
+void (*pick_lin(const stzs_conv_args& a))(stzs_conv_args) {
+    const bool g = a.gate != nullptr, r = a.res != nullptr, h = a.acc_in != nullptr;
+    switch (a.epi_act) {
+        case STZS_ACT_NONE: return pick_lin_e<STZS_ACT_NONE>(g, r, h);
+        case STZS_ACT_GELU: return pick_lin_e<STZS_ACT_GELU>(g, r, h);
+        case STZS_ACT_SILU: return pick_lin_e<STZS_ACT_SILU>(g, r, h);
+        default: return nullptr;
+    }
+}
+
 template <int PACT, bool HR, bool HA, int BT, int NCH, bool AL>
 void (*pick_ks(int ks))(stzs_conv_args) {
     switch (ks) {
@@ -398,8 +601,30 @@ void (*pick_form(const stzs_conv_args& a))(stzs_conv_args) {
 
 }  // namespace
 
+// the precise FLAT linear (ks 1): validated and launched by stzs_mrfx_conv_launch
+static int mrfx_lin_launch(const stzs_conv_args& a, hipStream_t s) {
+    if (a.pad || a.stride != 1 || a.T_in != a.T_out || a.pro_mode != STZS_PRO_NONE || a.pro_act != STZS_ACT_NONE ||
+        a.stat_part || a.ups || a.refl || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO ||
+        a.in_dtype != STZS_F32 || a.out_dtype != STZS_F32 || a.ldx % 8 || a.bsx % 8 || a.ldy % 8 || a.bsy % 8 ||
+        (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv != 1)) || (a.acc_in && (a.lda % 8 || a.bsa % 8)) ||
+        (long)a.B * a.T_in >= (1L << 22) - 256 || (long)a.B * a.bsx >= (1L << 31))
+        return STZS_ESHAPE;
+    if (!stzs_aligned(a.x, 32) || !stzs_aligned(a.y, 32) || (a.res && !stzs_aligned(a.res, 32)) ||
+        (a.acc_in && !stzs_aligned(a.acc_in, 32)))
+        return STZS_EINVAL;
+    void (*k)(stzs_conv_args) = pick_lin(a);
+    if (!k) return STZS_EINVAL;
+    const size_t lds = (size_t)2 * 128 * PX;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dim3 grid((unsigned)(((long)a.B * a.T_in + 127) / 128), a.co_pad / BCO);
+    hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
 // internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32X3 weights (csrc/dispatch.hip)
 __attribute__((visibility("hidden"))) int stzs_mrfx_conv_launch(const stzs_conv_args& a, hipStream_t s) {
+    if (a.ks == 1) return mrfx_lin_launch(a, s);
     if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || a.ups || a.refl || a.gate ||
         a.in_dtype != STZS_F32 || a.out_dtype != STZS_F32 || a.epi_act != STZS_ACT_NONE || a.ldx % 8 || a.bsx % 8 ||
         a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv <= 0)) ||

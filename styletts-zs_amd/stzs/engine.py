@@ -369,11 +369,15 @@ class StyleTTSZS:
                 and cscale == 1.0 and x.t.dtype in (torch.bfloat16, torch.float8_e4m3fn)
                 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
+        fx3_conv = (cw.ks in (3, 7, 11) and epi_act == L.ACT_NONE and gate is None and
+                    (pro_act == L.ACT_SNAKE or (cw.ks == 3 and acc_in is None)))
+        fx3_lin = (cw.ks == 1 and pad == 0 and pro is None and pro_act == L.ACT_NONE and stats_key is None and
+                   a.T_out == x.T and epi_act in (L.ACT_NONE, L.ACT_GELU, L.ACT_SILU) and res_tdiv == 1)
         if (getattr(cw, "fx3", None) is not None and self.mrfx and x.t.dtype == torch.float32 and
-                y.t.dtype == torch.float32 and stride == 1 and not cw.ups and epi_act == L.ACT_NONE and gate is None and
-                (pro_act == L.ACT_SNAKE or (cw.ks == 3 and acc_in is None)) and
+                y.t.dtype == torch.float32 and stride == 1 and not cw.ups and (fx3_conv or fx3_lin) and
                 (res is None or res.t.dtype == torch.float32) and x.ptr % 32 == 0 and y.ptr % 32 == 0):
-            # precise mode, register-direct: split bf16 operands on the mrfv data movement (csrc/mrfx.hip)
+            # precise mode, register-direct: split bf16 operands on the mrfv data movement (csrc/mrfx.hip; the linears
+            # on its FLAT form mrfx_lin)
             a.w, a.cic = self._t(cw.fx3).data_ptr(), 128
             flags = (flags & ~8) | L.CONV_W_FRAG32X3
         elif cw.wx3 is not None:  # precise mode: split bf16 operands (csrc/conv.hip conv_x3)
@@ -418,7 +422,7 @@ class StyleTTSZS:
             a.splitk, a.splitk_ws = splitk, self._scratch("sk_ws", nb // 4).data_ptr()
             a.splitk_ctr = self._counters("sk_ctr", nb // (splitk * 32768)).data_ptr()
         elif (splitk > 1 and not (a.flags & (8 | L.CONV_ROWS | L.CONV_W_X3 | L.CONV_W_F32 | L.CONV_W_FRAG32 |
-                                             L.CONV_W_LANE16 | L.CONV_W_NARROW32)) and not cw.f8):
+                                             L.CONV_W_LANE16 | L.CONV_W_NARROW32 | L.CONV_W_FRAG32X3)) and not cw.f8):
             # conv_mfma split over input-channel chunks: one 64-KB fp32 slab per (128-row tile, slice) + a ticket
             # per tile (grid.x is at most B x ceil(T_out / 128))
             tiles = x.B * ((a.T_out + 127) // 128) * (cw.co_pad // 128)

@@ -230,13 +230,18 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
         # the precise register-direct form (csrc/mrfx.hip) of the plain convs
         fx3 = A.add(name + ".wfx3", frag32x3_stream(wp)) if (x3 and not ups) else None
         return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, w32=w32, frag32=True, wx3=wx3, fx3=fx3)
+    # the precise register-direct FLAT linear (csrc/mrfx.hip mrfx_lin): ks 1, 128-channel chunks
+    fx3 = None
+    if x3 and ks == 1 and not ups and cic == 128 and Co % 8 == 0:
+        wf = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, frag32_perm()].reshape(ks, co_pad, ci_pad)
+        fx3 = A.add(name + ".wfx3", frag32x3_stream(wf))
     if lane16:
         assert cic == 128 and Co % 16 == 0, (name, Ci, Co)
         perm = lane16_perm()
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, perm].reshape(ks, co_pad, ci_pad)
     wn = A.add(name + ".wpk", kstep_stream(wp, cic).to(torch.bfloat16))
     bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16, w32=w32, wx3=wx3)
+    return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, lane16, w32=w32, wx3=wx3, fx3=fx3)
 
 
 def noise_super_weights(wn: torch.Tensor, s: int, ld: int) -> torch.Tensor:

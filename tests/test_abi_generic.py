@@ -62,7 +62,8 @@ def test_pack_conv_x3_matches_python(Co, Ci, ks, ups):
     assert out.tobytes() == want
 
 
-@pytest.mark.parametrize("Co,Ci,ks", [(128, 128, 3), (256, 256, 11), (176, 256, 7), (64, 130, 3)])
+@pytest.mark.parametrize("Co,Ci,ks", [(128, 128, 3), (256, 256, 11), (176, 256, 7), (64, 130, 3), (1536, 512, 1),
+                                      (2048, 640, 1)])
 def test_pack_conv_frag32x3_matches_python(Co, Ci, ks):
     """the precise register-direct split stream (hi | lo FRAG32 blocks per K-step, csrc/mrfx.hip) bit-identical to
     stzs/weights.py frag32x3_stream."""
@@ -71,7 +72,7 @@ def test_pack_conv_frag32x3_matches_python(Co, Ci, ks):
     g = torch.Generator().manual_seed(Co + 5 * Ci + ks)
     w = torch.randn(Co, Ci, ks, generator=g) / math.sqrt(Ci * ks)
     A = Arena()
-    cw = pack_conv(A, "t", w, None, frag32=True, x3=True)
+    cw = pack_conv(A, "t", w[:, :, 0] if ks == 1 else w, None, frag32=ks > 1, x3=True)
     A.finalize("cpu")
     want = A[cw.fx3].contiguous().view(torch.uint8).numpy().tobytes()
     n = lib.stzs_pack_conv_size(Co, Ci, ks, 0, L.PACK_FRAG32X3)

@@ -253,6 +253,71 @@ def test_mrfx_kernel(gpu_device, case):
         assert max_rel(r.double(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
 
 
+# FLAT linears of the precise pipeline (csrc/mrfx.hip mrfx_lin): rows, T per utterance, K, N, epilogue act, gate,
+# residual (broadcast over utterances = the positional table), accumulate, cscale
+MRFX_LIN_CASES = [
+    (6400, 50, 512, 1536, "none", False, False, False, 1.0),   # qkv at batch 64 (CFG-doubled)
+    (6400, 50, 2048, 512, "none", True, True, False, 1.0),     # ff2: K 2048 (16 chunks), gate + residual
+    (300, 50, 512, 2048, "gelu", False, False, False, 1.0),    # ff1 (300 rows: a ragged last tile)
+    (100, 50, 256, 512, "none", False, "bcast", False, 0.37),  # dn.in: cscale = c_in, the positional rows as residual
+    (250, 50, 512, 256, "none", False, False, True, 1.0),      # dn.out: alpha c_out, beta c_skip accumulate
+    (173, 173, 640, 2048, "none", False, False, False, 1.0),   # an LSTM input projection (In 640 = 5 chunks), T 173
+    (64, 1, 128, 600, "silu", False, False, False, 1.0),       # a per-utterance linear (one row each), Co % 128 != 0
+]
+
+
+@pytest.mark.parametrize("case", MRFX_LIN_CASES)
+def test_mrfx_linear(gpu_device, case):
+    """the precise FLAT linear (csrc/mrfx.hip mrfx_lin: split bf16 operands, fp32 rows in and out, the next chunk's rows
+    in flight during the K loop) vs an fp64 torch reference: max-abs 4e-5 of max|ref| (the conv_x3 bound)."""
+    from stzs import _lib as L
+    from stzs.engine import Act, StyleTTSZS
+    from stzs.params import init_params
+    from stzs.spec import SPEC_TINY
+    from stzs.weights import Arena, pack_conv
+    R, T, K, N, act, gated, res, acc, cs = case
+    B = R // T
+    eng = StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, seed=0), device=gpu_device)
+    g = torch.Generator().manual_seed(R + K + N)
+    x = torch.randn(B, T, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g) * 0.1
+    gate = torch.rand(B, N, generator=g) + 0.5
+    rv = torch.randn(1 if res == "bcast" else B, T, N, generator=g) if res else None
+    av = torch.randn(B, T, N, generator=g) if acc else None
+    ref = (x.double() * cs) @ w.double().t() + b.double()
+    if act == "gelu":
+        ref = F.gelu(ref)
+    elif act == "silu":
+        ref = F.silu(ref)
+    if gated:
+        ref = ref * gate.double()[:, None, :]
+    if res:
+        ref = ref + rv.double()
+    alpha, beta = (0.75, 1.25) if acc else (1.0, 0.0)
+    ref = ref * alpha
+    if acc:
+        ref = ref + beta * av.double()
+    A = Arena()
+    cw = pack_conv(A, "t", w, b, x3=True)
+    A.finalize(gpu_device)
+    cw.w, cw.wx3, cw.fx3, cw.b = A[cw.w], A[cw.wx3], A[cw.fx3], A[cw.b]
+    outs = []
+    for mrfx in (True, False):
+        eng.mrfx = mrfx
+        y = Act(torch.zeros(B, T, (N + 7) // 8 * 8, device=gpu_device), 0, N)
+        gd = gate.to(gpu_device)
+        eng.conv(cw, Act(x.to(gpu_device)), y, cscale=cs,
+                 epi_act={"none": L.ACT_NONE, "gelu": L.ACT_GELU, "silu": L.ACT_SILU}[act],
+                 gate=gd.data_ptr() if gated else None, gate_bs=N, res=Act(rv.to(gpu_device)) if res else None,
+                 acc_in=Act(av.to(gpu_device)) if acc else None, alpha=alpha, beta=beta, what="mrfx_lin")
+        torch.cuda.synchronize()
+        outs.append(y.t[:, :, :N].double().cpu())
+    e, e_x3 = max_rel(outs[0], ref), max_rel(outs[0], outs[1])
+    print("mrfx_lin", case, f"max-rel vs fp64 {e:.2e}, vs conv_x3 {e_x3:.2e}")
+    assert e < 4e-5 and e_x3 < 4e-5
+
+
 def test_mrfx_is_the_precise_path(gpu_device):
     """the precise engine routes its FRAG32 convs to the register-direct split-operand kernel: a stage-1 MRF conv shape
     returns STZS_OK through STZS_CONV_W_FRAG32X3, and the form refuses bf16 operands (ESHAPE before any launch)."""
