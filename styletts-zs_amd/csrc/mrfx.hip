@@ -63,9 +63,11 @@ STZS_DEV void split8(const float* z, uint4& hi, uint4& lo) {
 
 // NCH = 1: one 128-channel input chunk (the stage-1 generator convs); 0: any number (accumulators live across chunks).
 // AL: the epilogue scales by a.alpha.  BT: 128 or 64 time rows per tile.
-template <int PACT, bool HR, bool HA, int KS, int BT, int NCH, bool AL>
+// NW (narrow, Co <= 32: conv_post 128 -> 22): the 4 waves split the tile's ROWS (32 each) and all compute output
+// channels 0..31 from packed wave 0's fragments; no statistics, masked stores past Co.
+template <int PACT, bool HR, bool HA, int KS, int BT, int NCH, bool AL, bool NW = false>
 __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
-    constexpr int MT = BT / 16;   // 16-row B fragments per wave
+    constexpr int MT = NW ? BT / 64 : BT / 16;  // 16-row B fragments per wave
     constexpr int NKC = KS * 4;   // 32-wide K-steps per 128-channel chunk
     constexpr int SB = sb_rows(KS, BT);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -84,7 +86,9 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
     const int t0 = (bx - bq * tpb) * BT;
     const int nchunk = NCH ? NCH : a.ci_pad >> 7;
     // weights: [co tile][chunk][tap][kq][hl][wave][nt][lane][8] bf16 -> 1024 bf16x8 per K-step
-    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + ((long)by * nchunk * NKC) * 1024 + wave * 128 + lane;
+    const bf16x8* Wf = reinterpret_cast<const bf16x8*>(a.w) + ((long)by * nchunk * NKC) * 1024 + (NW ? 0 : wave * 128) +
+                       lane;
+    const int wrow = NW ? wave * (BT / 4) : 0;  // this wave's first tile row
     auto wload = [&](bf16x8 (&w)[4], int kk) {  // [0, 1] hi of row tiles 0, 1; [2, 3] lo
         const bf16x8* p = Wf + (long)kk * 1024;
         w[0] = p[0];
@@ -216,7 +220,7 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
             auto frag_off = [&](int s) {  // byte offset of this lane's B fragment (row tile 0) at K-step s
                 const int tap = s >> 2, kq = s & 3;
                 const int r = lr + tap * dil;
-                return r * PX + ((((kq << 2) + g4) ^ (r & 15)) << 4);
+                return (wrow + r) * PX + ((((kq << 2) + g4) ^ (r & 15)) << 4);
             };
             {
                 const int o = frag_off(0);
@@ -278,20 +282,22 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
     const float* Aq = reinterpret_cast<const float*>(a.acc_in) + (long)bq * a.bsa;
     float* Y = reinterpret_cast<float*>(a.y) + (long)bq * a.bsy;
     const int nch = (a.T_out + 63) / 64;
-    const int co0 = by * BCO + wave * 32 + g * 8;
+    const int co0 = by * BCO + (NW ? 0 : wave * 32) + g * 8;
     const bool col_ok = co0 < a.Co;
     const int coc = col_ok ? co0 : 0;
+    const int ncv = a.Co - co0 < 8 ? a.Co - co0 : 8;  // valid channels of this lane's group (NW: Co % 8 != 0)
     float bias[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
-    constexpr int NH = MT / 4;  // 64-row halves: one statistics partial each
+    for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[(NW && i >= ncv) ? coc : coc + i] : 0.f;
+    constexpr int MH = MT < 4 ? MT : 4;  // row tiles per epilogue pass
+    constexpr int NH = MT / MH;          // (BT >= 64, not NW: 64-row halves, one statistics partial each)
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
         // this half's residual / accumulate rows in flight at once (32-B fp32 row vectors)
-        float4 rr[4][2], aa[4][2];
+        float4 rr[MH][2], aa[MH][2];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int t = t0 + (h * 4 + m) * 16 + n;
+        for (int m = 0; m < MH; ++m) {
+            const int t = t0 + wrow + (h * MH + m) * 16 + n;
             const int tc = t < a.T_out ? t : a.T_out - 1;
             if constexpr (HR) {
                 const int tr = TD1 ? tc : tc / a.res_tdiv;
@@ -309,9 +315,9 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int mt = h * 4 + m;
-            const int t = t0 + mt * 16 + n;
+        for (int m = 0; m < MH; ++m) {
+            const int mt = h * MH + m;
+            const int t = t0 + wrow + mt * 16 + n;
             const bool ok = col_ok && t < a.T_out;
             float v[8];
 #pragma unroll
@@ -335,9 +341,15 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
                 for (int i = 0; i < 8; ++i) v[i] = fmaf(a.beta, f[i], v[i]);
             }
             if (ok) {
-                float4* p = reinterpret_cast<float4*>(Y + (long)t * a.ldy + coc);
-                p[0] = make_float4(v[0], v[1], v[2], v[3]);
-                p[1] = make_float4(v[4], v[5], v[6], v[7]);
+                if (!NW || ncv == 8) {
+                    float4* p = reinterpret_cast<float4*>(Y + (long)t * a.ldy + coc);
+                    p[0] = make_float4(v[0], v[1], v[2], v[3]);
+                    p[1] = make_float4(v[4], v[5], v[6], v[7]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (i < ncv) Y[(long)t * a.ldy + coc + i] = v[i];
+                }
             }
             if (stat && ok) {
 #pragma unroll
@@ -347,7 +359,7 @@ __global__ __launch_bounds__(NTH, 2) void mrfx_conv(const stzs_conv_args a) {
                 }
             }
         }
-        if (stat) {
+        if (!NW && stat) {
             row_sum16_n<8>(ss);
             row_sum16_n<8>(sq);
             const int r0 = t0 + h * 64;
@@ -625,7 +637,11 @@ static int mrfx_lin_launch(const stzs_conv_args& a, hipStream_t s) {
 // internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32X3 weights (csrc/dispatch.hip)
 __attribute__((visibility("hidden"))) int stzs_mrfx_conv_launch(const stzs_conv_args& a, hipStream_t s) {
     if (a.ks == 1) return mrfx_lin_launch(a, s);
-    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || a.ups || a.refl || a.gate ||
+    // conv_post (128 -> 22, k7, LeakyReLU(0.01), fp32 out): the narrow form, waves split the rows
+    const bool narrow = a.Co <= 32 && a.ci_pad == 128 && a.ks == 7 && !a.res && !a.acc_in && !a.stat_part &&
+                        a.pro_mode == STZS_PRO_NONE && a.pro_act == STZS_ACT_LEAKY && a.alpha == 1.f &&
+                        128 + 6 * a.dil <= 16 * sb_rows(7, 128);
+    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || (a.Co % 8 && !narrow) || a.co_pad % BCO || a.ups || a.refl || a.gate ||
         a.in_dtype != STZS_F32 || a.out_dtype != STZS_F32 || a.epi_act != STZS_ACT_NONE || a.ldx % 8 || a.bsx % 8 ||
         a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv <= 0)) ||
         (a.acc_in && (a.lda % 8 || a.bsa % 8)) || (a.stat_part && a.stat_ld < a.Co) ||
@@ -646,11 +662,12 @@ __attribute__((visibility("hidden"))) int stzs_mrfx_conv_launch(const stzs_conv_
         bt = 64;
     if (!bt) return STZS_ESHAPE;
     void (*k)(stzs_conv_args) = bt == 128 ? pick_form<128>(a) : pick_form<64>(a);
+    if (narrow) k = mrfx_conv<STZS_ACT_LEAKY, false, false, 7, 128, 1, false, true>;
     if (!k) return STZS_ESHAPE;
     const int rows_in = bt + (ks - 1) * a.dil;
     const size_t lds = (size_t)2 * rows_in * PX + NCS * 128 * 4;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + bt - 1) / bt), a.co_pad / BCO);
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + bt - 1) / bt), narrow ? 1u : (unsigned)(a.co_pad / BCO));
     hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;

@@ -370,7 +370,9 @@ class StyleTTSZS:
                 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
         fx3_conv = (cw.ks in (3, 7, 11) and epi_act == L.ACT_NONE and gate is None and
-                    (pro_act == L.ACT_SNAKE or (cw.ks == 3 and acc_in is None)))
+                    (pro_act == L.ACT_SNAKE or (cw.ks == 3 and acc_in is None) or
+                     (cw.Co <= 32 and cw.ks == 7 and pro_act == L.ACT_LEAKY and pro is None and res is None and
+                      acc_in is None and stats_key is None)))  # (the last: conv_post on the narrow form)
         fx3_lin = (cw.ks == 1 and pad == 0 and pro is None and pro_act == L.ACT_NONE and stats_key is None and
                    a.T_out == x.T and epi_act in (L.ACT_NONE, L.ACT_GELU, L.ACT_SILU) and res_tdiv == 1)
         if (getattr(cw, "fx3", None) is not None and self.mrfx and x.t.dtype == torch.float32 and

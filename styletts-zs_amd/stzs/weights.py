@@ -220,7 +220,11 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
         assert not ups and cic == 128 and Co <= 32, (name, Ci, Co)
         wn = A.add(name + ".wpk", narrow32_stream(wp[:, :32], cic).to(torch.bfloat16))
         bn = A.add(name + ".bpk", b.float().clone()) if b is not None else None
-        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True, w32=w32, wx3=wx3)
+        fx3 = None  # precise: the narrow register-direct split-operand form (csrc/mrfx.hip, conv_post)
+        if x3 and ks in (3, 7, 11):
+            wf = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, frag32_perm()].reshape(ks, co_pad, ci_pad)
+            fx3 = A.add(name + ".wfx3", frag32x3_stream(wf))
+        return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True, w32=w32, wx3=wx3, fx3=fx3)
     if frag32:  # register-direct MRF convs (csrc/mrfv.hip) and the polyphase ConvTranspose (csrc/ups.hip, ups > 0)
         assert cic == 128 and ((not ups and Co % 8 == 0 and ks in (3, 7, 11)) or (ups and Co % 32 == 0)), \
             (name, Ci, Co, ks, ups)

@@ -253,6 +253,41 @@ def test_mrfx_kernel(gpu_device, case):
         assert max_rel(r.double(), 1 / torch.sqrt(vr + 1e-5)) < 1e-5
 
 
+@pytest.mark.parametrize("B,T", [(2, 3001), (1, 24001), (3, 130)])
+def test_mrfx_conv_post(gpu_device, B, T):
+    """conv_post (LeakyReLU(0.01), 128 -> 22, k7, fp32 out) on the narrow precise form (csrc/mrfx.hip NW: waves split
+    the rows, masked stores past Co = 22 -- the two padding columns of the row pitch 24 stay untouched) vs fp64 and vs
+    conv_x3: max-abs 4e-5 of max|ref|."""
+    from stzs import _lib as L
+    from stzs.engine import Act, StyleTTSZS
+    from stzs.params import init_params
+    from stzs.spec import SPEC_TINY
+    from stzs.weights import Arena, pack_conv
+    eng = StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, seed=0), device=gpu_device)
+    g = torch.Generator().manual_seed(B * T)
+    Ci, Co, k = 128, 22, 7
+    x = torch.randn(B, T, Ci, generator=g)
+    w = torch.randn(Co, Ci, k, generator=g) / math.sqrt(Ci * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    ref = F.conv1d(F.leaky_relu(x.double().transpose(1, 2), 0.01), w.double(), b.double(), padding=3).transpose(1, 2)
+    A = Arena()
+    cw = pack_conv(A, "t", w, b, narrow32=True, x3=True)
+    A.finalize(gpu_device)
+    cw.w, cw.wx3, cw.fx3, cw.b = A[cw.w], A[cw.wx3], A[cw.fx3], A[cw.b]
+    outs = []
+    for mrfx in (True, False):
+        eng.mrfx = mrfx
+        yb = torch.full((B, T, 24), 7.0, device=gpu_device)
+        eng.conv(cw, Act(x.to(gpu_device)), Act(yb, 0, Co), pad=3, pro_act=L.ACT_LEAKY, pro_slope=0.01,
+                 what="conv_post")
+        torch.cuda.synchronize()
+        assert bool((yb[:, :, Co:] == 7.0).all()), "columns past Co written"
+        outs.append(yb[:, :, :Co].double().cpu())
+    e, e_x3 = max_rel(outs[0], ref), max_rel(outs[0], outs[1])
+    print("mrfx conv_post", B, T, f"max-rel vs fp64 {e:.2e}, vs conv_x3 {e_x3:.2e}")
+    assert e < 4e-5 and e_x3 < 4e-5
+
+
 # FLAT linears of the precise pipeline (csrc/mrfx.hip mrfx_lin): rows, T per utterance, K, N, epilogue act, gate,
 # residual (broadcast over utterances = the positional table), accumulate, cscale
 MRFX_LIN_CASES = [
