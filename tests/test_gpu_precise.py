@@ -143,6 +143,7 @@ def test_conv_x3_kernel(gpu_device, B, T, Ci, Co, k, dil, stride, ups, act):
     A.add("alpha", alpha)
     A.finalize(gpu_device)
     cw.w, cw.wx3, cw.b = A[cw.w], A[cw.wx3], A[cw.b]
+    cw.fx3 = None  # (this test is the LDS-ring conv_x3 form; the register-direct one: test_mrfx_*)
     ld = (Ci + 7) // 8 * 8
     xt = torch.zeros(B, T, ld, device=gpu_device)
     xt[:, :, :Ci] = x.to(gpu_device)
