@@ -174,6 +174,13 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * accumulate input), stride 1, fp32 x / y / res / acc_in (32-B aligned rows), Co % 8 == 0; the InstanceNorm
  * statistics are those of the stored fp32 values. */
 #define STZS_CONV_W_FRAG32X3 16384
+/* flags bit (FRAG32 weights, Snake prologue): keep the register-direct MRF conv's 128-row time tiles where its
+ * launcher would take 64-row tiles (grids of fewer than two 128-row tiles per CU, e.g. batch 1).  Bit-identical either
+ * way (same staged operands, K order and 64-row statistics chunks); an A/B switch. */
+#define STZS_CONV_MRFV_T128 32768
+/* flags bit (conv_mfma split-K with one input-channel chunk per slice): keep the 3-slot weight ring instead of the
+ * DEEP form (every K-step of the slice in its own LDS slot, all issued at entry).  Bit-identical; an A/B switch. */
+#define STZS_CONV_RING 65536
 /* bytes of splitk_ws for a K-sliced small-M linear over `rows` rows, Co columns, kgroups slices: covers both the
  * csrc/rows.hip form (STZS_CONV_ROWS) and the 16-row K-slice form of stzs_ln_linear (ln = NULL, splitk in {2, 4}) */
 size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);

@@ -28,8 +28,12 @@ int stzs_conv_f32_launch(const stzs_conv_args* a, hipStream_t s);    // csrc/con
 
 namespace {
 
-template <typename TIn, typename TOut, bool FLAT, int PACT>
-__global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
+// DEEP (r05, the batch-1 split-K launches, one input-channel chunk per slice): every weight K-step of the slice is
+// issued into its own LDS slot at entry, beside the staging loads, so the slice pays ONE memory latency and its K loop
+// runs from LDS with no wait and no barrier (the 3-slot ring waited a fill latency every other K-step: ~0.37 us per
+// K-step at batch 1).  Same K order, same combine: bit-identical to the ring form at the same slice count.
+template <typename TIn, typename TOut, bool FLAT, int PACT, bool DEEP = false>
+__global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int cic = a.cic;
     const int pitch = cic * 2 + 16;
@@ -37,7 +41,8 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
     const int rows_in = FLAT ? BT : (BT - 1) * a.stride + (ks - 1) * a.dil + 1;
     unsigned char* in_lds = smem;
     unsigned char* ring = smem + ((rows_in * pitch + 15) & ~15);
-    float* c_sc = reinterpret_cast<float*>(ring + NSLOT * SLOT_BYTES);
+    const int nslot = DEEP ? (FLAT ? 1 : a.ks) * (cic >> 5) : NSLOT;
+    float* c_sc = reinterpret_cast<float*>(ring + nslot * SLOT_BYTES);
     float* c_sh = c_sc + 128;
     float* c_al = c_sh + 128;
     float* c_ia = c_al + 128;
@@ -78,7 +83,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
 
     auto fill = [&](int k) {
         const bf16_t* src = Wt + (long)k * (BCO * 32) + wave * 1024 + lane * 8;
-        unsigned char* dst = ring + (k % NSLOT) * SLOT_BYTES + wave * 2048;
+        unsigned char* dst = ring + (DEEP ? k - k_lo : k % NSLOT) * SLOT_BYTES + wave * 2048;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 512),
@@ -102,8 +107,14 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         boff[nt] = rr * 64 + (((lane >> 4) ^ gswz(rr)) << 4);
     }
 
-    fill(k_lo);
-    if (k_lo + 1 < k_hi) fill(k_lo + 1);
+    CPROF_RT(15)
+    CPROF(0)
+    if constexpr (DEEP) {
+        for (int kk = k_lo; kk < k_hi; ++kk) fill(kk);  // the whole slice (one chunk): ks x cic / 32 slots
+    } else {
+        fill(k_lo);
+        if (k_lo + 1 < k_hi) fill(k_lo + 1);
+    }
     int k = k_lo;
     for (int cc = cc_lo; cc < cc_hi; ++cc) {
         __syncthreads();
@@ -196,14 +207,18 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
                 *reinterpret_cast<uint4*>(in_lds + r * pitch + cv * 16) = pack8(o);
             }
         }
+        if constexpr (DEEP) waitcnt_vm(0);  // this wave's weight slots landed (the barrier publishes every wave's)
         __syncthreads();
+        if (cc == cc_lo) { CPROF(1) }
         for (int tap = 0; tap < ((a.flags & 2) ? 0 : ks); ++tap) {
             const int roff = FLAT ? 0 : tap * a.dil;
             for (int kq = 0; kq < kpc; ++kq, ++k) {
-                waitcnt_vm(k + 1 < k_hi ? 2 : 0);
-                __builtin_amdgcn_s_barrier();
-                if (k + 2 < k_hi) fill(k + 2);
-                const unsigned char* wl = ring + (k % NSLOT) * SLOT_BYTES;
+                if constexpr (!DEEP) {
+                    waitcnt_vm(k + 1 < k_hi ? 2 : 0);
+                    __builtin_amdgcn_s_barrier();
+                    if (k + 2 < k_hi) fill(k + 2);
+                }
+                const unsigned char* wl = ring + (DEEP ? k - k_lo : k % NSLOT) * SLOT_BYTES;
                 const int kb = (kq * 32 + 8 * (lane >> 4)) * 2;
                 bf16x8 af[4], bw[4];
 #pragma unroll
@@ -223,13 +238,26 @@ __global__ __launch_bounds__(NTHR, 2) void conv_mfma(const stzs_conv_args a) {
         }
     }
 
-    if (SKr > 1 && !splitk_combine_rt<BT>(a, acc, smem, SKr)) return;
+    CPROF(2)
+    if (SKr > 1 && !splitk_combine_rt<BT, DEEP ? 4 : 1>(a, acc, smem, SKr)) {
+        CPROF_RT(14)
+        return;
+    }
+    CPROF(5)
     finish<TOut, FLAT>(a, acc, smem, bq, t0, row0, by);
+    CPROF(6)
+    CPROF_RT(14)
+#ifdef STZS_CONV_PROF
+    if (threadIdx.x == 0) {
+        const unsigned wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        if (wg_ < 8192) g_cprof[wg_ * 16 + 13] = __builtin_amdgcn_s_getreg(0x14 | (3 << 11)) + 1;  // HW_REG_XCC_ID (+1)
+    }
+#endif
 }
 
 // splitk_combine with the slice count at run time (conv_mfma): the same slabs, ticket and slice-order sum, the
 // slices loaded one at a time (no [SK][NV] register block).
-template <int BTM>
+template <int BTM, int RB>
 STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK) {
     constexpr int NV = BTM / 32 * 4;
     constexpr int SLAB = NV * NTHR * 16;
@@ -244,6 +272,7 @@ STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][
                                                (z * NV + i) * (NTHR * 16) + tid * 16, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    CPROF(3)
     volatile int* flag = reinterpret_cast<volatile int*>(smem);  // staging / ring idle: every wave is past its K loop
     if (tid == 0) {
         typedef __attribute__((address_space(1))) unsigned int gu32;
@@ -254,23 +283,31 @@ STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][
         *flag = last;
     }
     __syncthreads();
+    CPROF(4)
     if (!*flag) return false;
 #pragma unroll
     for (int i = 0; i < NV; ++i)
         acc[i >> 2][i & 3] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, i * (NTHR * 16) + tid * 16, 0, 16));
-    for (int sl = 1; sl < SK; ++sl) {
-        u32x4 v[NV];
+    // RB slices per round, all their loads in flight at once, summed in slice order (the same sum for every RB)
+    for (int sl = 1; sl < SK; sl += RB) {
+        u32x4 v[RB][NV];
 #pragma unroll
-        for (int i = 0; i < NV; ++i)
-            v[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, (sl * NV + i) * (NTHR * 16) + tid * 16, 0, 16);
+        for (int j = 0; j < RB; ++j)
+            if (sl + j < SK)
 #pragma unroll
-        for (int i = 0; i < NV; ++i) acc[i >> 2][i & 3] += __builtin_bit_cast(f32x4, v[i]);
+                for (int i = 0; i < NV; ++i)
+                    v[j][i] = __builtin_amdgcn_raw_buffer_load_b128(wr, ((sl + j) * NV + i) * (NTHR * 16) + tid * 16, 0, 16);
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
+            if (sl + j < SK)
+#pragma unroll
+                for (int i = 0; i < NV; ++i) acc[i >> 2][i & 3] += __builtin_bit_cast(f32x4, v[j][i]);
     }
     return true;
 }
 
-size_t lds_bytes(int rows_in, int cic) {
-    const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + NSLOT * SLOT_BYTES + 4 * 128 * 4;
+size_t lds_bytes(int rows_in, int cic, int nslot = NSLOT) {
+    const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + (size_t)nslot * SLOT_BYTES + 4 * 128 * 4;
     const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
     return main > epi ? main : epi;
 }
@@ -280,7 +317,11 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     const bool flat = (a.ks == 1 && a.stride == 1 && a.pad == 0 && a.ups == 0 && a.pro_mode == STZS_PRO_NONE &&
                        a.pro_act == STZS_ACT_NONE && a.T_in == a.T_out);
     const int rows_in = flat ? BT : (BT - 1) * a.stride + (a.ks - 1) * a.dil + 1;
-    const size_t lds = lds_bytes(rows_in, a.cic);
+    // DEEP: split-K with one input-channel chunk per slice whose K-steps all fit LDS beside the staged rows
+    const int nslot_deep = (flat ? 1 : a.ks) * (a.cic >> 5);
+    const bool deep = a.splitk > 1 && a.splitk == a.ci_pad / a.cic && !(a.flags & STZS_CONV_RING) &&
+                      lds_bytes(rows_in, a.cic, nslot_deep) <= 160 * 1024;
+    const size_t lds = lds_bytes(rows_in, a.cic, deep ? nslot_deep : NSLOT);
     if (lds > 160 * 1024) return STZS_ESHAPE;
     const unsigned gx = flat ? (unsigned)(((long)a.B * a.T_out + BT - 1) / BT)
                              : (unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT);
@@ -289,8 +330,8 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     void (*k)(stzs_conv_args);
     if (F8 || (flat && sizeof(TIn) == 2 && (a.flags & STZS_CONV_A_DMA) && a.pro_cscale == 1.f))
         return stzs_gemm_glds_launch(a, s);  // (csrc/gemm.hip)
-    if (a.splitk > 1) {  // conv_mfma: split over input-channel chunks (2..8 slices, at least one chunk each)
-        if (F8 || a.splitk > 8 || a.splitk > a.ci_pad / a.cic || !a.splitk_ws || !a.splitk_ctr ||
+    if (a.splitk > 1) {  // conv_mfma: split over input-channel chunks (2..16 slices, at least one chunk each)
+        if (F8 || a.splitk > 16 || a.splitk > a.ci_pad / a.cic || !a.splitk_ws || !a.splitk_ctr ||
             !stzs_aligned(a.splitk_ws, 16) || !stzs_aligned(a.splitk_ctr, 4))
             return STZS_EINVAL;
         grid.z = (unsigned)a.splitk;
@@ -298,7 +339,16 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     if constexpr (F8) {
         return STZS_EDTYPE;  // (unreachable: fp8 is a pure linear)
     } else {
-        if (flat)
+        if (deep) {
+            if (flat)
+                k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE, true>;
+            else if (a.pro_act == STZS_ACT_LEAKY)
+                k = conv_mfma<TIn, TOut, false, STZS_ACT_LEAKY, true>;
+            else if (a.pro_act == STZS_ACT_NONE)
+                k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE, true>;
+            else
+                k = conv_mfma<TIn, TOut, false, STZS_ACT_SNAKE, true>;
+        } else if (flat)
             k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE>;
         else if (a.pro_act == STZS_ACT_SNAKE)
             k = conv_mfma<TIn, TOut, false, STZS_ACT_SNAKE>;
@@ -375,4 +425,16 @@ extern "C" size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32
 
 #ifdef STZS_GEMM_PROF
 extern "C" int stzs_gemm_prof_conv(const stzs_conv_args* a, void* stream) { return stzs_conv1d_core(a, stream); }
+#endif
+
+#ifdef STZS_CONV_PROF
+// probe build only: copy the stamps to the host (n <= 16 * 8192 words) / zero them
+extern "C" int stzs_conv_prof_read(unsigned long long* host, size_t n, int zero) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_cprof)) != hipSuccess) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (host && hipMemcpy(host, p, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (zero && hipMemset(p, 0, sizeof(unsigned long long) * 16 * 8192) != hipSuccess) return -1;
+    return 0;
+}
 #endif

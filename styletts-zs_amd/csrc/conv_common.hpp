@@ -15,6 +15,26 @@ constexpr int NSLOT = 3;
 constexpr int SLOT_BYTES = BCO * 32 * 2;  // one K-step of weights
 constexpr int EP_PITCH = BCO + 4;         // fp32 epilogue row pitch (floats)
 
+// STZS_CONV_PROF probe build (tools/conv_phase.py --build): thread 0 of every workgroup stamps s_memtime at the phase
+// boundaries of conv_mfma / finish into g_cprof[workgroup][16] (slot 15: s_memrealtime at entry, 14: at exit, 13: XCC id)
+#ifdef STZS_CONV_PROF
+__device__ unsigned long long g_cprof[16 * 8192];
+#define CPROF(i)                                                                                                   \
+    if (threadIdx.x == 0) {                                                                                        \
+        const unsigned wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                       \
+        if (wg_ < 8192) g_cprof[wg_ * 16 + (i)] = __builtin_amdgcn_s_memtime();                                    \
+    }
+#define CPROF_RT(i)                                                                                                \
+    if (threadIdx.x == 0) {                                                                                        \
+        const unsigned wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                       \
+        if (wg_ < 8192) g_cprof[wg_ * 16 + (i)] = __builtin_amdgcn_s_memrealtime();                                \
+    }
+#else
+#define CPROF(i)
+#define CPROF_RT(i)
+#endif
+
+
 STZS_DEV int gswz(int r) { return (0x1320 >> (((r >> 2) & 3) * 4)) & 3; }
 
 // flat row R -> (utterance q, step R - q T) without a 64-bit integer division (hipcc expands `long / int` into a
@@ -287,6 +307,7 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
             }
         }
         if (stat) stat_flush(v0 == 0 ? 0 : 1);
+        CPROF(9 + (v0 > 0))
     }
     if (stat) {
         __syncthreads();
@@ -321,7 +342,7 @@ STZS_DEV void epilogue_act(const stzs_conv_args& a, const float* ep, const float
     }
 }
 
-template <int BTM>
+template <int BTM, int RB = 1>
 STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK);
 // EP: the epilogue variant compiled into the calling kernel.  -1: all of them behind runtime tests (the conv kernels);
 // 0..15: ONE vectorised variant, HR = bit 0, HA = bit 1, activation index (ep_act) = bits 2-3 (the GEMM kernels:
@@ -372,6 +393,7 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigne
                 ep[(wt * (BTM / 2) + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
     if (a.flags & 4) return;
     GPROF_E(5)
+    CPROF(7)
     float* c_bias = ep + BTM * EP_PITCH;      // [BCO] bias, [BCO] gate (conv mode: one utterance)
     float* c_gate = c_bias + BCO;
     if (tid < BCO) {
@@ -382,6 +404,7 @@ STZS_DEV void finish(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigne
     }
     __syncthreads();
     GPROF_E(6)
+    CPROF(8)
     if constexpr (EP >= 0) {
         epilogue<TOut, FLAT, true, (EP & 1) != 0, (EP & 2) != 0, ep_act(EP >> 2), BTM>(a, ep, c_bias, c_gate, bq, t0, row0, tid, by);
     } else if (epi_vec(a)) {

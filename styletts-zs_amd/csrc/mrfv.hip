@@ -29,12 +29,14 @@
 namespace {
 
 constexpr int NTH = 256;
-constexpr int BT = 128, BCO = 128;
+constexpr int BCO = 128;
 constexpr int P = 272;  // staged input row pitch, bytes (conflict-free ds_read_b128)
 // staged 16-B vectors per thread (16 rows each): rows_in = 128 + (KS - 1) dil <= 16 SB.  Sized per kernel width
 // (k3: dil <= 8; k7 / k11: dil <= 5), not for the widest: every staged vector costs its transform (the cosines
 // of the Snake) whether or not its row is used, and a k3 tile with SB = 12 transformed 192 rows for 130-138
 constexpr int sb_rows(int ks) { return ks == 3 ? 9 : (ks == 7 ? 10 : 12); }
+// the 64-row tiles (BT 64, small grids): 64 + (ks - 1) dil rows
+constexpr int sb_rows64(int ks) { return ks == 3 ? 5 : (ks == 7 ? 6 : 8); }
 constexpr int SB_MAX = 12;
 constexpr int CS_BYTES = 5 * 128 * 4;  // per-channel prologue constants
 
@@ -63,10 +65,14 @@ STZS_DEV void row_sum16_n(float* x) {
 // inputs with co_pad % 256 == 0): 256, so a 256-channel layer stages (loads + AdaIN + Snake) each input row ONCE
 // instead of once per 128-channel tile, and every B fragment read from LDS feeds 4 MFMAs instead of 2.  Same K
 // order per output element either way (bit-identical).
-template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1>
+// BT: time rows per tile, 128 or 64 (r05: small grids -- batch 1 -- where the 128-row tiles leave CUs idle).  The
+// staged operands, the K order of every output element and the 64-row statistics chunks are the same: bit-identical.
+template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int BT = 128>
 __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
     static_assert(WPW == 1 || (WPW == 2 && NCH != 1), "the wide form is for multi-chunk inputs");
+    static_assert(BT == 128 || (BT == 64 && WPW == 1), "64-row tiles: narrow form");
     constexpr int NA = 2 * WPW;  // A fragments (16 output channels each) per wave and K-step
+    constexpr int MT = BT / 16;  // 16-row B fragments per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NKC = KS * 4;  // 32-wide K-steps per 128-channel chunk
     const int dil = a.dil;
@@ -81,7 +87,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     const int bq = bx / tpb;
     const int t0 = (bx - bq * tpb) * BT;
     const int nchunk = NCH ? NCH : a.ci_pad >> 7;
-    constexpr int SB = sb_rows(KS);
+    constexpr int SB = BT == 128 ? sb_rows(KS) : sb_rows64(KS);
     // weights: [co tile][chunk][tap][kq][wave][nt][lane][8] bf16 -> 512 bf16x8 per K-step.  Wide form: wave w takes
     // the packed waves 2 (w & 1) and 2 (w & 1) + 1 of 128-channel tile 2 by + (w >> 1) -- consecutive in the stream
     const int ct = WPW == 1 ? by : by * 2 + (wave >> 1);
@@ -92,7 +98,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 #pragma unroll
         for (int j = 0; j < NA; ++j) w[j] = p[64 * j];
     };
-    f32x4 acc[NA][8];
+    f32x4 acc[NA][MT];
 
     const int xoff0 = (lane & 15) * P + (lane >> 4) * 16;
     const int dP = dil * P;
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     // time, and two spill its 256 VGPRs)
     constexpr int PD = WPW == 2 ? 1 : STZS_MRFV_PD;
     bf16x8 wf[PD + 1][NA];
-    bf16x8 xf[8];
+    bf16x8 xf[MT];
 
     for (int cc = 0; cc < nchunk; ++cc) {
         const int kb = cc * NKC;
@@ -222,14 +228,14 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
             constexpr bool FIRST = decltype(first_tag)::value;
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
+            for (int mt = 0; mt < MT; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
 #pragma unroll
             for (int s = 0; s < NKC; ++s) {
                 if (s + PD < NKC) wload(wf[(s + PD) % (PD + 1)], kb + s + PD);
                 const int sn = s + 1;
                 const int offn = (sn >> 2) * dP + (sn & 3) * 64;
 #pragma unroll
-                for (int mt = 0; mt < 8; ++mt) {
+                for (int mt = 0; mt < MT; ++mt) {
                     const bool z = FIRST && s == 0;
 #pragma unroll
                     for (int j = 0; j < NA; ++j)
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                     __builtin_amdgcn_sched_group_barrier(0x020, NA, 0);  // the weight loads first
                 }
 #pragma unroll
-                for (int mt = 0; mt < 8; ++mt) {
+                for (int mt = 0; mt < MT; ++mt) {
                     __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
                     if (sn < NKC) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 #pragma unroll
                 for (int i = 0; i < NA; ++i)
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
             kloop(std::integral_constant<bool, false>{});
         }
@@ -280,9 +286,9 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[coc + i] : 0.f;
     // the residual / accumulate rows of BOTH halves in flight at once (the second half's HBM latency hides
     // behind the first half's epilogue); uniform utterance bases + 32-bit per-lane offsets
-    uint4 rr[8], aa[8];
+    uint4 rr[MT], aa[MT];
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
+    for (int mt = 0; mt < MT; ++mt) {
         const int t = t0 + mt * 16 + n;
         const int tc = t < a.T_out ? t : a.T_out - 1;
         if constexpr (HR) {
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
         if constexpr (HA) aa[mt] = *reinterpret_cast<const uint4*>(Aq + (unsigned)(tc * (int)a.lda + coc) * 2u);
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // two 64-row halves: one statistics partial each
+    for (int h = 0; h < MT / 4; ++h) {  // 64-row halves: one statistics partial each
         float ss[8], sq[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
@@ -351,18 +357,22 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     }
 }
 
-template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1>
+template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1, int BT = 128>
 void (*pick_ks(int ks))(stzs_conv_args) {
     switch (ks) {
-        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL, WPW>;
-        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL, WPW>;
-        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH, AL, WPW>;
+        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL, WPW, BT>;
+        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL, WPW, BT>;
+        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH, AL, WPW, BT>;
         default: return nullptr;
     }
 }
 template <int PACT, bool HR, bool HA>
-void (*pick(int ks, bool one, bool al, bool wide))(stzs_conv_args) {
+void (*pick(int ks, bool one, bool al, bool wide, bool t64))(stzs_conv_args) {
     if (wide) return al ? pick_ks<PACT, HR, HA, 0, true, 2>(ks) : pick_ks<PACT, HR, HA, 0, false, 2>(ks);
+    if (t64) {  // (64-row tiles: the Snake forms of small grids)
+        if (al) return one ? pick_ks<PACT, HR, HA, 1, true, 1, 64>(ks) : pick_ks<PACT, HR, HA, 0, true, 1, 64>(ks);
+        return one ? pick_ks<PACT, HR, HA, 1, false, 1, 64>(ks) : pick_ks<PACT, HR, HA, 0, false, 1, 64>(ks);
+    }
     if (al) return one ? pick_ks<PACT, HR, HA, 1, true>(ks) : pick_ks<PACT, HR, HA, 0, true>(ks);
     return one ? pick_ks<PACT, HR, HA, 1, false>(ks) : pick_ks<PACT, HR, HA, 0, false>(ks);
 }
@@ -374,7 +384,7 @@ int stzs_ups_conv_launch(const stzs_conv_args& a, hipStream_t s);   // csrc/ups.
 // internal entry used by stzs_conv1d for STZS_CONV_W_FRAG32 weights
 __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s) {
     if (a.ups > 0) return stzs_ups_conv_launch(a, s);
-    const int rows_in = BT + (a.ks - 1) * a.dil;
+    const int rows_in = 128 + (a.ks - 1) * a.dil;
     if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || rows_in > 16 * (a.ks == 3 ? sb_rows(3) : a.ks == 7 ? sb_rows(7) : SB_MAX) ||
         a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.gate || a.epi_act != STZS_ACT_NONE || a.ups ||
         a.refl || a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv <= 0)) ||
@@ -382,20 +392,28 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
     if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
-    const size_t lds = (((size_t)rows_in * P + 15) & ~(size_t)15) + CS_BYTES;
     void (*k)(stzs_conv_args) = nullptr;
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
     // the wide form (256 output channels per workgroup) for multi-chunk Snake convs whose wide grid still gives every
     // CU two workgroups (at batch 1 a stage-0 conv has 32 row tiles: the narrow form's 64 workgroups finish sooner),
     // unless STZS_CONV_MRFV_NARROW.  Both forms are bit-identical, so the choice never changes a result.
-    const long wide_tiles = (long)a.B * ((a.T_out + BT - 1) / BT) * (a.co_pad / (2 * BCO));
+    const long wide_tiles = (long)a.B * ((a.T_out + 127) / 128) * (a.co_pad / (2 * BCO));
     const bool wide = a.pro_act == STZS_ACT_SNAKE && a.ci_pad > 128 && a.co_pad % (2 * BCO) == 0 &&
                       wide_tiles >= 512 && !(a.flags & STZS_CONV_MRFV_NARROW);
+    // 64-row tiles where the narrow 128-row grid would not give every CU two workgroups (batch 1: a stage-1 conv is
+    // 188 tiles, a stage-0 conv 64); also bit-identical.  STZS_CONV_MRFV_T128 keeps the 128-row tiles (A/B switch).
+    const long tiles128 = (long)a.B * ((a.T_out + 127) / 128) * (a.co_pad / BCO);
+    const int rows64 = 64 + (a.ks - 1) * a.dil;
+    const bool t64 = !wide && a.pro_act == STZS_ACT_SNAKE && tiles128 < 2 * stzs_cu_count() &&
+                     rows64 <= 16 * (a.ks == 3 ? sb_rows64(3) : a.ks == 7 ? sb_rows64(7) : sb_rows64(11)) &&
+                     !(a.flags & STZS_CONV_MRFV_T128);
+    const int BT = t64 ? 64 : 128;
+    const size_t lds = ((((size_t)BT + (a.ks - 1) * a.dil) * P + 15) & ~(size_t)15) + CS_BYTES;
     if (a.pro_act == STZS_ACT_SNAKE) {
         const bool one = a.ci_pad == 128;
         const bool al = a.alpha != 1.f;
-        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide))
-              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide));
+        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide, t64))
+              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide, t64));
     } else if (!A && a.ks == 3) {  // the AdaIN residual blocks of the decoder / prosody predictor
         if (a.pro_act == STZS_ACT_LEAKY)
             k = R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true>;

@@ -52,9 +52,10 @@ LATENCY_DN_ROWS = dict(inp=1, qkv=1, o=1, q=1, co=1, ff1=1, ff2=4, out=1)
 TE_SPLITK = 0
 LATENCY_TE_SPLITK = 4
 # split-K slices of the decoder / predictor AdaIN-block convs (their generic-layout copies, BlkW.conv1s / conv2s) in
-# the batch-1 latency engine: at 200-400 frames a decoder conv is 16 tiles x 108 K-steps on 16 CUs; 0 = off
+# the batch-1 latency engine: at 200-400 frames a decoder conv is 16 tiles x 108 K-steps on 16 CUs; 0 = off.  16 (r05)
+# = one input-channel chunk per slice for every block conv (<= 9 chunks): the DEEP form (csrc/conv.hip)
 BLK_SPLITK = 0
-LATENCY_BLK_SPLITK = 8
+LATENCY_BLK_SPLITK = 16
 
 
 _ES = {L.F32: 4, L.BF16: 2, L.F8: 1}
@@ -415,8 +416,9 @@ class StyleTTSZS:
             splitk = min(splitk, 4)  # (gemm_glds takes 2 or 4 slices)
             while splitk > 1 and (cw.ci_pad // 32) % splitk:
                 splitk //= 2
-        elif splitk > 1:  # conv_mfma: the slices split the input-channel chunks (2..8, at most one slice per chunk)
-            splitk = min(splitk, 8, cw.ci_pad // cw.cic)
+        elif splitk > 1:  # conv_mfma: the slices split the input-channel chunks (2..16, at most one slice per chunk;
+            # one chunk per slice takes the DEEP form: the slice's whole weight stream issued at entry)
+            splitk = min(splitk, 16, cw.ci_pad // cw.cic)
         if splitk > 1 and (a.flags & 8) and not cw.f8 and cw.wx3 is None and cw.w32 is None:
             # in-launch split-K (stzs_conv_args.splitk): per-branch fp32 slabs + self-resetting tile counters
             nb = self.lib.stzs_conv_splitk_workspace(x.B * x.T, cw.co_pad, splitk)

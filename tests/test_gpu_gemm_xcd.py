@@ -107,7 +107,7 @@ SPLITK_CASES = [  # (B, T, Ci, Co, k, epilogue): the text-encoder shape, then T_
 ]
 
 
-@pytest.mark.parametrize("splitk", [2, 4])
+@pytest.mark.parametrize("splitk", [2, 4, 16])
 @pytest.mark.parametrize("case", SPLITK_CASES, ids=lambda c: f"B{c[0]}-T{c[1]}-k{c[4]}-{c[5]}")
 def test_conv_mfma_splitk(eng, splitk, case):
     """conv_mfma in-launch split-K over input-channel chunks (the latency engine's text-encoder k5 convs,
@@ -115,7 +115,9 @@ def test_conv_mfma_splitk(eng, splitk, case):
     fused InstanceNorm statistics partials), T_out > 128 and a 1x1 conv: matches F.conv1d on the same bf16 operands,
     utterance 0 of a B-utterance launch is bit-identical to the 1-utterance launch (per-utterance tiles:
     batch-invariant), a re-run is bit-identical (the self-resetting tile tickets), and the result is within fp32
-    re-association of the unsplit conv (statistics included)."""
+    re-association of the unsplit conv (statistics included).  splitk 16 = one chunk per slice (the engine clamps to
+    the chunk count): the DEEP form where the slice's K-steps fit LDS, bit-identical to the 3-slot ring form
+    (STZS_CONV_RING) at the same slice count."""
     from stzs import _lib as L
     from stzs.engine import Act
     from stzs.weights import Arena, pack_conv
@@ -136,11 +138,11 @@ def test_conv_mfma_splitk(eng, splitk, case):
     accd = acc.to(torch.bfloat16).cuda()
     alpha, beta = (0.7, 0.5) if epi.startswith("acc") else (1.0, 0.0)
 
-    def run(n, sk):
+    def run(n, sk, flags=0):
         xb = xd[:n].contiguous()
         a0 = accd[:n].clone()
         y = a0 if epi == "acc_inplace" else torch.zeros(n, T, Co, dtype=torch.bfloat16, device="cuda:0")
-        kw = dict(pad=k // 2, splitk=sk)
+        kw = dict(pad=k // 2, splitk=sk, flags=flags)
         if epi == "leaky":
             kw.update(pro_act=L.ACT_LEAKY, pro_slope=0.2)
         if epi == "res":
@@ -162,6 +164,11 @@ def test_conv_mfma_splitk(eng, splitk, case):
     y0, s0 = run(B, 0)
     assert torch.equal(y3, y3b)
     assert torch.equal(y3[:1], y1)
+    if splitk == 16:  # DEEP (where it fits) vs the ring form: same slices, same K order -> bit-identical
+        yr, sr = run(B, splitk, L.CONV_RING)
+        assert torch.equal(y3, yr)
+        if epi == "stats":
+            assert torch.equal(s3[0], sr[0]) and torch.equal(s3[1], sr[1])
     xin = bf(F.leaky_relu(x, 0.2)) if epi == "leaky" else x
     ref = F.conv1d(xin.transpose(1, 2), bf(w), b, padding=k // 2).transpose(1, 2)
     if epi == "res":

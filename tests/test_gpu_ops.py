@@ -405,6 +405,28 @@ def test_mrf_wide_bit_identical(eng, case):
         assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
 
 
+# Snake convs whose 128-row grid has fewer than two tiles per CU (batch 1): the 64-row-tile mrfv form
+T64_CASES = [
+    (1, 24001, 128, 128, 3, 1, "snake", False, False, True, 1),   # batch-1 stage-1 c1 (188 -> 376 workgroups)
+    (1, 24001, 128, 128, 11, 5, "snake", True, True, False, 1),   # stage-1 last c2: residual + accumulate, dil 5 halo
+    (1, 3001, 256, 256, 7, 3, "snake", True, False, True, 1),     # stage 0 (2 chunks), ragged: 3001 % 64 = 57
+    (2, 4033, 384, 176, 11, 5, "snake", True, True, True, 1),     # 3 chunks, Co < co_pad, a 1-row last tile
+]
+
+
+@pytest.mark.parametrize("case", T64_CASES)
+def test_mrf_t64_bit_identical(eng, case):
+    """the 64-row-tile register-direct form (the launcher's choice when the 128-row grid has fewer than 2 workgroups per
+    CU) vs the 128-row tiles (STZS_CONV_MRFV_T128): same staged operands, same K order per output, same 64-row
+    statistics chunks -> outputs and fused statistics bit-identical (tolerance 0)."""
+    from stzs import _lib as L
+    a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_T128, ref=False)
+    b, sb, _ = _run_mrf(eng, case, "frag32", ref=False)
+    assert torch.equal(a, b)
+    if sa is not None:
+        assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
+
+
 @pytest.mark.parametrize("B,T,Ci,Co,k", [(2, 3001, 128, 22, 7), (1, 300, 256, 32, 3), (3, 257, 128, 8, 7)])
 def test_narrow_conv(eng, B, T, Ci, Co, k):
     """narrow conv (conv_post form: LeakyReLU(0.01) prologue, Co <= 32, fp32 out, csrc/mrf.hip
