@@ -181,6 +181,10 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
 /* flags bit (conv_mfma split-K with one input-channel chunk per slice): keep the 3-slot weight ring instead of the
  * DEEP form (every K-step of the slice in its own LDS slot, all issued at entry).  Bit-identical; an A/B switch. */
 #define STZS_CONV_RING 65536
+/* flags bit (with the DEEP split-K form): combine the slices in the tile's last-arriving workgroup (one workgroup reads
+ * every other slice's 64-KB fp32 slab) instead of the second launch splitk_epi (8 workgroups per tile).  Outputs are
+ * bit-identical; the fused statistics partials differ in fp32 association only.  An A/B switch. */
+#define STZS_CONV_SK_TICKET 131072
 /* bytes of splitk_ws for a K-sliced small-M linear over `rows` rows, Co columns, kgroups slices: covers both the
  * csrc/rows.hip form (STZS_CONV_ROWS) and the 16-row K-slice form of stzs_ln_linear (ln = NULL, splitk in {2, 4}) */
 size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);

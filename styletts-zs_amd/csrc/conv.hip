@@ -32,7 +32,10 @@ namespace {
 // issued into its own LDS slot at entry, beside the staging loads, so the slice pays ONE memory latency and its K loop
 // runs from LDS with no wait and no barrier (the 3-slot ring waited a fill latency every other K-step: ~0.37 us per
 // K-step at batch 1).  Same K order, same combine: bit-identical to the ring form at the same slice count.
-template <typename TIn, typename TOut, bool FLAT, int PACT, bool DEEP = false>
+// SKE (with DEEP): the slice stores its fp32 partial tile row-major into its slab and ends; the combine and the fused
+// epilogue run in splitk_epi, a second launch spread over 8 workgroups per tile (the last-arriver combine read every
+// other slice's 64-KB slab through ONE workgroup: 7.5 us of a 24-us batch-1 decoder conv, tools/conv_phase.py).
+template <typename TIn, typename TOut, bool FLAT, int PACT, bool DEEP = false, bool SKE = false>
 __global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int cic = a.cic;
@@ -239,6 +242,30 @@ __global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_
     }
 
     CPROF(2)
+    if constexpr (SKE) {
+        // the partial tile through LDS (fp32, padded rows) to the slab [tile = by gx + bx][z][128 rows][128], valid rows only
+        __syncthreads();  // every wave is past its K loop (staging / weight slots idle)
+        float* ep = reinterpret_cast<float*>(smem);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    ep[(wt * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
+        __syncthreads();
+        const long tile = (long)by * gridDim.x + bx;
+        float* slab = reinterpret_cast<float*>(a.splitk_ws) + (tile * SKr + blockIdx.z) * (long)(BT * BCO);
+        const long rows_left = FLAT ? (long)a.B * a.T_out - row0 : (long)(a.T_out - t0);
+        const int nrow = rows_left < BT ? (int)rows_left : BT;
+        for (int e = tid; e < nrow * (BCO / 4); e += NTHR) {
+            const int r = e >> 5, v = e & 31;
+            *reinterpret_cast<float4*>(slab + r * BCO + v * 4) = *reinterpret_cast<const float4*>(ep + r * EP_PITCH + v * 4);
+        }
+        CPROF(3)
+        CPROF_RT(14)
+        return;
+    }
     if (SKr > 1 && !splitk_combine_rt<BT, DEEP ? 4 : 1>(a, acc, smem, SKr)) {
         CPROF_RT(14)
         return;
@@ -306,6 +333,146 @@ STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][
     return true;
 }
 
+// The split-K combine + fused epilogue of the SKE slices (a second launch): workgroup (bx, 8 by + cg) owns rows
+// [0, 128) x columns [by 128 + 16 cg, +16) of tile (bx, by); thread (row = tid / 2, 8-column vector tid % 2) sums the
+// SK slabs in slice order (the last-arriver combine's order: y is bit-identical to it), then bias, activation,
+// conv-mode gate, residual (t / res_tdiv), alpha, beta * acc_in, the store, and the InstanceNorm partials of the
+// stored values per 64-row half (one deterministic fp32 partial per (utterance, 64-row chunk, channel), reduced
+// lanes -> waves in a fixed order).
+template <typename TOut, bool FLAT>
+__global__ __launch_bounds__(NTHR) void splitk_epi(const stzs_conv_args a, int SK) {
+    __shared__ float red[4][2][8][2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int bx = blockIdx.x, by = blockIdx.y >> 3, cg = blockIdx.y & 7;
+    const int rl = tid >> 1, cvl = tid & 1;
+    int bq = 0, t0 = 0;
+    long row0 = 0;
+    if (FLAT) {
+        row0 = (long)bx * BT;
+    } else {
+        const int tpb = (a.T_out + BT - 1) / BT;
+        bq = bx / tpb;
+        t0 = (bx - bq * tpb) * BT;
+    }
+    const int co = by * BCO + cg * 16 + cvl * 8;
+    const bool col_ok = co < a.Co;
+    const int cc = col_ok ? co : 0;
+    long bb = bq, t = t0 + rl;
+    bool ok = col_ok;
+    if (FLAT) {
+        const long R = row0 + rl;
+        ok = ok && R < (long)a.B * a.T_out;
+        bb = ok ? R / a.T_out : 0;
+        t = ok ? R - bb * a.T_out : 0;
+    } else {
+        ok = ok && t < a.T_out;
+    }
+    const long tile = (long)by * gridDim.x + bx;
+    const float* S = reinterpret_cast<const float*>(a.splitk_ws) + tile * SK * (long)(BT * BCO) + rl * BCO + cg * 16 + cvl * 8;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    float bias[8], gt[8], rr[8], ai[8];
+    if (ok) {
+        // residual / accumulate / bias / gate loads in flight with the slabs'
+        const TOut* Rp = reinterpret_cast<const TOut*>(a.res);
+        const TOut* AI = reinterpret_cast<const TOut*>(a.acc_in);
+        if (a.res) {
+            const long tr = a.res_tdiv == 1 ? t : (long)((int)t / a.res_tdiv);
+            load8(Rp + bb * a.bsr + tr * a.ldr + cc, rr);
+        }
+        if (a.acc_in) load8(AI + bb * a.bsa + t * a.lda + cc, ai);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            bias[j] = a.bias ? a.bias[cc + j] : 0.f;
+            gt[j] = (!FLAT && a.gate) ? a.gate[(long)bq * a.gate_bs + cc + j] : 1.f;
+        }
+        // slice 0, then slices 1.. in order, 4 slices' loads in flight per round
+        float4 p0 = *reinterpret_cast<const float4*>(S), p1 = *reinterpret_cast<const float4*>(S + 4);
+        v[0] = p0.x; v[1] = p0.y; v[2] = p0.z; v[3] = p0.w; v[4] = p1.x; v[5] = p1.y; v[6] = p1.z; v[7] = p1.w;
+        for (int z = 1; z < SK; z += 4) {
+            float4 q[4][2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (z + i < SK) {
+                    q[i][0] = *reinterpret_cast<const float4*>(S + (long)(z + i) * (BT * BCO));
+                    q[i][1] = *reinterpret_cast<const float4*>(S + (long)(z + i) * (BT * BCO) + 4);
+                }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (z + i < SK) {
+                    v[0] += q[i][0].x; v[1] += q[i][0].y; v[2] += q[i][0].z; v[3] += q[i][0].w;
+                    v[4] += q[i][1].x; v[5] += q[i][1].y; v[6] += q[i][1].z; v[7] += q[i][1].w;
+                }
+        }
+    }
+    float st_s[8], st_q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
+    if (ok) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float x;
+            switch (a.epi_act) {  // (uniform)
+                case STZS_ACT_GELU: x = epi_act<STZS_ACT_GELU>(v[j] + bias[j], a.epi_slope); break;
+                case STZS_ACT_SILU: x = epi_act<STZS_ACT_SILU>(v[j] + bias[j], a.epi_slope); break;
+                case STZS_ACT_LEAKY: x = epi_act<STZS_ACT_LEAKY>(v[j] + bias[j], a.epi_slope); break;
+                default: x = v[j] + bias[j]; break;
+            }
+            if (!FLAT) x *= gt[j];
+            if (a.res) x += rr[j];
+            x *= a.alpha;
+            if (a.acc_in) x += a.beta * ai[j];
+            o[j] = x;
+        }
+        TOut* Y = reinterpret_cast<TOut*>(a.y) + bb * a.bsy + t * a.ldy + co;
+        if constexpr (sizeof(TOut) == 2) {
+            const uint4 pk = pack8(o);
+            *reinterpret_cast<uint4*>(Y) = pk;
+            unpack8(pk, o);  // statistics of the value as stored (bf16-rounded)
+        } else {
+            store8(Y, o);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            st_s[j] = o[j];
+            st_q[j] = o[j] * o[j];
+        }
+    }
+    if (FLAT || !a.stat_part) return;
+    // rows of this wave: 32 per column vector (lane & 1); lanes -> wave partial, then the two waves of each 64-row half
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int m = 2; m < 64; m <<= 1) {
+            st_s[j] += __shfl_xor(st_s[j], m, 64);
+            st_q[j] += __shfl_xor(st_q[j], m, 64);
+        }
+    }
+    if (lane < 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            red[wave][lane][j][0] = st_s[j];
+            red[wave][lane][j][1] = st_q[j];
+        }
+    }
+    __syncthreads();
+    if (tid < 32) {
+        const int half = tid >> 4, c16 = tid & 15, cv = c16 >> 3, j = c16 & 7;
+        const int c = by * BCO + cg * 16 + c16;
+        const int r0 = t0 + half * 64;
+        if (c < a.Co && r0 < a.T_out) {
+            const float ss = red[2 * half][cv][j][0] + red[2 * half + 1][cv][j][0];
+            const float qq = red[2 * half][cv][j][1] + red[2 * half + 1][cv][j][1];
+            const int nch = (a.T_out + 63) / 64;
+            float* P = reinterpret_cast<float*>(a.stat_part) + (((long)bq * nch + r0 / 64) * a.stat_ld + c) * 2;
+            P[0] = ss;
+            P[1] = qq;
+        }
+    }
+}
+
 size_t lds_bytes(int rows_in, int cic, int nslot = NSLOT) {
     const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + (size_t)nslot * SLOT_BYTES + 4 * 128 * 4;
     const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
@@ -339,6 +506,25 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     if constexpr (F8) {
         return STZS_EDTYPE;  // (unreachable: fp8 is a pure linear)
     } else {
+        // DEEP slices hand their partials to splitk_epi (vectorised epilogue, no DiT row gate) unless STZS_CONV_SK_TICKET
+        const bool ske = deep && epi_vec(a) && !(flat && a.gate) && a.ups == 0 && !(a.flags & STZS_CONV_SK_TICKET);
+        if (ske) {
+            if (flat)
+                k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE, true, true>;
+            else if (a.pro_act == STZS_ACT_LEAKY)
+                k = conv_mfma<TIn, TOut, false, STZS_ACT_LEAKY, true, true>;
+            else if (a.pro_act == STZS_ACT_NONE)
+                k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE, true, true>;
+            else
+                k = conv_mfma<TIn, TOut, false, STZS_ACT_SNAKE, true, true>;
+            if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, a);
+            STZS_LAUNCH_CHECK();
+            auto ke = flat ? splitk_epi<TOut, true> : splitk_epi<TOut, false>;
+            hipLaunchKernelGGL(ke, dim3(grid.x, grid.y * 8), dim3(NTHR), 0, s, a, (int)a.splitk);
+            STZS_LAUNCH_CHECK();
+            return STZS_OK;
+        }
         if (deep) {
             if (flat)
                 k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE, true>;

@@ -32,7 +32,7 @@
 
 namespace {
 
-constexpr int MROWS = 64;   // utterances per group (4 MFMA row tiles)
+constexpr int MROWS = 64;   // utterances per group at most (4 MFMA row tiles): the slab / LDS capacity of a group
 constexpr int UNITS = 32;   // hidden units per workgroup
 constexpr unsigned SPIN_LIMIT = 1u << 22;
 constexpr int TAG_ROWS = 2;  // groups with <= TAG_ROWS valid rows use granules (32: bench -3%, the sweep's bytes)
@@ -72,7 +72,9 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 STZS_DEV float acc_sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
 
-template <int NKS, bool PR>
+// GR: utterances per group (16 / 32 / 64, lstm_group_rows: more workgroups, less MFMA / h-load / cell work per step
+// and group; every row's gate chain and cell update are the same, so the result does not depend on GR)
+template <int NKS, bool PR, int GR = MROWS>
 __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.H, G4 = 4 * H;
@@ -86,8 +88,8 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     const int gate = wave & 3, mh = wave >> 2;  // 8 waves: two per gate, each half of the row tiles
     const int p = blockIdx.x, dir = blockIdx.y, grp = blockIdx.z;
     const int P = H / UNITS;
-    const int b0 = grp * MROWS;
-    const int nrows = min(MROWS, a.B - b0);
+    const int b0 = grp * GR;
+    const int nrows = min(GR, a.B - b0);
     const int nmt = (nrows + 15) >> 4;
     // exchange slab [group][dir][2][64][NH H] bf16, counters [group][dir] (16 words apart)
     bf16_t* X = reinterpret_cast<bf16_t*>(reinterpret_cast<unsigned char*>(a.xchg) + TAG_BYTES) +
@@ -244,7 +246,9 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
                 const float fg = dpp_f<0x55>(act), gt = dpp_f<0xAA>(act), og = dpp_f<0xFF>(act);  // quad lanes 1, 2, 3
                 c1 = cell_c(act, fg, gt, c1);  // (meaningful in the g = 0 lane)
                 const float h = cell_h(og, c1);
-                const float h1 = __shfl_down(h, 4, 64);  // unit u + 1's h (its g = 0 lane)
+                // unit u + 1's h (its g = 0 lane, 4 lanes up -- inside the same 16-lane row for the even units that
+                // publish): DPP row_shl:4 instead of a ds_bpermute round trip
+                const float h1 = dpp_f<0x104>(h);
                 if (g == 0 && (u & 1) == 0) {
                     const unsigned pr = pack2bf(h, h1);
                     gu64* gp8 = gran + (s & 1) * TAG_ROWS * (H / 2) + row * (H / 2) + (p * UNITS + u) / 2;
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         }
     }
     __syncthreads();
-    if (s_last && a.B - (int)(gridDim.z - 1) * MROWS <= TAG_ROWS && !PR) {  // the last group ran tagged: its granules back to zero
+    if (s_last && a.B - (int)(gridDim.z - 1) * GR <= TAG_ROWS && !PR) {  // the last group ran tagged: its granules back to zero
         gu64* g0 = (gu64*)(a.xchg);
         for (int e = tid; e < TAG_BYTES / 8; e += 512) __hip_atomic_store(g0 + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -352,8 +356,25 @@ extern "C" int stzs_lstm_state_reset(void* sync, void* xchg, void* stream) {
     return STZS_OK;
 }
 
+// utterances per group: 16 above 16 utterances (one MFMA row tile: the step's MFMA, h-load and cell work of a
+// 16-row group; measured at B = 64 x H = 256, tools/probe/lstm_prof.py: 2.7 us per step vs 3.1 at 32 rows and 3.8 at
+// 64), falling back to 32 / 64 where the grid would not stay co-resident (<= 63 groups x directions, <= 256
+// workgroups).  STZS_LSTM_GROUP=32|64 caps the group (A/B switch -- the result is the same either way)
+static int lstm_group_rows(int B, int H, int ndir) {
+    static const int force = [] {
+        const char* e = getenv("STZS_LSTM_GROUP");
+        return e ? atoi(e) : 0;
+    }();
+    if (B <= 16) return MROWS;
+    for (int gr = 16; gr < MROWS; gr *= 2) {
+        const int g = (B + gr - 1) / gr;
+        if (gr >= force && g * ndir <= 63 && (H / UNITS) * ndir * g <= 256) return gr;
+    }
+    return MROWS;
+}
+
 extern "C" size_t stzs_lstm_workspace(int B, int H, int ndir) {
-    const int groups = (B + MROWS - 1) / MROWS;
+    const int groups = (B + lstm_group_rows(B, H, ndir) - 1) / lstm_group_rows(B, H, ndir);
     // the small-batch granule region, then the slab (sized for the precise hi | lo rows)
     return (size_t)TAG_BYTES + (size_t)groups * ndir * 2 * MROWS * 2 * H * sizeof(bf16_t);
 }
@@ -363,7 +384,8 @@ extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     if (a->B <= 0 || a->T <= 0 || a->H <= 0 || a->H > 256 || a->H % UNITS || (a->ndir != 1 && a->ndir != 2))
         return STZS_ESHAPE;
     if (a->ldg % 8 || a->bsg % 8 || a->ldy % 8 || a->bsy % 8) return STZS_ESHAPE;
-    const int groups = (a->B + MROWS - 1) / MROWS;
+    const int gr = lstm_group_rows(a->B, a->H, a->ndir);
+    const int groups = (a->B + gr - 1) / gr;
     const int P = a->H / UNITS;
     if (groups * a->ndir > 63 || P * a->ndir * groups > 256) return STZS_ESHAPE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -378,7 +400,8 @@ extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     switch (a->H / 32) {
 #define STZS_LSTM_CASE(n)                                                                                   \
     case n: {                                                                                               \
-        auto k = a->precise ? lstm_xchg<n, true> : lstm_xchg<n, false>;                                     \
+        auto k = a->precise ? (gr == 32 ? lstm_xchg<n, true, 32> : gr == 16 ? lstm_xchg<n, true, 16> : lstm_xchg<n, true>) \
+                            : (gr == 32 ? lstm_xchg<n, false, 32> : gr == 16 ? lstm_xchg<n, false, 16> : lstm_xchg<n, false>); \
         if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
         hipLaunchKernelGGL(k, grid, dim3(512), lds, s, *a);                                                 \
         break;                                                                                              \

@@ -28,6 +28,7 @@ CONV_UPS_NOISE = 4096  # include/stzs.h STZS_CONV_UPS_NOISE (ConvTranspose + fus
 CONV_MRFV_NARROW = 8192  # include/stzs.h STZS_CONV_MRFV_NARROW (register-direct MRF conv at 128 channels per workgroup)
 CONV_MRFV_T128 = 32768  # include/stzs.h STZS_CONV_MRFV_T128 (register-direct MRF conv: keep 128-row tiles on small grids)
 CONV_RING = 65536  # include/stzs.h STZS_CONV_RING (split-K conv_mfma: keep the 3-slot weight ring)
+CONV_SK_TICKET = 131072  # include/stzs.h STZS_CONV_SK_TICKET (DEEP split-K: last-arriver combine)
 CONV_W_FRAG32X3 = 16384  # include/stzs.h STZS_CONV_W_FRAG32X3 (precise register-direct MRF conv, csrc/mrfx.hip)
 
 vp = C.c_void_p

@@ -517,8 +517,8 @@ def _v0_lstm(In=640, H=256, seed=9):
 
 @pytest.mark.parametrize("B,T", [(64, 80), (40, 23), (1, 80), (2, 50), (65, 7)])
 def test_lstm_v0_width(eng, B, T):
-    """the benchmarked LSTM shape: H = 256 (8 exchanging workgroups per direction), up to 64 utterances per
-    group (4 MFMA row tiles, multi-row exchange loads) vs torch.nn.LSTM on identical bf16 inputs; B = 1 / 2 and
+    """the benchmarked LSTM shape: H = 256 (8 exchanging workgroups per direction), 16-64 utterances per
+    group (1-4 MFMA row tiles, multi-row exchange loads) vs torch.nn.LSTM on identical bf16 inputs; B = 1 / 2 and
     the 1-row last group of B = 65 hand h over as tagged granules (csrc/lstm.hip TAG_ROWS), run twice: the second
     call must not see the first call's tags (bit-identical).
     tolerance: max-abs error <= 2e-2 of max|ref| (bf16 h exchanged every step, fp32 cell state)."""
@@ -539,6 +539,25 @@ def test_lstm_v0_width(eng, B, T):
     e = max_rel(y.t.float().cpu(), ref)
     print("lstm v0", B, T, e, rel_err(y.t.float().cpu(), ref))
     assert e < 2e-2
+
+
+def test_lstm_group_rows_invariant(eng):
+    """B = 64 runs as four 16-utterance groups (csrc/lstm.hip lstm_group_rows: 64 workgroups, one MFMA row tile of
+    work per group and step), B = 32 as two, B = 16 as one group, B = 1 on the tagged granules: every utterance's h
+    must be the same bits in all four (the per-row gate chain and cell update do not depend on the group)."""
+    from stzs.engine import Act
+    _P, lw, _A = _v0_lstm()
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(64, 60, 640, generator=g).to(torch.bfloat16).cuda()
+    outs = {}
+    for B in (64, 32, 16, 1):
+        y = Act(torch.zeros(B, 60, 512, dtype=torch.bfloat16, device="cuda:0"))
+        eng.lstm(lw, Act(x[:B].contiguous()), y, f"t.lstmg{B}")
+        assert eng.check_status() == 0
+        outs[B] = y.t.clone()
+    assert torch.equal(outs[64][:32], outs[32])
+    assert torch.equal(outs[64][:16], outs[16])
+    assert torch.equal(outs[64][:1], outs[1])
 
 
 def test_lstm_timeout_tagged_never_hangs(eng):

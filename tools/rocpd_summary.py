@@ -1,7 +1,7 @@
 """Per-kernel summary of a rocprofv3 SQLite output (`rocprofv3 --kernel-trace -d DIR -o p`): calls, average and
 total duration per (kernel, grid), largest total first.
 
-    python tools/rocpd_summary.py gpurun_out/DIR/p_results.db [name filter] [--per N]   (--per: divide totals by N)
+    python tools/rocpd_summary.py gpurun_out/DIR/p_results.db [name regex] [--per N]   (--per: divide totals by N)
 """
 import re
 import sqlite3
@@ -20,7 +20,7 @@ q = """select s.kernel_name, count(*), sum(k.end - k.start), k.grid_size_x / k.w
 tot = 0
 for n, cnt, t, gx, gy, gz in c.execute(q):
     short = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", n).replace("Ev14stzs_conv_args.kd", "").replace(".kd", "")[:64]
-    if flt and flt not in n:
+    if flt and not re.search(flt, n):
         continue
     tot += t
     print(f"{short:64s} {cnt / per:8.1f} x {t / cnt / 1e3:8.2f} us = {t / per / 1e3:9.1f} us  grid {gx}x{gy}x{gz}")
