@@ -106,6 +106,16 @@ typedef struct stzs_conv_args {
     unsigned int* splitk_ctr;
     int32_t splitk;
     int32_t pad_sk;
+    /* optional (the generic conv path only -- no STZS_CONV_W_* / A_DMA / ROWS flag): the AdaIN prologue's
+     * statistics straight from InstanceNorm partials instead of pro_mean / pro_rstd.  When pro_part != NULL,
+     * mean and rstd of (utterance b, channel c) are computed in the prologue from the fp32 (sum, sumsq) pairs
+     * pro_part[((b * pro_nch + k) * pro_ld + c) * 2 + {0, 1}], k < pro_nch <= 8 (the layout of
+     * stzs_chan_stats_partial and of the conv's own fused statistics), over pro_T input rows with pro_eps,
+     * in fp64 in the order of stzs_chan_stats_final -- the same bits as finalising first (one launch less). */
+    const float* pro_part;
+    int64_t pro_ld;
+    int32_t pro_nch, pro_T;
+    float pro_eps, pad_pp;
 } stzs_conv_args;
 /* split-K workspace of a linear over `rows` flat rows: fp32 slab bytes; the tile (= counter) count is
  * bytes / (splitk * 32768).  0 for a bad argument. */
@@ -204,6 +214,10 @@ typedef struct stzs_stats_args {
 } stzs_stats_args;
 size_t stzs_chan_stats_workspace(int B, int T, int C);
 int stzs_chan_stats(const stzs_stats_args* a, void* stream);
+/* pass 1 of stzs_chan_stats alone: the fp32 (sum, sumsq) partials of every 256-row chunk into a->partial
+ * ([B][ceil(T / 256)][C][2]; mean / rstd not written, may be NULL) -- for a consumer that finalises them itself
+ * (stzs_conv_args.pro_part) or a later stzs_chan_stats_final(a, 256). */
+int stzs_chan_stats_partial(const stzs_stats_args* a, void* stream);
 /* second pass only: mean / rstd from a partial slab already holding ceil(T / chunk_rows) chunks
  * (written by stzs_conv1d's stat_part epilogue with chunk_rows = STZS_CONV_STAT_ROWS); x unused. */
 int stzs_chan_stats_final(const stzs_stats_args* a, int chunk_rows, void* stream);

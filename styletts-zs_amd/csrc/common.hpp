@@ -29,6 +29,17 @@ STZS_DEV uint32_t pack2bf(float a, float b) {
 // (id % 8 labels the blocks that share an L2), so give each such group a CONTIGUOUS range of tiles --
 // neighbouring time tiles then share their dilation halos (and weight K-steps) in one L2.  Speed only: any
 // bijection is correct (cdna_hip_programming.md T1, bijective form for nwg % 8 != 0).
+// InstanceNorm mean / rstd from the fp64 (sum, sumsq) of T rows, every rounding explicit (no contraction choice left
+// to the compiler): stzs_chan_stats_final and the conv prologue's pro_part path (conv.hip) give the same bits
+STZS_DEV void stat_finish(double s, double q, int T, float eps, float& mu, float& rs) {
+#pragma clang fp contract(off)
+    const double mean = s / (double)T;
+    double var = q / (double)T - mean * mean;
+    if (var < 0.0) var = 0.0;
+    mu = (float)mean;
+    rs = (float)(1.0 / __dsqrt_rn(var + (double)eps));
+}
+
 STZS_DEV int xcd_remap(int bid, int nwg) {
     const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);

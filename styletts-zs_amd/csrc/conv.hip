@@ -168,8 +168,25 @@ __global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_
             float sc = 0.f, sh = 0.f, al = 1.f;
             if (cg < a.Ci) {
                 if (a.pro_mode == STZS_PRO_ADAIN) {
-                    const float mu = a.pro_mean[(long)bq * a.stat_bs + cg];
-                    const float rs = a.pro_rstd[(long)bq * a.stat_bs + cg];
+                    float mu, rs;
+                    if (a.pro_part) {  // statistics from the partials (stzs_conv_args.pro_part: <= 8 chunks)
+                        const float2* Pp = reinterpret_cast<const float2*>(a.pro_part) + (long)bq * a.pro_nch * a.pro_ld + cg;
+                        float2 pv[8];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if (k < a.pro_nch) pv[k] = Pp[(long)k * a.pro_ld];
+                        double ssum = 0.0, qsum = 0.0;  // chunk order, as stzs_chan_stats_final's groups
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if (k < a.pro_nch) {
+                                ssum += (double)pv[k].x;
+                                qsum += (double)pv[k].y;
+                            }
+                        stat_finish(ssum, qsum, a.pro_T, a.pro_eps, mu, rs);
+                    } else {
+                        mu = a.pro_mean[(long)bq * a.stat_bs + cg];
+                        rs = a.pro_rstd[(long)bq * a.stat_bs + cg];
+                    }
                     const float g = a.pro_gb[(long)bq * a.gb_bs + cg];
                     const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + cg];
                     sc = (1.f + g) * rs;
@@ -576,7 +593,12 @@ __attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args*
         return STZS_EINVAL;
     }
     if (a->res && a->res_tdiv <= 0) return STZS_EINVAL;
-    if (a->pro_mode == STZS_PRO_ADAIN && (!a->pro_mean || !a->pro_rstd || !a->pro_gb)) return STZS_EINVAL;
+    if (a->pro_part && (a->pro_nch < 1 || a->pro_nch > 8 || a->pro_T < 1 || a->pro_ld < a->Ci ||
+                        (a->flags & (STZS_CONV_W_X3 | STZS_CONV_W_F32 | STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 |
+                                     STZS_CONV_W_FRAG32 | STZS_CONV_W_FRAG32X3 | STZS_CONV_ROWS | STZS_CONV_A_DMA))))
+        return STZS_EINVAL;  // (the prologue partials: generic conv path, <= 8 chunks)
+    if (a->pro_mode == STZS_PRO_ADAIN && (!a->pro_part && (!a->pro_mean || !a->pro_rstd)) ) return STZS_EINVAL;
+    if (a->pro_mode == STZS_PRO_ADAIN && !a->pro_gb) return STZS_EINVAL;
     if (a->pro_act == STZS_ACT_SNAKE && !a->pro_alpha) return STZS_EINVAL;
     if (a->stat_part && (a->ups > 0 || !epi_vec(*a) || a->stat_ld < a->Co || !stzs_aligned(a->stat_part, 8)))
         return STZS_EINVAL;

@@ -10,6 +10,8 @@ int stzs_rows_gemm_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/ro
 int stzs_mrfx_conv_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/mrfx.hip
 
 extern "C" int stzs_conv1d(const stzs_conv_args* a, void* stream) {
+    // prologue statistics from partials (pro_part): the generic conv path only (csrc/conv.hip checks the rest)
+    if (a && a->pro_part && (a->flags & (STZS_CONV_W_FRAG32X3 | STZS_CONV_W_FRAG32 | STZS_CONV_ROWS))) return STZS_EINVAL;
     if (a && (a->flags & STZS_CONV_W_FRAG32X3)) {  // the precise register-direct form
         if (!a->x || !a->w || !a->y) return STZS_EINVAL;
         if (a->flags & (STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 | STZS_CONV_W_F32 | STZS_CONV_W_X3 | STZS_CONV_A_DMA |

@@ -91,14 +91,14 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     const int b0 = grp * GR;
     const int nrows = min(GR, a.B - b0);
     const int nmt = (nrows + 15) >> 4;
-    // exchange slab [group][dir][2][64][NH H] bf16, counters [group][dir] (16 words apart)
+    // exchange slab [group][dir][2][GR][NH H] bf16, counters [group][dir] (16 words apart)
     bf16_t* X = reinterpret_cast<bf16_t*>(reinterpret_cast<unsigned char*>(a.xchg) + TAG_BYTES) +
-                ((long)(grp * a.ndir + dir) * 2) * MROWS * NH * H;
+                ((long)(grp * a.ndir + dir) * 2) * GR * NH * H;
     const bool tagged = !PR && nrows <= TAG_ROWS;  // uniform: the group's row count
     gu64* gran = (gu64*)(a.xchg) + dir * 2 * TAG_ROWS * (H / 2);  // this direction's [parity][row][H/2] granules
     gu32* ctr = (gu32*)(a.sync) + (grp * a.ndir + dir) * 16;
     // the slab through a buffer descriptor: 16-B write-through (sc1, aux 16) stores and loads
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(X, 0, 2 * MROWS * NH * H * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(X, 0, 2 * GR * NH * H * 2, 0x00020000);
     gu32* err = (gu32*)(a.sync) + 1023;
     gu32* status = (gu32*)a.status;
     const unsigned limit = a.spin_limit ? a.spin_limit : SPIN_LIMIT;
@@ -186,8 +186,8 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
             PROF(1)
             __syncthreads();
             // h_{s-1}: MROWS x H bf16 = H/8 16-B words per row, all of this thread's sc1 loads in flight
-            const int base = ((s - 1) & 1) * MROWS * NH * H * 2;
-            constexpr int NWT = MROWS * NH * NKS * 32 / 8;     // 16-B words of h (H = 32 NKS)
+            const int base = ((s - 1) & 1) * GR * NH * H * 2;
+            constexpr int NWT = GR * NH * NKS * 32 / 8;        // 16-B words of h (H = 32 NKS)
             constexpr int NW = (NWT + 511) / 512;              // per thread
             // only the group's valid rows (a batch-1 group moves 1/64 of the slab); rows >= nrows of the A
             // tile stay as zeroed at s = 0 and only feed gate rows no cell reads
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         const uint2 hb = make_uint2(pack2bf(hv[0], hv[1]), pack2bf(hv[2], hv[3]));
         if (cvalid) {
             const __attribute__((ext_vector_type(2))) unsigned int hw = {hb.x, hb.y};
-            const int so = ((s & 1) * MROWS * NH * H + crow * NH * H + p * UNITS + cu0) * 2;
+            const int so = ((s & 1) * GR * NH * H + crow * NH * H + p * UNITS + cu0) * 2;
             __builtin_amdgcn_raw_buffer_store_b64(hw, xr, so, 0, 16);
             if constexpr (PR) {  // lo = bf16(h - hi) (exact difference)
                 float hf[4];
@@ -376,7 +376,7 @@ static int lstm_group_rows(int B, int H, int ndir) {
 extern "C" size_t stzs_lstm_workspace(int B, int H, int ndir) {
     const int groups = (B + lstm_group_rows(B, H, ndir) - 1) / lstm_group_rows(B, H, ndir);
     // the small-batch granule region, then the slab (sized for the precise hi | lo rows)
-    return (size_t)TAG_BYTES + (size_t)groups * ndir * 2 * MROWS * 2 * H * sizeof(bf16_t);
+    return (size_t)TAG_BYTES + (size_t)groups * ndir * 2 * lstm_group_rows(B, H, ndir) * 2 * H * sizeof(bf16_t);
 }
 
 extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {

@@ -113,11 +113,10 @@ __global__ __launch_bounds__(256) void chan_stats_final(const stzs_stats_args a,
             s += red[y][tid][0];
             q += red[y][tid][1];
         }
-        const double mean = s / a.T;
-        double var = q / a.T - mean * mean;
-        if (var < 0.0) var = 0.0;
-        a.mean[(long)b * a.stat_bs + c] = (float)mean;
-        a.rstd[(long)b * a.stat_bs + c] = (float)(1.0 / sqrt(var + (double)a.eps));
+        float mu, rs;
+        stat_finish(s, q, a.T, a.eps, mu, rs);  // (common.hpp: the same rounding as the conv prologue's pro_part path)
+        a.mean[(long)b * a.stat_bs + c] = mu;
+        a.rstd[(long)b * a.stat_bs + c] = rs;
     }
 }
 
@@ -157,11 +156,9 @@ extern "C" size_t stzs_chan_stats_workspace(int B, int T, int C) {
     return (size_t)B * nchunk * C * 2 * sizeof(float);
 }
 
-extern "C" int stzs_chan_stats(const stzs_stats_args* a, void* stream) {
-    if (!a || !a->x || !a->mean || !a->rstd || !a->partial) return STZS_EINVAL;
+static int chan_stats_pass1(const stzs_stats_args* a, hipStream_t s, int* nchunk_out) {
     if (a->B <= 0 || a->T <= 0 || a->C <= 0 || a->ld % 8 || a->bs % 8 || a->ld < a->C) return STZS_ESHAPE;
     if (a->C % 8) return STZS_ESHAPE;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int nchunk = (a->T + STAT_ROWS - 1) / STAT_ROWS;
     dim3 g1(nchunk, a->B, (a->C + STAT_CG * 8 - 1) / (STAT_CG * 8));
     if (a->dtype == STZS_BF16)
@@ -170,6 +167,25 @@ extern "C" int stzs_chan_stats(const stzs_stats_args* a, void* stream) {
         hipLaunchKernelGGL(chan_stats_partial<float>, g1, dim3(256), 0, s, *a, nchunk);
     else
         return STZS_EDTYPE;
+    *nchunk_out = nchunk;
+    return STZS_OK;
+}
+
+extern "C" int stzs_chan_stats_partial(const stzs_stats_args* a, void* stream) {
+    if (!a || !a->x || !a->partial) return STZS_EINVAL;
+    int nchunk = 0;
+    const int rc = chan_stats_pass1(a, reinterpret_cast<hipStream_t>(stream), &nchunk);
+    if (rc != STZS_OK) return rc;
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_chan_stats(const stzs_stats_args* a, void* stream) {
+    if (!a || !a->x || !a->mean || !a->rstd || !a->partial) return STZS_EINVAL;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int nchunk = 0;
+    const int rc = chan_stats_pass1(a, s, &nchunk);
+    if (rc != STZS_OK) return rc;
     STZS_LAUNCH_CHECK();
     hipLaunchKernelGGL(chan_stats_final, dim3(a->B, (a->C + FIN_CH - 1) / FIN_CH), dim3(256), 0, s, *a, nchunk);
     STZS_LAUNCH_CHECK();

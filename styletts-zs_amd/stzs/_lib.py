@@ -47,7 +47,8 @@ class ConvArgs(C.Structure):
                                    "in_dtype", "out_dtype", "pro_mode", "pro_act", "epi_act", "flags")] + \
                [(n, f32) for n in ("pro_cscale", "pro_slope", "epi_slope", "alpha", "beta", "pad_f")] + \
                [("stat_part", vp), ("stat_ld", i64), ("x_scale", vp), ("w_scale", vp),
-                ("splitk_ws", vp), ("splitk_ctr", vp), ("splitk", i32), ("pad_sk", i32)]
+                ("splitk_ws", vp), ("splitk_ctr", vp), ("splitk", i32), ("pad_sk", i32),
+                ("pro_part", vp), ("pro_ld", i64), ("pro_nch", i32), ("pro_T", i32), ("pro_eps", f32), ("pad_pp", f32)]
 
 
 class StatsArgs(C.Structure):
@@ -207,7 +208,7 @@ def params(ints=(), floats=()) -> Params:
 EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_conv_splitk_workspace",
            "stzs_conv_rows_workspace",
            "stzs_chan_stats_workspace",
-           "stzs_chan_stats", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_ln_linear", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm",
+           "stzs_chan_stats", "stzs_chan_stats_partial", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_ln_linear", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm",
            "stzs_lstm_state_reset", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
@@ -242,6 +243,7 @@ def load():
         "stzs_conv_rows_workspace": ([i64, i32, i32], C.c_size_t),
         "stzs_chan_stats_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
+        "stzs_chan_stats_partial": ([P(StatsArgs), vp], i32),
         "stzs_chan_stats_final": ([P(StatsArgs), i32, vp], i32),
         "stzs_row_layernorm": ([P(RowLNArgs), vp], i32),
         "stzs_ln_linear": ([P(ConvArgs), P(RowLNArgs), vp], i32),

@@ -152,6 +152,54 @@ def fourier_features(spec: Spec, c_noise: float) -> np.ndarray:
     return np.concatenate([np.cos(arg), np.sin(arg)]).astype(np.float32)
 
 
+class _StatsRef:
+    """InstanceNorm statistics as fp32 (sum, sumsq) partials of `nch` chunks of `chunk_rows` rows, [B][nch][ld][2]
+    in `part`, finalised into mean / rstd (stzs_chan_stats_final) only when something needs them: a generic-path
+    conv reads the partials in its AdaIN prologue instead (stzs_conv_args.pro_part, the same bits)."""
+
+    def __init__(self, eng, part, ld, nch, T, B, mean, rstd, chunk_rows):
+        self.eng, self.part, self.ld, self.nch, self.T, self.B = eng, part, ld, nch, T, B
+        self.mean, self.rstd, self.chunk_rows, self.done = mean, rstd, chunk_rows, False
+
+    def finalize(self):
+        if not self.done:
+            s = L.StatsArgs()
+            s.mean, s.rstd, s.partial = self.mean.data_ptr(), self.rstd.data_ptr(), self.part.data_ptr()
+            s.stat_bs, s.B, s.T, s.C, s.eps = self.ld, self.B, self.T, self.ld, 1e-5
+            self.eng.launches += 1
+            L.check(self.eng.lib.stzs_chan_stats_final(C.byref(s), self.chunk_rows, self.eng.stream()),
+                    "chan_stats_final")
+            self.done = True
+
+    def mean_ptr(self):
+        self.finalize()
+        return self.mean.data_ptr()
+
+    def rstd_ptr(self):
+        self.finalize()
+        return self.rstd.data_ptr()
+
+
+class _StatPtr:
+    """the mean (which 0) or rstd (1) of a _StatsRef, usable wherever a tensor's data_ptr() is taken (finalises)."""
+
+    def __init__(self, ref, which):
+        self.ref, self.which = ref, which
+
+    def data_ptr(self):
+        return self.ref.mean_ptr() if self.which == 0 else self.ref.rstd_ptr()
+
+    def tensor(self):
+        self.ref.finalize()
+        return self.ref.mean if self.which == 0 else self.ref.rstd
+
+    def clone(self):
+        return self.tensor().clone()
+
+    def __getitem__(self, k):
+        return self.tensor()[k]
+
+
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
                  packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None, dn_rows=None,
@@ -211,6 +259,10 @@ class StyleTTSZS:
         self.te_splitk = int(os.environ.get("STZS_TE_SPLITK", TE_SPLITK)) if te_splitk is None else int(te_splitk)
         # split-K slices of the bf16 AdaIN-block convs (LATENCY_BLK_SPLITK); 0 = the register-direct form
         self.blk_splitk = int(os.environ.get("STZS_BLK_SPLITK", BLK_SPLITK)) if blk_splitk is None else int(blk_splitk)
+        # InstanceNorm statistics of <= 8 partial chunks handed to the consuming generic-path conv unfinalised
+        # (stzs_conv_args.pro_part: the prologue finalises them, bit-identical, one launch less per statistics) --
+        # the engines whose AdaIN-block convs run the generic path (blk_splitk); STZS_DEFER_STATS=0|1 overrides
+        self.defer_stats = os.environ.get("STZS_DEFER_STATS", "1" if self.blk_splitk else "0") != "0"
         # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
         # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
@@ -347,10 +399,15 @@ class StyleTTSZS:
             a.T_out = T_out if T_out is not None else (x.T + 2 * pad - dil * (cw.ks - 1) - 1) // stride + 1
         a.ci_pad, a.co_pad, a.cic = cw.ci_pad, cw.co_pad, cw.cic
         a.in_dtype, a.out_dtype = x.dt, y.dt
+        pro_ref = None
         if pro is not None:  # AdaIN: (mean, rstd, stat_bs, gb_ptr, gb_bs, beta_off)
             mean, rstd, stat_bs, gbp, gb_bs, boff = pro
             a.pro_mode = L.PRO_ADAIN
-            a.pro_mean, a.pro_rstd, a.stat_bs = mean.data_ptr(), rstd.data_ptr(), stat_bs
+            if isinstance(mean, _StatPtr) and not mean.ref.done:
+                pro_ref = mean.ref  # (resolved below, once the path is known)
+            else:
+                a.pro_mean, a.pro_rstd = mean.data_ptr(), rstd.data_ptr()
+            a.stat_bs = stat_bs
             a.pro_gb, a.gb_bs, a.gb_beta_off = gbp, gb_bs, boff
         a.pro_act, a.pro_slope, a.pro_cscale = pro_act, pro_slope, cscale
         a.pro_alpha = self._t(pro_alpha).data_ptr() if pro_alpha is not None else None
@@ -433,14 +490,24 @@ class StyleTTSZS:
             a.splitk = splitk
             a.splitk_ws = self._scratch("csk_ws", tiles * splitk * 16384).data_ptr()
             a.splitk_ctr = self._counters("csk_ctr", tiles).data_ptr()
+        if pro_ref is not None:
+            generic = not (a.flags & (8 | L.CONV_ROWS | L.CONV_W_X3 | L.CONV_W_F32 | L.CONV_W_FRAG32 |
+                                      L.CONV_W_LANE16 | L.CONV_W_NARROW32 | L.CONV_W_FRAG32X3)) and not cw.f8
+            if generic and pre_ln is None:  # the prologue finalises the partials itself
+                a.pro_part, a.pro_ld, a.pro_nch, a.pro_T, a.pro_eps = pro_ref.part.data_ptr(), pro_ref.ld, pro_ref.nch, \
+                    pro_ref.T, 1e-5
+            else:
+                a.pro_mean, a.pro_rstd = pro_ref.mean_ptr(), pro_ref.rstd_ptr()
         st = None
         if stats_key is not None:
             Cc = _rup(cw.Co, 8)
             ntile = (a.T_out + L.CONV_STAT_ROWS - 1) // L.CONV_STAT_ROWS
-            slab = self._slab(y.B * ntile * Cc * 2)
+            defer = self.defer_stats and ntile <= 8
+            # (deferred: the partials must outlive this launch until their consumer reads them -- a slab per key)
+            slab = self._scratch("stat_slab." + stats_key, y.B * ntile * Cc * 2) if defer else self._slab(y.B * ntile * Cc * 2)
             a.stat_part, a.stat_ld = slab.data_ptr(), Cc
             st = (slab, Cc, self.buf(stats_key + ".m", (y.B, Cc), torch.float32),
-                  self.buf(stats_key + ".r", (y.B, Cc), torch.float32))
+                  self.buf(stats_key + ".r", (y.B, Cc), torch.float32), defer, ntile)
         tm = self.timer
         launch = lambda: self.lib.stzs_conv1d(C.byref(a), self.stream())
         fused = False
@@ -499,13 +566,12 @@ class StyleTTSZS:
             self.attention(*attn)
         if st is None:
             return y
-        slab, Cc, mean, rstd = st
-        s = L.StatsArgs()
-        s.mean, s.rstd, s.partial = mean.data_ptr(), rstd.data_ptr(), slab.data_ptr()
-        s.stat_bs, s.B, s.T, s.C, s.eps = Cc, y.B, a.T_out, Cc, 1e-5
-        self.launches += 1
-        L.check(self.lib.stzs_chan_stats_final(C.byref(s), L.CONV_STAT_ROWS, self.stream()), "chan_stats_final")
-        return y, (mean, rstd, Cc)
+        slab, Cc, mean, rstd, defer, ntile = st
+        ref = _StatsRef(self, slab, Cc, ntile, a.T_out, y.B, mean, rstd, L.CONV_STAT_ROWS)
+        if not defer:
+            ref.finalize()
+            return y, (mean, rstd, Cc)
+        return y, (_StatPtr(ref, 0), _StatPtr(ref, 1), Cc)
 
     def _rows_z(self, cw: ConvW) -> int:
         """1 = the whole-chip small-M form (one K slice: no hand-off state) for a per-utterance linear whose K gives
@@ -582,16 +648,25 @@ class StyleTTSZS:
         return [(w, e0.elapsed_time(e1) * 1e-3, f, b, shp, stg) for (w, e0, e1, f, b, shp, stg) in tm["rec"]]
 
     def stats(self, x: Act, key):
-        """InstanceNorm statistics of x over time -> (mean, rstd, stat_bs)."""
+        """InstanceNorm statistics of x over time -> (mean, rstd, stat_bs); with defer_stats and <= 8 256-row chunks
+        only the partials pass runs here (the consuming conv's prologue, or the first other use, finalises)."""
         Cc = _rup(x.C, 8)
         mean = self.buf(key + ".m", (x.B, Cc), torch.float32)
         rstd = self.buf(key + ".r", (x.B, Cc), torch.float32)
-        ws = self._scratch("stat_ws", self.lib.stzs_chan_stats_workspace(x.B, x.T, Cc) // 4 + 1)
+        nch = (x.T + 255) // 256
+        defer = self.defer_stats and nch <= 8
+        nws = self.lib.stzs_chan_stats_workspace(x.B, x.T, Cc) // 4 + 1
+        ws = self._scratch("stat_ws." + key, nws) if defer else self._scratch("stat_ws", nws)
         a = L.StatsArgs()
         a.x, a.mean, a.rstd, a.partial = x.ptr, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr()
         a.ld, a.bs, a.stat_bs, a.B, a.T, a.C, a.dtype, a.eps = x.ld, x.bs, Cc, x.B, x.T, Cc, x.dt, 1e-5
-        self._call(self.lib.stzs_chan_stats, a, "chan_stats", cost=(0, x.B * x.T * x.C * x.t.element_size()))
-        return mean, rstd, Cc
+        cost = (0, x.B * x.T * x.C * x.t.element_size())
+        if not defer:
+            self._call(self.lib.stzs_chan_stats, a, "chan_stats", cost=cost)
+            return mean, rstd, Cc
+        self._call(self.lib.stzs_chan_stats_partial, a, "chan_stats", cost=cost)
+        ref = _StatsRef(self, ws, Cc, nch, x.T, x.B, mean, rstd, 256)
+        return _StatPtr(ref, 0), _StatPtr(ref, 1), Cc
 
     def rowln(self, x: Act, y: Act, *, G=None, gs=0, Bt=None, bs=0, gdiv=1, gadd=1.0, act=L.ACT_NONE, slope=0.0,
               R=None, y_scale=None, what="rowln"):

@@ -132,7 +132,7 @@ def test_istft_stream_spans_tile_the_output(Tf, chunks):
 
 
 _STRUCT_CALLS = [  # entry point, ctypes struct, extra int arguments between the struct and the stream
-    ("stzs_conv1d", "ConvArgs", ()), ("stzs_chan_stats", "StatsArgs", ()),
+    ("stzs_conv1d", "ConvArgs", ()), ("stzs_chan_stats", "StatsArgs", ()), ("stzs_chan_stats_partial", "StatsArgs", ()),
     ("stzs_chan_stats_final", "StatsArgs", (64,)), ("stzs_row_layernorm", "RowLNArgs", ()),
     ("stzs_quant_rows", "QuantArgs", ()), ("stzs_attention", "AttnArgs", ()), ("stzs_lstm", "LstmArgs", ()),
     ("stzs_predictor_prep", "PrPrepArgs", ()), ("stzs_durations", "DurArgs", ()),

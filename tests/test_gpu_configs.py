@@ -289,3 +289,26 @@ def test_latency_engine_batch_invariant(v0):
         o1 = e.synth(tok[i:i + 1], ref[i:i + 1], noise=eps[i:i + 1], durations=dur[i:i + 1], seeds=[seeds[i]], **kw)
         for k in ("codes", "F0", "wav"):
             assert torch.equal(o1[k].cpu(), keep[k][i:i + 1]), (i, k)
+
+
+def test_latency_engine_deferred_stats_bit_identical(v0):
+    """the latency engine hands InstanceNorm statistics of <= 8 partial chunks to the consuming split-K block conv
+    unfinalised (stzs_conv_args.pro_part: the prologue sums the partials in fp64 in stzs_chan_stats_final's order):
+    the synthesis must be the same bits as with every statistics finalised by its own launch, with fewer launches."""
+    from stzs.engine import latency_engine
+    S, P, eng = v0
+    e = latency_engine(S, eng.W, eng.device)
+    assert e.defer_stats
+    tok, ref, eps, dur, seeds = bench.rank_inputs(S, 2, 7)
+    kw = dict(steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG, noise=eps, durations=dur, seeds=seeds)
+    outs, launches = {}, {}
+    for d in (True, False):
+        e.defer_stats = d
+        n0 = e.launches
+        o = e.synth(tok, ref, **kw)
+        launches[d] = e.launches - n0
+        outs[d] = {k: o[k].detach().clone().cpu() for k in ("codes", "F0", "N", "wav")}
+    for k in outs[True]:
+        assert torch.equal(outs[True][k], outs[False][k]), k
+    print("launches deferred / finalised", launches[True], launches[False])
+    assert launches[True] < launches[False]
