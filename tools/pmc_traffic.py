@@ -32,17 +32,17 @@ def per_dispatch(counter):
 
 
 def shape(name, grid):
-    m = re.search(r"mrfv_conv<(\d+), (true|false), (true|false), (\d+), (\d+), (true|false), (\d+)>", name)
+    m = re.search(r"mrfv_conv<(\d+), (true|false), (true|false), (\d+), (\d+), (true|false), (\d+)(?:, (\d+))?>", name)
     if not m:
         return None
-    pact, hr, ha, ks, nch, _, wpw = m.groups()
-    ks, nch, wpw = int(ks), int(nch), int(wpw)
+    pact, hr, ha, ks, nch, _, wpw, bt = m.groups()
+    ks, nch, wpw, bt = int(ks), int(nch), int(wpw), int(bt or 128)
     st = 1 if nch == 1 else (2 if wpw == 2 else 0)
     if st == 0 or pact != "2":
         return None
     C, T = STAGE[st]
     wgs = grid // 256
-    B = wgs // ((T + 127) // 128)
+    B = wgs // ((T + bt - 1) // bt)  # (mrfv_conv<..., BT>: 128- or 64-row tiles)
     nop = 2 + (hr == "true") + (ha == "true")
     alg = B * T * C * 2 * nop + ks * C * C * 2
     form = "c1" if hr == "false" else ("c2+acc" if ha == "true" else "c2")
