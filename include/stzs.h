@@ -96,9 +96,10 @@ typedef struct stzs_conv_args {
      * stzs_conv_splitk_workspace() bytes; splitk_ctr: one uint32 per tile, ZERO before the first launch (every
      * launch leaves them zero).  Used for the batch-1 denoiser linears, whose 8-32 output tiles would otherwise
      * stream all of K through 8-32 CUs (configs[1]).
-     * Also on the generic bf16 conv (conv_mfma: k >= 1, no W_* / A_DMA / ROWS flag): splitk in 2..8 (at most the
+     * Also on the generic bf16 conv (conv_mfma: k >= 1, no W_* / A_DMA / ROWS flag): splitk in 2..16 (at most the
      * chunk count) splits the n = ci_pad / cic input-channel chunks, slice z taking chunks [z n / splitk,
-     * (z+1) n / splitk); each 128-row x 128-column tile (per utterance) sums its slices the same way.  splitk_ws:
+     * (z+1) n / splitk); each 128-row x 128-column tile (per utterance) sums its slices the same way (with one
+     * chunk per slice, the DEEP form: a second launch splitk_epi combines the slices -- same output bits).  splitk_ws:
      * B * ceil(T_out / 128) * (co_pad / 128) * splitk * 65536 bytes, splitk_ctr: one zeroed uint32 per tile.  Used
      * for the batch-1 text-encoder k5 convs (4 tiles x 80 K-steps otherwise) and the batch-1 decoder / predictor
      * AdaIN-block convs (16 tiles x 108 K-steps for a decoder conv1). */
