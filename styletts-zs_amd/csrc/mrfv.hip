@@ -394,6 +394,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
     void (*k)(stzs_conv_args) = nullptr;
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
+    bool blk_wide = false;
     // the wide form (256 output channels per workgroup) for multi-chunk Snake convs whose wide grid still gives every
     // CU two workgroups (at batch 1 a stage-0 conv has 32 row tiles: the narrow form's 64 workgroups finish sooner),
     // unless STZS_CONV_MRFV_NARROW.  Both forms are bit-identical, so the choice never changes a result.
@@ -415,14 +416,22 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
         k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide, t64))
               : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide, t64));
     } else if (!A && a.ks == 3) {  // the AdaIN residual blocks of the decoder / prosody predictor
+        // (r05) the wide form here too where the wide grid gives every CU two workgroups (a decoder conv at 64
+        // utterances: 512 wide tiles): each 9-chunk input row staged once per 256 output channels instead of per 128 --
+        // 111 -> 88 us per 1024-channel decoder conv at B = 64; at 32 utterances (256 wide tiles) the narrow form is as
+        // fast (56.4 vs 57.5 us), so it stays there (`tools/blk_probe.py` FRAG32=1).  Bit-identical.
+        blk_wide = a.ci_pad > 128 && a.co_pad % (2 * BCO) == 0 && wide_tiles >= 2 * stzs_cu_count() &&
+                   !(a.flags & STZS_CONV_MRFV_NARROW);
         if (a.pro_act == STZS_ACT_LEAKY)
-            k = R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true>;
+            k = blk_wide ? (R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true, 2> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true, 2>)
+                         : (R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true>);
         else if (a.pro_act == STZS_ACT_NONE)
-            k = R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0, true>;
+            k = blk_wide ? (R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0, true, 2> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0, true, 2>)
+                         : (R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0, true>);
     }
     if (!k) return STZS_ESHAPE;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / (wide ? 2 * BCO : BCO));
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / (wide || blk_wide ? 2 * BCO : BCO));
     hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;

@@ -389,13 +389,17 @@ WIDE_CASES = [
     (20, 3300, 256, 256, 7, 3, "snake", True, True, True, 1),    # stage-0 width, residual + accumulate + stats
     (18, 3700, 384, 256, 11, 5, "snake", True, False, True, 1),  # 3 input chunks, ragged last row tile
     (20, 3300, 256, 176, 3, 1, "snake", False, False, True, 1),  # Co < co_pad: masked column groups
+    # the AdaIN-block convs (r05: wide where the wide grid has >= two tiles per CU): LeakyReLU prologue, x2 shortcut
+    (64, 200, 1090, 1024, 3, 1, "leaky", True, False, True, 2),   # decoder up-block conv2 form, 9 chunks
+    (64, 400, 1090, 512, 3, 1, "none", False, False, True, 1),    # up-block conv1 after the depthwise ConvT
+    (66, 203, 514, 1024, 3, 1, "leaky", False, False, True, 1),   # encode-block conv1, ragged last tile
 ]
 
 
 @pytest.mark.parametrize("case", WIDE_CASES)
 def test_mrf_wide_bit_identical(eng, case):
     """the wide register-direct form (256 output channels per workgroup, the default for multi-chunk Snake convs whose
-    wide grid has >= 512 workgroups) vs the narrow one (STZS_CONV_MRFV_NARROW: 128 per workgroup): same staged
+    wide grid has >= 512 workgroups, and for the LeakyReLU / identity block convs likewise) vs the narrow one (STZS_CONV_MRFV_NARROW: 128 per workgroup): same staged
     operands, same K order per output -> outputs and fused statistics bit-identical (tolerance 0)."""
     from stzs import _lib as L
     a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_NARROW, ref=False)

@@ -2,7 +2,7 @@
 decoder / predictor block conv shapes at B = 1 (HIP events over REPS launches), with the diagnostic flag bits
 (1: no staging, 2: no K loop, 4: no epilogue) to split the time, and the ring depth from the launcher.
 
-    python tools/blk_probe.py            (env: SPLITK=8, REPS=50, FLAGS="0,1,2,4")
+    python tools/blk_probe.py            (env: SPLITK=8, REPS=50, FLAGS="0,1,2,4", B=1, FRAG32=0)
 """
 import math
 import os
@@ -21,6 +21,8 @@ from stzs.weights import Arena, pack_conv  # noqa: E402
 dev = "cuda:0"
 eng = StyleTTSZS(SPEC_TINY, init_params(SPEC_TINY, 0), device=dev)
 sk = int(os.environ.get("SPLITK", 8))
+B = int(os.environ.get("B", 1))
+frag = os.environ.get("FRAG32", "0") != "0"  # the register-direct form (mrfv) of the throughput engine, no split
 reps = int(os.environ.get("REPS", 50))
 flag_list = [int(f, 0) for f in os.environ.get("FLAGS", "0,1,2,4").split(",")]
 # (T, Ci, Co, name): decoder encode / decode block convs at T40 = 200, predictor F0/N blocks
@@ -32,16 +34,16 @@ for (T, Ci, Co, name) in CASES:
     w = torch.randn(Co, Ci, 3, generator=g) / math.sqrt(Ci * 3)
     b = torch.randn(Co, generator=g) * 0.1
     A = Arena()
-    cw = pack_conv(A, "a", w, b)
+    cw = pack_conv(A, "a", w, b, frag32=frag)
     A.finalize(dev)
     cw.w, cw.b = A[cw.w], A[cw.b]
     Cp = (Ci + 7) // 8 * 8
-    x = Act(torch.randn(1, T, Cp, generator=g).to(torch.bfloat16).to(dev), 0, Ci)
-    ske = min(sk, cw.ci_pad // cw.cic)
-    y = Act(torch.zeros(1, T, Co, dtype=torch.bfloat16, device=dev))
-    mean = (torch.randn(1, Ci, generator=g) * 0.1).to(dev)
-    rstd = (torch.rand(1, Ci, generator=g) + 0.5).to(dev)
-    gb = (torch.randn(1, 2 * Ci, generator=g) * 0.2).to(dev)
+    x = Act(torch.randn(B, T, Cp, generator=g).to(torch.bfloat16).to(dev), 0, Ci)
+    ske = 0 if frag else min(sk, cw.ci_pad // cw.cic)
+    y = Act(torch.zeros(B, T, Co, dtype=torch.bfloat16, device=dev))
+    mean = (torch.randn(B, Ci, generator=g) * 0.1).to(dev)
+    rstd = (torch.rand(B, Ci, generator=g) + 0.5).to(dev)
+    gb = (torch.randn(B, 2 * Ci, generator=g) * 0.2).to(dev)
     line = []
     for fl in flag_list:
         def run():
