@@ -394,7 +394,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
     void (*k)(stzs_conv_args) = nullptr;
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
-    bool blk_wide = false;
+    bool blk_wide = false, blk_t64 = false;
     // the wide form (256 output channels per workgroup) for multi-chunk Snake convs whose wide grid still gives every
     // CU two workgroups (at batch 1 a stage-0 conv has 32 row tiles: the narrow form's 64 workgroups finish sooner),
     // unless STZS_CONV_MRFV_NARROW.  Both forms are bit-identical, so the choice never changes a result.
@@ -422,17 +422,31 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
         // fast (56.4 vs 57.5 us), so it stays there (`tools/blk_probe.py` FRAG32=1).  Bit-identical.
         blk_wide = a.ci_pad > 128 && a.co_pad % (2 * BCO) == 0 && wide_tiles >= 2 * stzs_cu_count() &&
                    !(a.flags & STZS_CONV_MRFV_NARROW);
+        // 64-row tiles for the narrow block convs below 4 128-row tiles per CU (a decoder conv at 32 utterances: 512
+        // tiles; 57.1 -> 55.2 us, the predictor's 256-channel convs 24.4 -> 21.8): more, shorter workgroups per CU
+        // hide more of each input chunk's staging latency.  Bit-identical; STZS_MRFV_T64_BLK=N sets the threshold
+        // (0: off), STZS_CONV_MRFV_T128 keeps 128 rows.
+        static const int t64_blk = [] {
+            const char* e = getenv("STZS_MRFV_T64_BLK");
+            return e ? atoi(e) : 4;
+        }();
+        blk_t64 = !blk_wide && t64_blk > 0 && tiles128 < t64_blk * stzs_cu_count() && !(a.flags & STZS_CONV_MRFV_T128);
         if (a.pro_act == STZS_ACT_LEAKY)
             k = blk_wide ? (R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true, 2> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true, 2>)
+              : blk_t64 ? (R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true, 1, 64> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true, 1, 64>)
                          : (R ? mrfv_conv<STZS_ACT_LEAKY, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_LEAKY, false, false, 3, 0, true>);
         else if (a.pro_act == STZS_ACT_NONE)
             k = blk_wide ? (R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0, true, 2> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0, true, 2>)
+              : blk_t64 ? (R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0, true, 1, 64> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0, true, 1, 64>)
                          : (R ? mrfv_conv<STZS_ACT_NONE, true, false, 3, 0, true> : mrfv_conv<STZS_ACT_NONE, false, false, 3, 0, true>);
     }
     if (!k) return STZS_ESHAPE;
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / (wide || blk_wide ? 2 * BCO : BCO));
-    hipLaunchKernelGGL(k, grid, dim3(NTH), lds, s, a);
+    const int BTk = (t64 || blk_t64) ? 64 : 128;
+    const size_t ldsk = ((((size_t)BTk + (a.ks - 1) * a.dil) * P + 15) & ~(size_t)15) + CS_BYTES;
+    (void)lds;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsk);
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BTk - 1) / BTk), a.co_pad / (wide || blk_wide ? 2 * BCO : BCO));
+    hipLaunchKernelGGL(k, grid, dim3(NTH), ldsk, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

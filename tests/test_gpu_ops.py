@@ -415,13 +415,16 @@ T64_CASES = [
     (1, 24001, 128, 128, 11, 5, "snake", True, True, False, 1),   # stage-1 last c2: residual + accumulate, dil 5 halo
     (1, 3001, 256, 256, 7, 3, "snake", True, False, True, 1),     # stage 0 (2 chunks), ragged: 3001 % 64 = 57
     (2, 4033, 384, 176, 11, 5, "snake", True, True, True, 1),     # 3 chunks, Co < co_pad, a 1-row last tile
+    # the narrow AdaIN-block convs below 4 128-row tiles per CU (r05): LeakyReLU + x2 shortcut, identity prologue
+    (8, 200, 1090, 1024, 3, 1, "leaky", True, False, True, 2),
+    (6, 401, 512, 256, 3, 1, "none", False, False, True, 1),
 ]
 
 
 @pytest.mark.parametrize("case", T64_CASES)
 def test_mrf_t64_bit_identical(eng, case):
     """the 64-row-tile register-direct form (the launcher's choice when the 128-row grid has fewer than 2 workgroups per
-    CU) vs the 128-row tiles (STZS_CONV_MRFV_T128): same staged operands, same K order per output, same 64-row
+    CU, or fewer than 4 for the LeakyReLU / identity block convs) vs the 128-row tiles (STZS_CONV_MRFV_T128): same staged operands, same K order per output, same 64-row
     statistics chunks -> outputs and fused statistics bit-identical (tolerance 0)."""
     from stzs import _lib as L
     a, sa, _ = _run_mrf(eng, case, "frag32", flags=L.CONV_MRFV_T128, ref=False)
