@@ -112,6 +112,34 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
     constexpr int PD = WPW == 2 ? 1 : STZS_MRFV_PD;
     bf16x8 wf[PD + 1][NA];
     bf16x8 xf[MT];
+    // PF (r05, the multi-chunk LeakyReLU / identity block convs): the NEXT input chunk's raw rows and AdaIN
+    // constants are loaded into registers right after this chunk's staging, so they fly under this chunk's K loop
+    // instead of being waited for at the next chunk's start (9 chunks per decoder conv: one staging latency each).
+    // Same values staged, same K order: bit-identical to the in-place loads.
+    constexpr bool PF = NCH == 0 && WPW == 1 && PACT != STZS_ACT_SNAKE;
+    uint4 rawn[PF ? SB : 1];
+    float pmu = 0.f, prs = 0.f, pgm = 0.f, pbe = 0.f;
+    auto prefetch = [&](int cn) {  // chunk cn's rows (clamped addresses: the interior tiles' addresses unchanged)
+        const int c = cn * 128 + cv * 8;
+        const int cl = c < a.Ci ? c : 0;
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+            int tin = t0 - a.pad + rsub + 16 * i;
+            tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+            rawn[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(X) + (unsigned)(tin * (int)a.ldx + cl) * 2u);
+        }
+        if (tid < 128 && a.pro_mode == STZS_PRO_ADAIN) {
+            const int ch = cn * 128 + tid;
+            const int chl = ch < a.Ci ? ch : 0;
+            pmu = a.pro_mean[(long)bq * a.stat_bs + chl];
+            prs = a.pro_rstd[(long)bq * a.stat_bs + chl];
+            pgm = a.pro_gb[(long)bq * a.gb_bs + chl];
+            pbe = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + chl];
+        }
+    };
+    if constexpr (PF) {
+        if (!(a.flags & 1)) prefetch(0);
+    }
 
     for (int cc = 0; cc < nchunk; ++cc) {
         const int kb = cc * NKC;
@@ -133,10 +161,10 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 const bool ok = ch < a.Ci;
                 float sc = 0.f, sh = 0.f;
                 if (ok && a.pro_mode == STZS_PRO_ADAIN) {
-                    const float mu = a.pro_mean[(long)bq * a.stat_bs + ch];
-                    const float rs = a.pro_rstd[(long)bq * a.stat_bs + ch];
-                    const float gm = a.pro_gb[(long)bq * a.gb_bs + ch];
-                    const float be = a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + ch];
+                    const float mu = PF ? pmu : a.pro_mean[(long)bq * a.stat_bs + ch];
+                    const float rs = PF ? prs : a.pro_rstd[(long)bq * a.stat_bs + ch];
+                    const float gm = PF ? pgm : a.pro_gb[(long)bq * a.gb_bs + ch];
+                    const float be = PF ? pbe : a.pro_gb[(long)bq * a.gb_bs + a.gb_beta_off + ch];
                     sc = (1.f + gm) * rs;
                     sh = be - mu * sc;
                 } else if (ok) {
@@ -164,10 +192,14 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 uint4 raw[SB];
 #pragma unroll
                 for (int i = 0; i < SB; ++i) {  // 32-bit offsets from the utterance base (SGPR): saddr loads
-                    int tin = t0 - a.pad + rsub + 16 * i;
-                    if constexpr (!FULL) tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
-                    const unsigned off = (unsigned)(tin * (int)a.ldx + cl) * 2u;
-                    raw[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(X) + off);
+                    if constexpr (PF) {
+                        raw[i] = rawn[i];  // (loaded under the previous chunk's K loop)
+                    } else {
+                        int tin = t0 - a.pad + rsub + 16 * i;
+                        if constexpr (!FULL) tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+                        const unsigned off = (unsigned)(tin * (int)a.ldx + cl) * 2u;
+                        raw[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(X) + off);
+                    }
                 }
                 __syncthreads();  // constants visible
                 // pair-major: the constants of one channel pair (10 registers) at a time, each vector's
@@ -221,6 +253,9 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 stage(std::integral_constant<bool, false>{});
         }
         __syncthreads();
+        if constexpr (PF) {
+            if (cc + 1 < nchunk && !(a.flags & 1)) prefetch(cc + 1);  // the next chunk flies under this K loop
+        }
         // K loop: no barrier.  K-step s = tap*4 + kq reads input rows t + tap*dil, channels kq*32 ..
         // FIRST (the first chunk): K-step 0 takes the MFMA's inline-constant 0 as its C operand instead of 64
         // v_mov zeroings of the accumulators (the same sums: 0 + products either way)
