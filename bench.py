@@ -285,11 +285,11 @@ def stage_roofline(eng, S, tok_d, ref_d, eps_d, dur_d, seeds, n_frames):
                 stages=out, families=fams, top_tags=top)
 
 
-def precise_mode(S, P, dev, B=64, steps=5, nstream=2):
+def precise_mode(S, P, dev, B=64, steps=5, nstream=2, stagger=1):
     """throughput of the PRECISE mode -- the whole pipeline (text encoder, style diffusion, predictor, decoder) on
     fp32 activations and split-operand bf16x3 products, the mode that meets the north-star log-mel L1 <= 1e-3
     END TO END (tests/test_gpu_precise.py: 4.2e-4 at configs[1]) -- on the throughput workload (batch 64, 5-s
-    targets, 2-step CFG 5): replayed as the main leg is, two shards on two streams (shard_runner), and as one graph
+    targets, 2-step CFG 5): replayed as the main leg is, `nstream` shards on their own streams (shard_runner), and as one graph
     on one stream beside it."""
     from stzs.engine import StyleTTSZS
     ep = StyleTTSZS(S, P, device=dev, precise=True)
@@ -310,7 +310,7 @@ def precise_mode(S, P, dev, B=64, steps=5, nstream=2):
     torch.cuda.synchronize()
     el1 = (time.perf_counter() - t0) / steps
     del g
-    run_steps, twins, _ = shard_runner(ep, S, dev, tok, ref, eps, dur, seeds, nf, nstream, True, None, host_src, nwav)
+    run_steps, twins, _ = shard_runner(ep, S, dev, tok, ref, eps, dur, seeds, nf, nstream, stagger, None, host_src, nwav)
     run_steps(1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -325,7 +325,7 @@ def precise_mode(S, P, dev, B=64, steps=5, nstream=2):
     torch.cuda.empty_cache()
     return dict(config=f"batch {B}, 5-s targets, 2-step CFG-5, precise mode (fp32 activations, split-operand "
                        f"bf16x3 convs / linears / LSTM / attention in every stage); {nstream} shards on {nstream} "
-                       f"streams as the main leg",
+                       f"streams (stagger {stagger})",
                 audio_s_per_s=round(B * TARGET_S / el, 1), ms_per_step=round(el * 1e3, 2),
                 single_stream_audio_s_per_s=round(B * TARGET_S / el1, 1), lstm_status=lstm_to, stages=st)
 
@@ -334,8 +334,8 @@ def shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstre
                  steps=STEPS_THROUGHPUT, cfg=CFG):
     """the per-GPU batch as `nstream` (near-)equal shards on engine twins (shared weights, own buffers), each captured
     as two graphs -- front (text, prompt, style diffusion, prosody) and back (decoder) -- replayed on its own stream;
-    shard j > 0 starts one front phase behind shard 0 (stagger), so one shard's latency-bound front (LSTM recurrences,
-    small GEMMs) runs beside another's decoder convs.  A step is one front + one back of every shard; steps are not
+    shard j > 0 starts one front phase behind shard 0 (stagger 1) or behind shard j - 1 (stagger 2: the first
+    fronts chain, spreading the shards' phases), so one shard's latency-bound front (LSTM recurrences, small GEMMs) runs beside another's decoder convs.  A step is one front + one back of every shard; steps are not
     joined, the timed region ends with a synchronize after the last one.
     Host-to-host steps (h2h=True): per shard one H2D and one D2H copy stream, ordered by events so the copies overlap
     the shard's other phase -- step i+1's inputs go in once step i's front graph has read them (during its back graph),
@@ -377,6 +377,7 @@ def shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstre
         for st in streams + (h2d_streams + d2h_streams if h2h else []):
             st.wait_stream(cur)
         ev = torch.cuda.Event()
+        evs = [torch.cuda.Event() for _ in range(nstream)]  # stagger 2: shard j waits for shard j - 1's first front
         front_done = [torch.cuda.Event() for _ in range(nstream)]
         back_done = [torch.cuda.Event() for _ in range(nstream)]
         in_ready = [torch.cuda.Event() for _ in range(nstream)]
@@ -393,7 +394,7 @@ def shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstre
                         in_ready[j].record(h2d_streams[j])
                 with torch.cuda.stream(st):
                     if i == 0 and j > 0 and stagger:
-                        st.wait_event(ev)
+                        st.wait_event(evs[j - 1] if stagger == 2 else ev)
                     if h2h:
                         st.wait_event(in_ready[j])
                     ga.replay()
@@ -401,6 +402,8 @@ def shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstre
                         front_done[j].record(st)
                     if i == 0 and j == 0:
                         ev.record(st)
+                    if i == 0:
+                        evs[j].record(st)
                     if h2h and i > 0:
                         st.wait_event(out_done[j])
                     gb.replay()
@@ -428,9 +431,10 @@ def main():
     ap.add_argument("--no-longform", action="store_true")
     ap.add_argument("--no-precise", action="store_true")
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage roofline pass")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=4,
                     help="split the per-GPU batch over this many concurrently replayed graphs (engine twins)")
-    ap.add_argument("--stagger", type=int, default=1, help="start shard j > 0 one front phase late")
+    ap.add_argument("--stagger", type=int, default=2,
+                    help="1: shards j > 0 start one front phase late; 2: shard j starts after shard j - 1's first front")
     ap.add_argument("--branch-streams", type=int, default=0,
                     help="fork the independent branches (text || prompt encoder, F0 || N) onto side streams")
     ap.add_argument("--shared-speaker", action="store_true",
@@ -490,7 +494,7 @@ def main():
     twins = [eng]
     if nstream > 1:
         run_steps, tws, host = shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstream,
-                                            bool(args.stagger), pidx, (tok, ref, eps, dur), out["wav"].shape[1])
+                                            int(args.stagger), pidx, (tok, ref, eps, dur), out["wav"].shape[1])
         twins += tws
     else:
         host = {}
@@ -621,7 +625,7 @@ def main():
         lstm_timeouts += lf.pop("lstm_timeouts")
     pr = None
     if not args.no_precise and world == 1:
-        pr = precise_mode(S, P, dev)
+        pr = precise_mode(S, P, dev)  # 2 shards: 4 measured slower in the fp32-activation mode (r05_j 6 491 vs 7 756)
         lstm_timeouts += int(pr["lstm_status"] != 0)
 
     cpu = None
@@ -649,7 +653,7 @@ def main():
             "config": {"workload": "configs[2]: batch 64/GPU, 5-s targets, 2-step distilled style diffusion, CFG 5",
                        "global_batch": world * B, "seq_len": n_frames, "parallelism": f"dp{world} (utterance shards)",
                        "spec": S.name, "graph": graph is not None, "branch_streams": bool(args.branch_streams), "streams": nstream,
-                       "stagger": bool(args.stagger and nstream > 1), "shared_speaker": bool(args.shared_speaker)},
+                       "stagger": int(args.stagger) if nstream > 1 else 0, "shared_speaker": bool(args.shared_speaker)},
             "audio_s_per_s_per_gpu": round(value / world, 2),
             "latency": lat,
             "roofline": roof,

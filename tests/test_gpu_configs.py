@@ -274,6 +274,32 @@ def test_two_shard_streams_match_eager(v0, c2, branch_streams):
     assert seq_ok and conc_ok and not bad
 
 
+@pytest.mark.parametrize("nstream,stagger", [(2, 1), (4, 2)])
+def test_bench_shard_runner_matches_eager(v0, c2, nstream, stagger):
+    """bench.shard_runner itself, as the headline line runs it: the configs[2] batch split over `nstream` twins on
+    their own streams (stagger 1: shards j > 0 one front phase late; 2: shard j starts after shard j - 1's first
+    front), steps not joined, host-to-host copies on their own streams -> every waveform the same bits as the eager
+    single-stream batch, after device-resident steps and after host-to-host steps."""
+    S, P, eng = v0
+    (tok, ref, eps, dur, seeds), g = c2
+    dev = eng.device
+    tok_d, ref_d, eps_d, dur_d = (t.to(dev) for t in (tok, ref, eps, dur))
+    run_steps, tws, host = bench.shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, int(dur[0].sum()),
+                                              nstream, stagger, None, (tok, ref, eps, dur), g["wav"].shape[1])
+    run_steps(3)
+    run_steps(1, h2h=True)  # the last device step's waveform, then 3 host-to-host steps into host["wav"]
+    torch.cuda.synchronize()
+    ok1 = torch.equal(host["wav"], g["wav"])
+    host["wav"].zero_()
+    run_steps(3, h2h=True)
+    torch.cuda.synchronize()
+    ok3 = torch.equal(host["wav"], g["wav"])
+    st = [tw.check_status() for tw in tws]
+    print(f"{nstream} shards, stagger {stagger}: h2h x1 {ok1}, h2h x3 {ok3}, max |dwav| "
+          f"{(host['wav'] - g['wav']).abs().max().item():.3e}, status {st}")
+    assert ok1 and ok3
+
+
 def test_latency_engine_batch_invariant(v0):
     """the latency engine (whole-chip small-M denoiser linears, split-K) keeps utterances independent: three
     utterances synthesized as one batch == each synthesized alone, bit for bit (the K structure of every linear is a
