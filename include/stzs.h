@@ -311,6 +311,13 @@ typedef struct stzs_lstm_args {
 #define STZS_STATUS_LSTM_TIMEOUT 1u
 size_t stzs_lstm_workspace(int B, int H, int ndir);
 int stzs_lstm(const stzs_lstm_args* a, void* stream);
+/* two INDEPENDENT recurrences in one launch (side by side on the chip, whatever a graph runtime does with
+ * concurrent branches): same B, H, ndir and precise (one kernel shape), each with its own gx / weights / T / y and
+ * its OWN xchg workspace and sync block (a->xchg != b->xchg, a->sync != b->sync, else STZS_EINVAL); each output is
+ * the same bits as its own stzs_lstm call.  STZS_ESHAPE when the shapes differ or the two grids would exceed one
+ * workgroup per CU.  (Replaces two back-to-back stzs_lstm calls -- the duration LSTM and the shared F0/N LSTM
+ * of ProsodyPredictor when the durations are given) */
+int stzs_lstm_pair(const stzs_lstm_args* a, const stzs_lstm_args* b, void* stream);
 /* zero an LSTM's exchange state -- the 4096-B `sync` block and the granule region at the start of `xchg` (may be
  * NULL) -- with a tiny kernel of agent-scope atomic stores (graph-replay coherent, unlike a memset node).  For
  * callers that keep that state in scratch memory shared with other work (the generic stzs_bilstm does this

@@ -74,8 +74,14 @@ STZS_DEV float acc_sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
 
 // GR: utterances per group (16 / 32 / 64, lstm_group_rows: more workgroups, less MFMA / h-load / cell work per step
 // and group; every row's gate chain and cell update are the same, so the result does not depend on GR)
+// PAIRED launches (stzs_lstm_pair): two independent recurrences of one shape class (same H, group height,
+// directions, mode; own gates, weights, T, outputs and exchange state) share the grid -- z < nz0 is the first,
+// z >= nz0 the second -- so they run side by side whatever the stream / graph runtime does with concurrent branches
 template <int NKS, bool PR, int GR = MROWS>
-__global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
+__global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a0, const stzs_lstm_args a1, const int nz0) {
+    const bool second = (int)blockIdx.z >= nz0;  // uniform per workgroup
+    const stzs_lstm_args& a = second ? a1 : a0;
+    const int nz = second ? (int)gridDim.z - nz0 : nz0;  // this recurrence's groups
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = a.H, G4 = 4 * H;
     const int hp = H + 8;
@@ -86,7 +92,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     const int gp = 4 * UNITS + 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int gate = wave & 3, mh = wave >> 2;  // 8 waves: two per gate, each half of the row tiles
-    const int p = blockIdx.x, dir = blockIdx.y, grp = blockIdx.z;
+    const int p = blockIdx.x, dir = blockIdx.y, grp = (int)blockIdx.z - (second ? nz0 : 0);
     const int P = H / UNITS;
     const int b0 = grp * GR;
     const int nrows = min(GR, a.B - b0);
@@ -319,10 +325,10 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
     __syncthreads();
     if (tid == 0) {
         gu32* done = (gu32*)(a.sync) + 1020;
-        const unsigned nwg = gridDim.x * gridDim.y * gridDim.z;
+        const unsigned nwg = gridDim.x * gridDim.y * nz;  // this recurrence's workgroups (its own done word)
         s_last = 0;
         if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
-            for (unsigned i = 0; i < gridDim.y * gridDim.z; ++i)
+            for (unsigned i = 0; i < gridDim.y * nz; ++i)
                 __hip_atomic_store((gu32*)(a.sync) + i * 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(err, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -330,7 +336,7 @@ __global__ __launch_bounds__(512, 1) void lstm_xchg(const stzs_lstm_args a) {
         }
     }
     __syncthreads();
-    if (s_last && a.B - (int)(gridDim.z - 1) * GR <= TAG_ROWS && !PR) {  // the last group ran tagged: its granules back to zero
+    if (s_last && a.B - (nz - 1) * GR <= TAG_ROWS && !PR) {  // the last group ran tagged: its granules back to zero
         gu64* g0 = (gu64*)(a.xchg);
         for (int e = tid; e < TAG_BYTES / 8; e += 512) __hip_atomic_store(g0 + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -379,31 +385,39 @@ extern "C" size_t stzs_lstm_workspace(int B, int H, int ndir) {
     return (size_t)TAG_BYTES + (size_t)groups * ndir * 2 * lstm_group_rows(B, H, ndir) * 2 * H * sizeof(bf16_t);
 }
 
-extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
+static int lstm_check(const stzs_lstm_args* a) {
     if (!a || !a->gx || !a->whhT || !a->y || !a->xchg || !a->sync) return STZS_EINVAL;
     if (a->B <= 0 || a->T <= 0 || a->H <= 0 || a->H > 256 || a->H % UNITS || (a->ndir != 1 && a->ndir != 2))
         return STZS_ESHAPE;
     if (a->ldg % 8 || a->bsg % 8 || a->ldy % 8 || a->bsy % 8) return STZS_ESHAPE;
     const int gr = lstm_group_rows(a->B, a->H, a->ndir);
     const int groups = (a->B + gr - 1) / gr;
+    if (groups * a->ndir > 63 || (a->H / UNITS) * a->ndir * groups > 256) return STZS_ESHAPE;
+    if (a->precise > 1) return STZS_EINVAL;
+    if (a->precise && (a->ldy % 4 || a->bsy % 4)) return STZS_ESHAPE;
+    return STZS_OK;
+}
+
+// one launch of one recurrence (b == nullptr) or of two of one shape class side by side
+static int lstm_launch(const stzs_lstm_args* a, const stzs_lstm_args* b, void* stream) {
+    const int gr = lstm_group_rows(a->B, a->H, a->ndir);
+    const int groups = (a->B + gr - 1) / gr;
     const int P = a->H / UNITS;
-    if (groups * a->ndir > 63 || P * a->ndir * groups > 256) return STZS_ESHAPE;
+    if (b && P * a->ndir * 2 * groups > 256) return STZS_ESHAPE;  // both grids co-resident, one workgroup per CU
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // the counters start at zero (caller-zeroed once) and every call leaves them zeroed (see the kernel's
     // tail); the caller's status word (a->status) accumulates over calls and is never cleared here
-    if (a->precise > 1) return STZS_EINVAL;
-    if (a->precise && (a->ldy % 4 || a->bsy % 4)) return STZS_ESHAPE;
     const int hp = a->H + 8;
     const int nh = a->precise ? 2 : 1;
     const size_t lds = ((nh * MROWS * hp * 2 + 15) & ~15) + (size_t)MROWS * (4 * UNITS + 4) * 4;
-    dim3 grid(P, a->ndir, groups);
+    dim3 grid(P, a->ndir, b ? 2 * groups : groups);
     switch (a->H / 32) {
 #define STZS_LSTM_CASE(n)                                                                                   \
     case n: {                                                                                               \
         auto k = a->precise ? (gr == 32 ? lstm_xchg<n, true, 32> : gr == 16 ? lstm_xchg<n, true, 16> : lstm_xchg<n, true>) \
                             : (gr == 32 ? lstm_xchg<n, false, 32> : gr == 16 ? lstm_xchg<n, false, 16> : lstm_xchg<n, false>); \
         if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-        hipLaunchKernelGGL(k, grid, dim3(512), lds, s, *a);                                                 \
+        hipLaunchKernelGGL(k, grid, dim3(512), lds, s, *a, b ? *b : *a, groups);                           \
         break;                                                                                              \
     }
         STZS_LSTM_CASE(1)
@@ -415,4 +429,21 @@ extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
     }
     STZS_LAUNCH_CHECK();
     return STZS_OK;
+}
+
+extern "C" int stzs_lstm(const stzs_lstm_args* a, void* stream) {
+    const int rc = lstm_check(a);
+    return rc != STZS_OK ? rc : lstm_launch(a, nullptr, stream);
+}
+
+// two independent recurrences in one launch: same B, H, directions and mode (so one group height and one
+// kernel), each with its own gates / weights / T / outputs and its OWN exchange workspace and sync words
+// (a->xchg != b->xchg, a->sync != b->sync); each result is the same bits as its own stzs_lstm call
+extern "C" int stzs_lstm_pair(const stzs_lstm_args* a, const stzs_lstm_args* b, void* stream) {
+    int rc = lstm_check(a);
+    if (rc == STZS_OK) rc = lstm_check(b);
+    if (rc != STZS_OK) return rc;
+    if (a->B != b->B || a->H != b->H || a->ndir != b->ndir || a->precise != b->precise) return STZS_ESHAPE;
+    if (a->xchg == b->xchg || a->sync == b->sync) return STZS_EINVAL;
+    return lstm_launch(a, b, stream);
 }

@@ -208,7 +208,7 @@ def params(ints=(), floats=()) -> Params:
 EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_conv_splitk_workspace",
            "stzs_conv_rows_workspace",
            "stzs_chan_stats_workspace",
-           "stzs_chan_stats", "stzs_chan_stats_partial", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_ln_linear", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm",
+           "stzs_chan_stats", "stzs_chan_stats_partial", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_ln_linear", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_lstm_pair",
            "stzs_lstm_state_reset", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
@@ -251,6 +251,7 @@ def load():
         "stzs_attention": ([P(AttnArgs), vp], i32),
         "stzs_lstm_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_lstm": ([P(LstmArgs), vp], i32),
+        "stzs_lstm_pair": ([P(LstmArgs), P(LstmArgs), vp], i32),
         "stzs_lstm_state_reset": ([vp, vp, vp], i32),
         "stzs_predictor_prep": ([P(PrPrepArgs), vp], i32),
         "stzs_durations": ([P(DurArgs), vp], i32),

@@ -203,7 +203,7 @@ class _StatPtr:
 class StyleTTSZS:
     def __init__(self, spec: Spec, params, device="cuda:0", fill=True, fp8_denoiser=False, precise_decoder=False,
                  packed: PackedModel = None, branch_streams=False, precise=False, dn_splitk=None, dn_rows=None,
-                 te_splitk=None, blk_splitk=None):
+                 te_splitk=None, blk_splitk=None, dur_overlap=None):
         """packed: an already packed (e.g. RCCL-broadcast, stzs/dist.py) PackedModel on `device`; params unused.
         fp8_denoiser: run the per-layer denoiser linears (qkv, o, q, co, ff1, ff2) on e4m3fn MFMA with
         per-row activation / per-column weight scales (configs[4]); bf16 otherwise.
@@ -216,7 +216,10 @@ class StyleTTSZS:
         front end stays bf16: its output is quantised to discrete codes.
         branch_streams: run the independent branches (text encoder || prompt encoder, F0 || N predictor branches)
         on forked side streams (graph-capturable: the fork/join is stream-ordered); each branch has its own
-        scratch (statistics slab / workspace), results bit-identical to the single-stream order."""
+        scratch (statistics slab / workspace), results bit-identical to the single-stream order.
+        dur_overlap: with durations given, the alignment reads them directly and the duration LSTM runs in ONE
+        launch with the shared F0/N LSTM (stzs_lstm_pair), its projection and durations kernel after the F0/N
+        branches -- bit-identical (default on; env STZS_DUR_OVERLAP=0 turns it off)."""
         self.spec = spec
         self.fp8_denoiser = fp8_denoiser
         precise_decoder = precise_decoder or precise
@@ -246,7 +249,10 @@ class StyleTTSZS:
         self._consts = {}
         self.branch_streams = branch_streams
         self._branch = ""  # scratch-key suffix of the branch being enqueued (see fork())
-        self._side = []
+        self._side = {}  # (fork depth, branch) -> side stream
+        self._depth = 0  # nesting depth of fork() calls being enqueued
+        self.dur_overlap = bool(int(os.environ.get("STZS_DUR_OVERLAP", "1"))) if dur_overlap is None else \
+            bool(dur_overlap)
         self.launches = 0
         self.lstm_spin_limit = 0  # 0 = the library default; tests force tiny values
         # split-K of the bf16 denoiser layer linears (stzs_conv_args.splitk): a property of the weight, used at
@@ -356,20 +362,22 @@ class StyleTTSZS:
         """weight reference -> device tensor (arena name, or an already-resolved tensor)."""
         return x if isinstance(x, torch.Tensor) else self.W.t(x)
 
-    def _call(self, fn, arg, what, cost=None):
-        """one library launch; cost = (algorithmic FLOP, algorithmic bytes) of it, recorded with HIP events when a
-        timer of every launch is running (start_timer("*"), the per-stage roofline of bench.py)."""
+    def _call(self, fn, arg, what, cost=None, b=None):
+        """one library launch (b: a second struct argument, stzs_lstm_pair); cost = (algorithmic FLOP, algorithmic
+        bytes) of it, recorded with HIP events when a timer of every launch is running (start_timer("*"), the
+        per-stage roofline of bench.py)."""
         self.launches += 1
+        args = (C.byref(arg),) if b is None else (C.byref(arg), C.byref(b))
         tm = self.timer
         if tm is not None and tm["all"] and cost is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
-            L.check(fn(C.byref(arg), self.stream()), what)
+            L.check(fn(*args, self.stream()), what)
             e1.record()
             tm["rec"].append((what, e0, e1, float(cost[0]), float(cost[1]), None, self.stage))
             return
-        L.check(fn(C.byref(arg), self.stream()), what)
+        L.check(fn(*args, self.stream()), what)
 
     # ------------------------------------------------------------------ ops
     def conv(self, cw: ConvW, x: Act, y: Act, *, T_out=None, pad=0, dil=1, stride=1, pro=None, pro_act=L.ACT_NONE,
@@ -611,23 +619,29 @@ class StyleTTSZS:
 
     def fork(self, *fns):
         """run fns[0] on the current stream and fns[1:] on side streams forked from it (waits on the current
-        stream, joined back into it before returning); sequential when branch_streams is off.  -> outputs"""
+        stream, joined back into it before returning); sequential when branch_streams is off.
+        Forks nest: a fork inside a branch takes side streams and scratch keys of its own depth, so an inner
+        branch never queues behind (or shares scratch with) an outer one.  -> outputs"""
         if not self.branch_streams or len(fns) < 2:
             return [f() for f in fns]
         cur = torch.cuda.current_stream(self.device)
-        while len(self._side) < len(fns) - 1:
-            self._side.append(torch.cuda.Stream(self.device))
-        side = self._side[:len(fns) - 1]
+        d, outer = self._depth, self._branch
+        side = []
+        for i in range(1, len(fns)):
+            if (d, i) not in self._side:
+                self._side[(d, i)] = torch.cuda.Stream(self.device)
+            side.append(self._side[(d, i)])
         for st in side:
             st.wait_stream(cur)
         outs = []
+        self._depth = d + 1
         try:
             for i, f in enumerate(fns):
-                self._branch = "" if i == 0 else f"@b{i}"
+                self._branch = outer if i == 0 else f"{outer}@b{d}.{i}"
                 with torch.cuda.stream(cur if i == 0 else side[i - 1]):
                     outs.append(f())
         finally:
-            self._branch = ""
+            self._branch, self._depth = outer, d
         for st in side:
             cur.wait_stream(st)
         return outs
@@ -705,6 +719,22 @@ class StyleTTSZS:
                          a.R * (2 * a.Lq + 2 * a.Lk) * a.heads * a.dh * q.t.element_size()))
 
     def lstm(self, lw, x: Act, y: Act, key):
+        a, cost = self._lstm_args(lw, x, y, key)
+        self._call(self.lib.stzs_lstm, a, key + ".rec", cost=cost)  # recurrent products + gate rows in, h rows out
+        return y
+
+    def lstm_pair(self, r0, r1):
+        """two independent recurrences r = (lw, x, y, key) of one shape class in ONE launch (stzs_lstm_pair: side by
+        side on the chip; each output the same bits as its own lstm() call): both input projections, then the
+        paired recurrence on separate exchange state."""
+        a0, c0 = self._lstm_args(*r0)
+        a1, c1 = self._lstm_args(*r1, pair=True)
+        self._call(self.lib.stzs_lstm_pair, a0, r0[3] + ".rec+" + r1[3] + ".rec",
+                   cost=(c0[0] + c1[0], c0[1] + c1[1]), b=a1)
+        return r0[2], r1[2]
+
+    def _lstm_args(self, lw, x: Act, y: Act, key, pair=False):
+        """input projection (one MFMA GEMM over all steps) + the recurrence's arguments -> (LstmArgs, cost)"""
         gx = self.act(key + ".gx", x.B, x.T, 8 * lw.H, torch.float32)
         self.conv(lw.ih, x, gx, what=key + ".ih")
         a = L.LstmArgs()
@@ -713,16 +743,16 @@ class StyleTTSZS:
             assert y.t.dtype == torch.float32
             a.whhT, a.precise = self._t(lw.whx3).data_ptr(), 1
         nx = self.lib.stzs_lstm_workspace(x.B, lw.H, 2)
-        xchg = self.buf("lstm.xchg", (max(nx, 16),), torch.uint8, zero=True)
-        sync = self.buf("lstm.sync", (4096,), torch.uint8, zero=True)
+        sk = self._branch + ("@pair" if pair else "")  # concurrent recurrences (branches, a pair) never share them
+        xchg = self.buf("lstm.xchg" + sk, (max(nx, 16),), torch.uint8, zero=True)
+        sync = self.buf("lstm.sync" + sk, (4096,), torch.uint8, zero=True)
         a.xchg, a.sync = xchg.data_ptr(), sync.data_ptr()
         a.ldg, a.bsg, a.ldy, a.bsy = gx.ld, gx.bs, y.ld, y.bs
         a.B, a.T, a.H, a.ndir = x.B, x.T, lw.H, 2
         a.status, a.spin_limit = self.status.data_ptr(), self.lstm_spin_limit
-        self._call(self.lib.stzs_lstm, a, key + ".rec",  # recurrent products + gate rows in, h rows out, W_hh once
-                   cost=(2.0 * x.B * x.T * 2 * 4 * lw.H * lw.H,
-                         x.B * x.T * (8 * lw.H * 4 + 2 * lw.H * y.t.element_size()) + 2 * 4 * lw.H * lw.H * 2))
-        return y
+        # (flops, bytes): recurrent products; gate rows in, h rows out, W_hh once
+        return a, (2.0 * x.B * x.T * 2 * 4 * lw.H * lw.H,
+                   x.B * x.T * (8 * lw.H * 4 + 2 * lw.H * y.t.element_size()) + 2 * 4 * lw.H * lw.H * 2)
 
     def copy2d(self, x: Act, y: Act, R, Cn, bsx=None):
         a = L.CopyArgs()
@@ -1040,6 +1070,16 @@ class StyleTTSZS:
     def predict_prosody(self, h_txt: Act, codes: torch.Tensor, durations=None, n_frames=None):
         """durations: optional int tensor [B, T_txt] (host or device); n_frames: their per-utterance sum if
         known (avoids the device->host sync, e.g. under graph capture).  Returns dict of device tensors."""
+        if self.dur_overlap and durations is not None and (n_frames is not None or durations.device.type == "cpu"):
+            # the alignment reads the given durations, so the duration LSTM no longer gates the frame branch: it
+            # runs in ONE launch with the shared F0/N LSTM (stzs_lstm_pair), its projection and the durations kernel
+            # after the F0/N branches -- every output the same bits as the sequential order
+            d, ov = self.duration_encoder(h_txt, codes, durations)
+            T40 = int(n_frames) if n_frames is not None else int(durations.to(torch.int64).sum(1)[0])
+            pro = self.prosody_frames(h_txt, codes, d, ov, T40, pair_dur=True)
+            du = self.duration_head(d, ov, hd=pro.pop("_hd"))
+            pro.update(du, dur=du["dur"])
+            return pro
         du = self.predict_durations(h_txt, codes, durations)
         if n_frames is not None:
             T40 = int(n_frames)
@@ -1055,6 +1095,12 @@ class StyleTTSZS:
 
     def predict_durations(self, h_txt: Act, codes: torch.Tensor, durations=None) -> dict:
         """a5-a6: DurationEncoder + duration LSTM + head -> dict(dur int32 [B, T], dsum, logits, d) (device)."""
+        d, ov = self.duration_encoder(h_txt, codes, durations)
+        return self.duration_head(d, ov)
+
+    def duration_encoder(self, h_txt: Act, codes: torch.Tensor, durations=None):
+        """a5: DurationEncoder (LSTM + AdaLN layers) -> (d [B, T, pr_in], the given durations as the int32
+        device buffer pr.dur_ov, or None)."""
         S, W = self.spec, self.W
         B, T = h_txt.B, h_txt.T
         pin = S.pr_in
@@ -1074,13 +1120,6 @@ class StyleTTSZS:
             self.conv(W.pr_aln[i], xin.sl(S.d_txt, S.style_pr), gb, what=f"pr.aln{i}")
             self.rowln(hout, Act(xin.t, 0, S.pr_hid), G=gb.ptr, gs=2 * S.pr_hid, Bt=gb.ptr + S.pr_hid * 4,
                        bs=2 * S.pr_hid, gdiv=1, gadd=1.0, what=f"pr.adaln{i}")
-        d = xin
-        hd = self.act("pr.hd", B, T, S.pr_hid, self.adt)
-        self.lstm(W.pr_dur_lstm, d, hd, "pr.dur_lstm")
-        logits = self.act("pr.logits", B, T, S.dur_bins, torch.float32)
-        self.conv(W.pr_dur_proj, hd, Act(logits.t, 0, S.dur_bins), what="pr.dur_proj")
-        dur = self.buf("pr.dur", (B, T), torch.int32)
-        dsum = self.buf("pr.dsum", (B, T), torch.float32)
         ov = None
         if durations is not None:
             ov = self.buf("pr.dur_ov", (B, T), torch.int32)
@@ -1088,6 +1127,21 @@ class StyleTTSZS:
                 ov.copy_(durations.to(torch.int32))
             elif durations.data_ptr() != ov.data_ptr():
                 ov.copy_(durations)
+        return xin, ov
+
+    def duration_head(self, d: Act, ov=None, hd: Act = None) -> dict:
+        """a6: duration LSTM + projection + durations kernel (sum of the bin sigmoids, rounded, >= 1; the given
+        durations `ov` override it); hd: the duration LSTM's output when already run (lstm_pair)
+        -> dict(dur int32 [B, T], dsum, logits, d)."""
+        S, W = self.spec, self.W
+        B, T = d.B, d.T
+        if hd is None:
+            hd = self.act("pr.hd", B, T, S.pr_hid, self.adt)
+            self.lstm(W.pr_dur_lstm, d, hd, "pr.dur_lstm")
+        logits = self.act("pr.logits", B, T, S.dur_bins, torch.float32)
+        self.conv(W.pr_dur_proj, hd, Act(logits.t, 0, S.dur_bins), what="pr.dur_proj")
+        dur = self.buf("pr.dur", (B, T), torch.int32)
+        dsum = self.buf("pr.dsum", (B, T), torch.float32)
         a = L.DurArgs()
         a.logits, a.override_dur, a.dur, a.dsum = logits.ptr, (ov.data_ptr() if ov is not None else None), \
             dur.data_ptr(), dsum.data_ptr()
@@ -1096,8 +1150,9 @@ class StyleTTSZS:
         return dict(dur=dur, dsum=dsum, logits=logits, d=d)
 
     def prosody_frames(self, h_txt: Act, codes: torch.Tensor, d: Act, dur: torch.Tensor, T40: int,
-                       extra: dict = None) -> dict:
-        """a7-a8 for a batch sharing T40 aligned frames: alignment, gathers, shared LSTM, F0 / N curves."""
+                       extra: dict = None, pair_dur=False) -> dict:
+        """a7-a8 for a batch sharing T40 aligned frames: alignment, gathers, shared LSTM, F0 / N curves.
+        pair_dur: the duration LSTM over d runs in the shared LSTM's launch (its output as "_hd")."""
         S, W = self.spec, self.W
         B, T = h_txt.B, h_txt.T
         pin = S.pr_in
@@ -1115,17 +1170,23 @@ class StyleTTSZS:
             self.copy2d(e16, enc_in, T40, S.d_txt)
         else:
             self.gather(h_txt, idx, enc_in, S.d_txt)
-        F0, Nn = self.f0n_predictor(en, codes)
+        hd = self.act("pr.hd", B, T, S.pr_hid, self.adt) if pair_dur else None
+        F0, Nn = self.f0n_predictor(en, codes, dur_rec=(W.pr_dur_lstm, d, hd, "pr.dur_lstm") if pair_dur else None)
         out = dict(extra or {}, dur=dur, idx=idx, T40=T40, en=en, asr_buf=enc_in, d=d, F0=F0, N=Nn)
+        if pair_dur:
+            out["_hd"] = hd
         return out
 
-    def f0n_predictor(self, en: Act, codes: torch.Tensor):
+    def f0n_predictor(self, en: Act, codes: torch.Tensor, dur_rec=None):
         """a8: shared BiLSTM over the aligned frames, then per branch (F0, N) three AdaIN residual blocks (the
         middle one x2 upsampling) and a 1x1 projection.  en [B, T40, pr_in] bf16 -> F0, N fp32 [B, 2 T40]."""
         S, W = self.spec, self.W
         B, T40 = en.B, en.T
         xs = self.act("pr.xs", B, T40, S.pr_hid, self.adt)
-        self.lstm(W.pr_shared, en, xs, "pr.shared")
+        if dur_rec is None:
+            self.lstm(W.pr_shared, en, xs, "pr.shared")
+        else:  # dur_rec = (lw, x, y, key): the duration LSTM beside it, one launch
+            self.lstm_pair((W.pr_shared, en, xs, "pr.shared"), dur_rec)
         sg = self.mean_rows(codes, S.style_ac, S.style_pr, "pr.sg")
         ng = W.pr_norm
         gbp = self.buf("pr.gbn", (B, ng.total), torch.float32)
@@ -1555,7 +1616,8 @@ class StyleTTSZS:
         latency-bound phases -- LSTM recurrences, statistics, small GEMMs -- overlap the other's convs)."""
         t = object.__new__(StyleTTSZS)
         t.__dict__.update(self.__dict__)
-        t._bufs, t._retired, t._consts, t._side, t._branch, t.launches, t.timer = {}, [], {}, [], "", 0, None
+        t._bufs, t._retired, t._consts, t._side, t._branch, t.launches, t.timer = {}, [], {}, {}, "", 0, None
+        t._depth = 0
         t.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         return t
 
@@ -1657,7 +1719,8 @@ class StyleTTSZS:
 def latency_engine(spec: Spec, packed: PackedModel, device="cuda:0") -> "StyleTTSZS":
     """the batch-1 serving engine bench.py times for the configs[1] p50 (and tests/test_gpu_configs.py checks against
     the oracle): the same packed weights, the denoiser layer linears on the whole-chip small-M form
-    (LATENCY_DN_ROWS, csrc/rows.hip) and split-K ffn2 wherever the rows form does not apply (LATENCY_DN_SPLITK)."""
+    (LATENCY_DN_ROWS, csrc/rows.hip) and split-K ffn2 wherever the rows form does not apply (LATENCY_DN_SPLITK);
+    with durations given, the duration LSTM paired with the shared LSTM (dur_overlap, on in every engine)."""
     return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS,
                       te_splitk=LATENCY_TE_SPLITK, blk_splitk=LATENCY_BLK_SPLITK)
 

@@ -166,6 +166,34 @@ def test_entry_points_reject_before_launch(name, struct, extra):
     assert fn(C.byref(a), *extra, None) == _lib.ESHAPE  # sizes all 0: rejected, nothing dereferenced
 
 
+def test_lstm_pair_rejects_before_launch():
+    """stzs_lstm_pair: each recurrence validated as stzs_lstm validates it, then the pair -- one shape class (B, H,
+    ndir, precise) and separate exchange state -- all before any HIP call."""
+    from stzs import _lib
+    L = _lib.load()
+    E, S = _lib.EINVAL, _lib.ESHAPE
+
+    def ok_args(base):
+        a = _lib.LstmArgs()
+        a.gx, a.whhT, a.y, a.xchg, a.sync = base, base + 0x100, base + 0x200, base + 0x300, base + 0x400
+        a.ldg, a.bsg, a.ldy, a.bsy, a.B, a.T, a.H, a.ndir = 1024, 8192, 256, 2048, 1, 8, 128, 2
+        return a
+    a, b = ok_args(0x10000), ok_args(0x20000)
+    assert L.stzs_lstm_pair(None, C.byref(b), None) == E and L.stzs_lstm_pair(C.byref(a), None, None) == E
+    b.H = 64
+    assert L.stzs_lstm_pair(C.byref(a), C.byref(b), None) == S  # shape classes differ
+    b.H, b.B = 128, 2
+    assert L.stzs_lstm_pair(C.byref(a), C.byref(b), None) == S
+    b.B, b.precise = 1, 1
+    assert L.stzs_lstm_pair(C.byref(a), C.byref(b), None) == S
+    b.precise, b.xchg = 0, a.xchg
+    assert L.stzs_lstm_pair(C.byref(a), C.byref(b), None) == E  # shared exchange workspace
+    b.xchg, b.sync = 0x20300, a.sync
+    assert L.stzs_lstm_pair(C.byref(a), C.byref(b), None) == E  # shared sync words
+    b.sync, b.T = 0x20400, 0
+    assert L.stzs_lstm_pair(C.byref(a), C.byref(b), None) == S  # the second recurrence's own checks
+
+
 def test_scalar_entry_points_reject_before_launch():
     from stzs import _lib
     L = _lib.load()

@@ -338,3 +338,41 @@ def test_latency_engine_deferred_stats_bit_identical(v0):
         assert torch.equal(outs[True][k], outs[False][k]), k
     print("launches deferred / finalised", launches[True], launches[False])
     assert launches[True] < launches[False]
+
+
+@pytest.mark.parametrize("branch_streams", [False, True])
+def test_dur_overlap_bit_identical(v0, branch_streams):
+    """with durations given, the alignment reads them directly and the duration LSTM runs in ONE launch with the
+    shared F0/N LSTM (engine.dur_overlap -> stzs_lstm_pair, each recurrence on its own exchange slab and counters),
+    its projection and durations kernel after the F0/N branches: eager and graph-replayed synthesis must be the
+    same bits as the sequential order, the predicted logits / dsum included; branch_streams adds the F0 || N fork
+    (nested forks take side streams and scratch of their own depth)."""
+    from stzs.engine import latency_engine
+    S, P, eng = v0
+    e = latency_engine(S, eng.W, eng.device)
+    assert e.dur_overlap
+    e.branch_streams = branch_streams
+    tok, ref, eps, dur, seeds = bench.rank_inputs(S, 2, 11)
+    nf = int(dur[0].sum())
+    dev = e.device
+    tok_d, ref_d, eps_d, dur_d = (t.to(dev) for t in (tok, ref, eps, dur))
+    keys = ("codes", "F0", "N", "wav", "dur", "dsum", "logits")
+    host = lambda v: (v if torch.is_tensor(v) else v.t).detach().clone().cpu()  # logits is an Act
+
+    def fn():
+        return e.synth(tok_d, ref_d, steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG, noise=eps_d, durations=dur_d,
+                       seeds=seeds, n_frames=nf, check=False)
+    outs = {}
+    for ov in (False, True):
+        e.dur_overlap = ov
+        o = fn()
+        outs[ov] = {k: host(o[k]) for k in keys}
+    for k in keys:
+        assert torch.equal(outs[True][k], outs[False][k]), k
+    g, o = e.capture(fn)
+    for rep in range(4):
+        g.replay()
+        torch.cuda.synchronize()
+        for k in keys:
+            assert torch.equal(host(o[k]), outs[False][k]), (rep, k)
+    e.check_status()

@@ -567,6 +567,29 @@ def test_lstm_group_rows_invariant(eng):
     assert torch.equal(outs[64][:1], outs[1])
 
 
+@pytest.mark.parametrize("B", [1, 2, 16, 64, 65])
+def test_lstm_pair_bit_identical(eng, B):
+    """stzs_lstm_pair (engine.lstm_pair): two independent recurrences of different lengths in one launch -- the first
+    over T = 60, the second over T = 23 -- each the same bits as its own stzs_lstm call (tagged granules at B = 1 / 2,
+    16-row counter groups above), run twice (each pair leaves its own exchange state zeroed)."""
+    from stzs.engine import Act
+    _P, lw, _A = _v0_lstm()
+    g = torch.Generator().manual_seed(500 + B)
+    xa = Act(torch.randn(B, 60, 640, generator=g).to(torch.bfloat16).cuda())
+    xb = Act(torch.randn(B, 23, 640, generator=g).to(torch.bfloat16).cuda())
+    ya, yb = (Act(torch.zeros(B, t, 512, dtype=torch.bfloat16, device="cuda:0")) for t in (60, 23))
+    eng.lstm(lw, xa, ya, "t.pa")
+    eng.lstm(lw, xb, yb, "t.pb")
+    assert eng.check_status() == 0
+    ra, rb = ya.t.clone(), yb.t.clone()
+    for _ in range(2):
+        ya.t.zero_()
+        yb.t.zero_()
+        eng.lstm_pair((lw, xa, ya, "t.pa"), (lw, xb, yb, "t.pb"))
+        assert eng.check_status() == 0
+        assert torch.equal(ya.t, ra) and torch.equal(yb.t, rb)
+
+
 def test_lstm_timeout_tagged_never_hangs(eng):
     """B = 1 (tagged-granule sweep) under a 1-poll spin limit: the tagged hand-off seldom waits past two polls, so
     a timeout cannot be forced deterministically; every run must either report STZS_STATUS_LSTM_TIMEOUT (and then

@@ -34,4 +34,4 @@ for _ in range(n):
     torch.cuda.synchronize()
     ts.append((time.perf_counter() - t0) * 1e3)
 ts.sort()
-print(f"STZS_DN_SPLITK={sk} STZS_DN_ROWS={rw} STZS_TE_SPLITK={te} STZS_BLK_SPLITK={bk} branch_streams={int(eng.branch_streams)} latency p50 {ts[len(ts) // 2]:.3f} ms  min {ts[0]:.3f}  launches/synth {eng.launches // 2}")
+print(f"STZS_DN_SPLITK={sk} STZS_DN_ROWS={rw} STZS_TE_SPLITK={te} STZS_BLK_SPLITK={bk} branch_streams={int(eng.branch_streams)} dur_overlap={int(eng.dur_overlap)} latency p50 {ts[len(ts) // 2]:.3f} ms  min {ts[0]:.3f}  launches/synth {eng.launches // 2}")
