@@ -616,7 +616,7 @@ def main():
                           "(p50_device_resident_ms: the replay alone, inputs already in HBM)",
                    config="batch 1, 10-step sampling, CFG 5, 5-s target, 3-s reference",
                    dn_splitk=dict(LATENCY_DN_SPLITK), dn_rows=dict(LATENCY_DN_ROWS),
-                   te_splitk=LATENCY_TE_SPLITK)
+                   te_splitk=LATENCY_TE_SPLITK, forks=sorted(elat.branch_streams))
 
     # ---- configs[4]: 30-s target, batch 1, fp8 denoiser linears, streaming iSTFT (1-s chunks) ----
     lf = None

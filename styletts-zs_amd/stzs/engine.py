@@ -617,12 +617,15 @@ class StyleTTSZS:
     def _slab(self, n):
         return self._scratch("stat_slab", n)
 
-    def fork(self, *fns):
+    def fork(self, site, *fns):
         """run fns[0] on the current stream and fns[1:] on side streams forked from it (waits on the current
-        stream, joined back into it before returning); sequential when branch_streams is off.
+        stream, joined back into it before returning); sequential unless branch_streams is on (True, or a set of
+        fork sites holding `site`: "enc" = text || prompt encoder, "f0n" = F0 || N predictor branches).
         Forks nest: a fork inside a branch takes side streams and scratch keys of its own depth, so an inner
         branch never queues behind (or shares scratch with) an outer one.  -> outputs"""
-        if not self.branch_streams or len(fns) < 2:
+        on = self.branch_streams is True or (isinstance(self.branch_streams, (set, frozenset)) and
+                                             site in self.branch_streams)
+        if not on or len(fns) < 2:
             return [f() for f in fns]
         cur = torch.cuda.current_stream(self.device)
         d, outer = self._depth, self._branch
@@ -1204,7 +1207,7 @@ class StyleTTSZS:
             self.blk(W.pr_blk[f"pr.{br}1"], y0, y1, ng, gbp, f"pr.{br}1", self.adt)
             self.blk(W.pr_blk[f"pr.{br}2"], y1, y2, ng, gbp, f"pr.{br}2", self.adt)
             self.conv(W.pr_blk[f"pr.{br}_proj"], y2, Act(out, 0, 1), what=f"pr.{br}_proj")
-        self.fork(lambda: branch("f0", F0), lambda: branch("n", Nn))
+        self.fork("f0n", lambda: branch("f0", F0), lambda: branch("n", Nn))
         return F0[:, :, 0], Nn[:, :, 0]
 
     def gather(self, x: Act, idx, y: Act, Cn):
@@ -1624,7 +1627,7 @@ class StyleTTSZS:
     def encode_inputs(self, tokens, ref_wav, prompt_idx=None):
         """text encoder || prompt encoder (independent; forked when branch_streams) -> (h_txt, prompt codes)."""
         ref = None if ref_wav is None else ref_wav.to(self.device)
-        return self.fork(lambda: self.text_encode(tokens), lambda: self.prompt_encode(ref, prompt_idx))
+        return self.fork("enc", lambda: self.text_encode(tokens), lambda: self.prompt_encode(ref, prompt_idx))
 
     def capture(self, fn):
         """Capture `fn()` into one HIP graph.  fn must be replay-safe: device-resident inputs, cached
@@ -1716,13 +1719,20 @@ class StyleTTSZS:
             self.check_status()
 
 
+# fork sites of the batch-1 latency engine: the text encoder beside the prompt encoder on a forked branch of the
+# captured graph (configs[1] p50 6.06-6.20 -> 5.91 ms, 4 A/B pairs, profiles/r05_m_fork_sites_ab.log); the F0 || N
+# fork measured slower (6.19-6.27 vs 6.05-6.18) and stays off.  env STZS_LATENCY_FORKS="" turns it off.
+LATENCY_FORKS = frozenset(v for v in os.environ.get("STZS_LATENCY_FORKS", "enc").split(",") if v)
+
+
 def latency_engine(spec: Spec, packed: PackedModel, device="cuda:0") -> "StyleTTSZS":
     """the batch-1 serving engine bench.py times for the configs[1] p50 (and tests/test_gpu_configs.py checks against
     the oracle): the same packed weights, the denoiser layer linears on the whole-chip small-M form
     (LATENCY_DN_ROWS, csrc/rows.hip) and split-K ffn2 wherever the rows form does not apply (LATENCY_DN_SPLITK);
-    with durations given, the duration LSTM paired with the shared LSTM (dur_overlap, on in every engine)."""
+    with durations given, the duration LSTM paired with the shared LSTM (dur_overlap, on in every engine); the text
+    and prompt encoders on forked graph branches (LATENCY_FORKS)."""
     return StyleTTSZS(spec, None, device=device, packed=packed, dn_splitk=LATENCY_DN_SPLITK, dn_rows=LATENCY_DN_ROWS,
-                      te_splitk=LATENCY_TE_SPLITK, blk_splitk=LATENCY_BLK_SPLITK)
+                      te_splitk=LATENCY_TE_SPLITK, blk_splitk=LATENCY_BLK_SPLITK, branch_streams=LATENCY_FORKS)
 
 
 class CheckedGraph:

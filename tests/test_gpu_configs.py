@@ -376,3 +376,36 @@ def test_dur_overlap_bit_identical(v0, branch_streams):
         for k in keys:
             assert torch.equal(host(o[k]), outs[False][k]), (rep, k)
     e.check_status()
+
+
+def test_latency_engine_enc_fork_bit_identical(v0):
+    """the latency engine forks the text encoder and the prompt encoder onto two branches of its captured graph
+    (stzs.engine.LATENCY_FORKS = {"enc"}: each branch on its own scratch): eager and graph-replayed synthesis must be
+    the same bits as the unforked order."""
+    from stzs.engine import latency_engine
+    S, P, eng = v0
+    e = latency_engine(S, eng.W, eng.device)
+    assert "enc" in e.branch_streams
+    tok, ref, eps, dur, seeds = bench.rank_inputs(S, 1, 13)
+    nf = int(dur[0].sum())
+    tok_d, ref_d, eps_d, dur_d = (t.to(e.device) for t in (tok, ref, eps, dur))
+    keys = ("prompt_idx", "codes", "F0", "N", "wav")
+
+    def fn():
+        return e.synth(tok_d, ref_d, steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG, noise=eps_d, durations=dur_d,
+                       seeds=seeds, n_frames=nf, check=False)
+    forks = e.branch_streams
+    e.branch_streams = False
+    o = fn()
+    ref_out = {k: o[k].detach().clone().cpu() for k in keys}
+    e.branch_streams = forks
+    o = fn()
+    for k in keys:
+        assert torch.equal(o[k].cpu(), ref_out[k]), k
+    g, o = e.capture(fn)
+    for rep in range(4):
+        g.replay()
+        torch.cuda.synchronize()
+        for k in keys:
+            assert torch.equal(o[k].cpu(), ref_out[k]), (rep, k)
+    e.check_status()

@@ -19,7 +19,8 @@ bk = os.environ.get("STZS_BLK_SPLITK")  # AdaIN-block conv split-K slices; unset
 eng = StyleTTSZS(S, init_params(S, 0), device="cuda:0", dn_splitk=None if sk is not None else LATENCY_DN_SPLITK,
                  dn_rows=None if rw is not None else LATENCY_DN_ROWS, te_splitk=None if te is not None else LATENCY_TE_SPLITK,
                  blk_splitk=None if bk is not None else LATENCY_BLK_SPLITK,
-                 branch_streams=os.environ.get("STZS_BRANCH_STREAMS", "0") != "0")  # text || prompt, F0 || N forked
+                 branch_streams=(lambda v: v != "0" if v in ("0", "1") else set(v.split(",")))(
+                     os.environ.get("STZS_BRANCH_STREAMS", "0")))  # "1": text || prompt and F0 || N forked; "f0n" / "enc"
 tok, ref, eps, dur = (t.cuda() for t in make_inputs(S, 1, 1000))
 nf = int(dur[0].sum())
 one = lambda: eng.synth(tok, ref, steps=STEPS_LATENCY, cfg_scale=CFG, noise=eps, durations=dur, seeds=[7], n_frames=nf)
@@ -34,4 +35,4 @@ for _ in range(n):
     torch.cuda.synchronize()
     ts.append((time.perf_counter() - t0) * 1e3)
 ts.sort()
-print(f"STZS_DN_SPLITK={sk} STZS_DN_ROWS={rw} STZS_TE_SPLITK={te} STZS_BLK_SPLITK={bk} branch_streams={int(eng.branch_streams)} dur_overlap={int(eng.dur_overlap)} latency p50 {ts[len(ts) // 2]:.3f} ms  min {ts[0]:.3f}  launches/synth {eng.launches // 2}")
+print(f"STZS_DN_SPLITK={sk} STZS_DN_ROWS={rw} STZS_TE_SPLITK={te} STZS_BLK_SPLITK={bk} branch_streams={eng.branch_streams} dur_overlap={int(eng.dur_overlap)} latency p50 {ts[len(ts) // 2]:.3f} ms  min {ts[0]:.3f}  launches/synth {eng.launches // 2}")
