@@ -435,8 +435,9 @@ def main():
                     help="split the per-GPU batch over this many concurrently replayed graphs (engine twins)")
     ap.add_argument("--stagger", type=int, default=2,
                     help="1: shards j > 0 start one front phase late; 2: shard j starts after shard j - 1's first front")
-    ap.add_argument("--branch-streams", type=int, default=0,
-                    help="fork the independent branches (text || prompt encoder, F0 || N) onto side streams")
+    ap.add_argument("--branch-streams", default="0",
+                    help="fork independent branches onto side streams inside the graphs: 0 / 1 (all sites) / a comma "
+                         "list of sites (enc = text || prompt encoder, f0n = F0 || N)")
     ap.add_argument("--shared-speaker", action="store_true",
                     help="one reference speaker for the whole job: rank 0 encodes the prompt once and broadcasts its "
                          "discrete codes (stzs.dist.broadcast_prompt_codes); every step then skips the prompt front "
@@ -457,7 +458,9 @@ def main():
     S = SPEC_V0
     # rank 0 owns the weights; every other rank receives them with ONE RCCL broadcast of the arena
     W, bcast_ms = rank_weights(S, rank, world, dev)
-    eng = StyleTTSZS(S, None, device=dev, packed=W, branch_streams=bool(args.branch_streams))
+    bsv = args.branch_streams
+    bs = (bsv == "1") if bsv in ("0", "1") else frozenset(v for v in bsv.split(",") if v)
+    eng = StyleTTSZS(S, None, device=dev, packed=W, branch_streams=bs)
     P = init_params(S, seed=0) if rank == 0 and world == 1 else None  # host params: CPU baseline / extra modes
 
     B = args.batch
@@ -652,7 +655,7 @@ def main():
             "data": "synthetic (seeded tokens 16/s, 3-s noise reference, forced [3,2] durations); random-init weights",
             "config": {"workload": "configs[2]: batch 64/GPU, 5-s targets, 2-step distilled style diffusion, CFG 5",
                        "global_batch": world * B, "seq_len": n_frames, "parallelism": f"dp{world} (utterance shards)",
-                       "spec": S.name, "graph": graph is not None, "branch_streams": bool(args.branch_streams), "streams": nstream,
+                       "spec": S.name, "graph": graph is not None, "branch_streams": bs if isinstance(bs, bool) else sorted(bs), "streams": nstream,
                        "stagger": int(args.stagger) if nstream > 1 else 0, "shared_speaker": bool(args.shared_speaker)},
             "audio_s_per_s_per_gpu": round(value / world, 2),
             "latency": lat,
