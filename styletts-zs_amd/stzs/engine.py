@@ -620,7 +620,8 @@ class StyleTTSZS:
     def fork(self, site, *fns):
         """run fns[0] on the current stream and fns[1:] on side streams forked from it (waits on the current
         stream, joined back into it before returning); sequential unless branch_streams is on (True, or a set of
-        fork sites holding `site`: "enc" = text || prompt encoder, "f0n" = F0 || N predictor branches).
+        fork sites holding `site`: "enc" = text || prompt encoder, "f0n" = F0 || N predictor branches, "src" =
+        decoder pre-blocks || harmonic source).
         Forks nest: a fork inside a branch takes side streams and scratch keys of its own depth, so an inner
         branch never queues behind (or shares scratch with) an outer one.  -> outputs"""
         on = self.branch_streams is True or (isinstance(self.branch_streams, (set, frozenset)) and
@@ -1258,8 +1259,10 @@ class StyleTTSZS:
     def decode(self, pro: dict, codes: torch.Tensor, seeds, istft=True) -> torch.Tensor:
         """a9-a13: decoder pre-blocks, generator, conv_post + iSTFT.  pro: asr_buf (aligned text features in the
         decoder input buffer), F0 / N [B, T80], T40 -> wav fp32 [B, 600 T40] (or conv_post rows, istft=False)."""
-        gen_in, gbd = self.decoder_pre(pro, codes)
-        return self.generator(gen_in, pro["F0"], seeds, gbd, istft=istft)
+        # the harmonic source depends on F0 only: forkable beside the decoder pre-blocks (fork site "src")
+        (gen_in, gbd), har = self.fork("src", lambda: self.decoder_pre(pro, codes),
+                                       lambda: self.sine_gen(pro["F0"], seeds))
+        return self.generator(gen_in, pro["F0"], seeds, gbd, istft=istft, har=har)
 
     def dec_style(self, codes: torch.Tensor) -> torch.Tensor:
         """every AdaIN gamma / beta of the decoder from the pooled acoustic codes: ONE GEMM -> [B, total] fp32."""
