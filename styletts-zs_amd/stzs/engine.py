@@ -1079,7 +1079,13 @@ class StyleTTSZS:
             # runs in ONE launch with the shared F0/N LSTM (stzs_lstm_pair), its projection and the durations kernel
             # after the F0/N branches -- every output the same bits as the sequential order
             d, ov = self.duration_encoder(h_txt, codes, durations)
-            T40 = int(n_frames) if n_frames is not None else int(durations.to(torch.int64).sum(1)[0])
+            if n_frames is not None:
+                T40 = int(n_frames)
+            else:
+                tot = durations.to(torch.int64).sum(1)
+                assert int(tot.min()) == int(tot.max()), \
+                    "one batch must share its total frame count (stzs.scheduler.BucketScheduler groups by it)"
+                T40 = int(tot[0])
             pro = self.prosody_frames(h_txt, codes, d, ov, T40, pair_dur=True)
             du = self.duration_head(d, ov, hd=pro.pop("_hd"))
             pro.update(du, dur=du["dur"])
