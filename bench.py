@@ -24,7 +24,7 @@ h2h     : the same steps timed host to host as well (tokens / reference / noise 
           reported beside `value`, which the driver contract fixes as device-resident (inputs in HBM when the
           timed region starts; the PCIe-inclusive rate is never `value`).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]        (N > 1: starts N rank processes itself)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 """
 from __future__ import annotations
@@ -106,7 +106,7 @@ def host_isa():
     return f"{model} ({cap})" if model else cap
 
 
-def cpu_baseline(S, P, budget_s=15.0):
+def cpu_baseline(S, P, budget_s=15.0, lat_runs=5):
     from oracle import stzs_ref as R
     # every core of this process's affinity, unless the job's CPU share is pinned (OMP_NUM_THREADS: the GPU box
     # sets it to the share one GPU may use; both numbers are reported)
@@ -122,9 +122,21 @@ def cpu_baseline(S, P, budget_s=15.0):
         el = time.perf_counter() - t0
         if el > budget_s or n >= 64:
             break
+    # configs[1] beside the GPU p50 (BASELINE.md c2 "CPU oracle latency, same inputs"): the latency leg's own inputs
+    # (batch 1, 10-step CFG 5, seed 1000 of rank 0), p50 over a few runs after one warm-up
+    tok1, ref1, eps1, dur1 = make_inputs(S, 1, seed=1000)
+    lat = []
+    for i in range(lat_runs + 1):
+        a = time.perf_counter()
+        R.synth(P, S, tok1, ref1, STEPS_LATENCY, CFG, eps1, dur1, seeds=[7])
+        if i:
+            lat.append((time.perf_counter() - a) * 1e3)
     return dict(value=n * TARGET_S / el, unit="audio-s/s", cores=nthr, affinity_cores=aff, isa=host_isa(), kind="port",
                 sample=f"{n} x 1 utterance of the bench workload (5-s target, {STEPS_THROUGHPUT}-step CFG-{CFG:g}), "
-                       f"CPU oracle torch fp32, {el:.1f} s")
+                       f"CPU oracle torch fp32, {el:.1f} s",
+                latency_ms=round(float(np.percentile(lat, 50)), 1),
+                latency_sample=f"configs[1] on the latency leg's inputs (batch 1, 5-s target, {STEPS_LATENCY}-step "
+                               f"CFG-{CFG:g}): p50 of {lat_runs} runs after one warm-up, {nthr} threads")
 
 
 def longform(S, P, dev, runs=7):
@@ -419,9 +431,81 @@ def shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstre
     return run_steps, twins, host
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) without an outside launcher: start N rank processes of this script, one per GPU
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), exactly as
+    `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N` would.  This
+    process makes no GPU call (no HIP runtime initialised here): the ranks own the GPUs, rank 0 prints the JSON line on
+    the shared stdout.  If any rank fails, the others are stopped (by their own PIDs) and its exit code is returned, so
+    a missing GPU or a failed rendezvous ends the run loudly instead of reporting fewer GPUs."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    print(f"[bench] rank process {p.pid} exited with {c}; stopping the other ranks", file=sys.stderr)
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc
+
+
+def dry_run(world, rank):
+    """--dry-run: the N-rank set-up path on CPU under gloo with the tiny spec, up to the first GPU call -- process
+    group, rank 0's weights broadcast to every rank (rank_weights), this rank's input shard (rank_inputs), the max
+    reduction of the timings -- and rank 0 prints one JSON line (tests/test_dist.py runs `bench.py --gpus 2
+    --dry-run` through launch_ranks)."""
+    from stzs.dist import arena_digest, reduce_max
+    from stzs.spec import SPEC_TINY
+    if world > 1:
+        dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    W, bcast_ms = rank_weights(SPEC_TINY, rank, world, dev)
+    tok, ref, eps, dur, seeds = rank_inputs(SPEC_TINY, 4, rank)
+    info = dict(rank=rank, digest=arena_digest(W), seeds=seeds, pid=os.getpid(),
+                env=dict(LOCAL_RANK=os.environ.get("LOCAL_RANK"), MASTER_ADDR=os.environ.get("MASTER_ADDR")))
+    allinfo = [None] * world
+    if world > 1:
+        dist.all_gather_object(allinfo, info)
+        bcast_ms = reduce_max([bcast_ms], dev)[0]
+    else:
+        allinfo = [info]
+    if rank == 0:
+        print(json.dumps(dict(dry_run=True, n_gpus=world, weight_broadcast_ms=round(bcast_ms, 3), ranks=allinfo)))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= rank processes) of this node; > 1 without WORLD_SIZE in the environment starts the "
+                         "ranks itself (launch_ranks); under torch.distributed.run it must equal WORLD_SIZE")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank set-up only (gloo, CPU, tiny spec): process group, weight broadcast, input shards")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=B_THROUGHPUT)
@@ -444,9 +528,22 @@ def main():
                          "end (reported in config; off by default: each utterance has its own reference)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus < 1:
+            sys.exit(f"[bench] --gpus {args.gpus}: need at least one GPU")
+        if args.gpus is not None and args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))  # (this process never touches a GPU)
+        world = 1
+    else:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            sys.exit(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dry_run(world, rank)
+        return
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     if world > 1:

@@ -314,8 +314,9 @@ int stzs_lstm(const stzs_lstm_args* a, void* stream);
 /* two INDEPENDENT recurrences in one launch (side by side on the chip, whatever a graph runtime does with
  * concurrent branches): same B, H, ndir and precise (one kernel shape), each with its own gx / weights / T / y and
  * its OWN xchg workspace and sync block (a->xchg != b->xchg, a->sync != b->sync, else STZS_EINVAL); each output is
- * the same bits as its own stzs_lstm call.  STZS_ESHAPE when the shapes differ or the two grids would exceed one
- * workgroup per CU.  (Replaces two back-to-back stzs_lstm calls -- the duration LSTM and the shared F0/N LSTM
+ * the same bits as its own stzs_lstm call.  STZS_ESHAPE when the shapes differ.  Where the two grids together
+ * would exceed one workgroup per CU (e.g. B > 128 at H = 256) the two recurrences are launched one after the other on
+ * the stream instead -- same bits, no error.  (Replaces two back-to-back stzs_lstm calls -- the duration LSTM and the shared F0/N LSTM
  * of ProsodyPredictor when the durations are given) */
 int stzs_lstm_pair(const stzs_lstm_args* a, const stzs_lstm_args* b, void* stream);
 /* zero an LSTM's exchange state -- the 4096-B `sync` block and the granule region at the start of `xchg` (may be

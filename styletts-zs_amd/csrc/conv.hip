@@ -530,10 +530,10 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
                 k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE, true, true>;
             else if (a.pro_act == STZS_ACT_LEAKY)
                 k = conv_mfma<TIn, TOut, false, STZS_ACT_LEAKY, true, true>;
-            else if (a.pro_act == STZS_ACT_NONE)
-                k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE, true, true>;
-            else
+            else if (a.pro_act == STZS_ACT_SNAKE)
                 k = conv_mfma<TIn, TOut, false, STZS_ACT_SNAKE, true, true>;
+            else
+                k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE, true, true>;
             if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, a);
             STZS_LAUNCH_CHECK();
@@ -547,10 +547,10 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
                 k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE, true>;
             else if (a.pro_act == STZS_ACT_LEAKY)
                 k = conv_mfma<TIn, TOut, false, STZS_ACT_LEAKY, true>;
-            else if (a.pro_act == STZS_ACT_NONE)
-                k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE, true>;
-            else
+            else if (a.pro_act == STZS_ACT_SNAKE)
                 k = conv_mfma<TIn, TOut, false, STZS_ACT_SNAKE, true>;
+            else
+                k = conv_mfma<TIn, TOut, false, STZS_ACT_NONE, true>;
         } else if (flat)
             k = conv_mfma<TIn, TOut, true, STZS_ACT_NONE>;
         else if (a.pro_act == STZS_ACT_SNAKE)
@@ -599,6 +599,9 @@ __attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args*
         return STZS_EINVAL;  // (the prologue partials: generic conv path, <= 8 chunks)
     if (a->pro_mode == STZS_PRO_ADAIN && (!a->pro_part && (!a->pro_mean || !a->pro_rstd)) ) return STZS_EINVAL;
     if (a->pro_mode == STZS_PRO_ADAIN && !a->pro_gb) return STZS_EINVAL;
+    // the prologue activations: NONE, LEAKY, SNAKE only (GELU / SILU are epilogue activations); every kernel family
+    // below selects its prologue template from these three
+    if (a->pro_act != STZS_ACT_NONE && a->pro_act != STZS_ACT_LEAKY && a->pro_act != STZS_ACT_SNAKE) return STZS_EINVAL;
     if (a->pro_act == STZS_ACT_SNAKE && !a->pro_alpha) return STZS_EINVAL;
     if (a->stat_part && (a->ups > 0 || !epi_vec(*a) || a->stat_ld < a->Co || !stzs_aligned(a->stat_part, 8)))
         return STZS_EINVAL;

@@ -403,7 +403,13 @@ static int lstm_launch(const stzs_lstm_args* a, const stzs_lstm_args* b, void* s
     const int gr = lstm_group_rows(a->B, a->H, a->ndir);
     const int groups = (a->B + gr - 1) / gr;
     const int P = a->H / UNITS;
-    if (b && P * a->ndir * 2 * groups > 256) return STZS_ESHAPE;  // both grids co-resident, one workgroup per CU
+    if (b && P * a->ndir * 2 * groups > 256) {
+        // both grids must be co-resident (one workgroup per CU); past that (e.g. B = 129: 9 groups of 16 rows, 144
+        // workgroups per recurrence) the two recurrences run as two launches on the stream, one after the other --
+        // the same bits as the paired launch (each recurrence's groups, gates and exchange are independent of the other)
+        const int rc = lstm_launch(a, nullptr, stream);
+        return rc != STZS_OK ? rc : lstm_launch(b, nullptr, stream);
+    }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // the counters start at zero (caller-zeroed once) and every call leaves them zeroed (see the kernel's
     // tail); the caller's status word (a->status) accumulates over calls and is never cleared here

@@ -30,7 +30,17 @@ namespace {
 
 constexpr int NTH = 256;
 constexpr int BCO = 128;
-constexpr int P = 272;  // staged input row pitch, bytes (conflict-free ds_read_b128)
+// staged input row pitch, bytes.  A B fragment is read by lane (n = lane & 15, g = lane >> 4) at row rb + n, 16-B chunk
+// g + 4 kq; ds_read_b128 serves 64 lanes in four 16-lane groups ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, +32) whose
+// lanes conflict on a 16-B bank slot (a / 16) mod 16.  At pitch 272 the slot is (rb + n + c) mod 16 and every group has
+// one 2-way collision (group 0: n = 12 at chunk g and n = 11 at chunk g + 1), i.e. 8 LDS cycles per read instead of 4
+// (SQ: conflict share 0.505, profiles/r05_g_sq_k11_full.json) -- at the MFMA rate the B reads then need the whole LDS.
+// At pitch 288 the slot is (2 (rb + n) + c) mod 16: within a group the chunk-g lanes land on slots of one parity and the
+// chunk-(g + 1) lanes on the other, 8 distinct slots each for ANY row base rb (every tap / dilation): conflict-free.
+#ifndef STZS_MRFV_P
+#define STZS_MRFV_P 288
+#endif
+constexpr int P = STZS_MRFV_P;
 // staged 16-B vectors per thread (16 rows each): rows_in = 128 + (KS - 1) dil <= 16 SB.  Sized per kernel width
 // (k3: dil <= 8; k7 / k11: dil <= 5), not for the widest: every staged vector costs its transform (the cosines
 // of the Snake) whether or not its row is used, and a k3 tile with SB = 12 transformed 192 rows for 130-138
@@ -39,6 +49,21 @@ constexpr int sb_rows(int ks) { return ks == 3 ? 9 : (ks == 7 ? 10 : 12); }
 constexpr int sb_rows64(int ks) { return ks == 3 ? 5 : (ks == 7 ? 6 : 8); }
 constexpr int SB_MAX = 12;
 constexpr int CS_BYTES = 5 * 128 * 4;  // per-channel prologue constants
+// At pitch >= 288 the constants live in the rows' 32 pad bytes (bytes 256..287, never read or written by the tile's
+// staging / K loop): float i at row i / 8, byte 256 + 4 (i % 8) -- 80 rows; the tile then costs rows x P bytes and
+// the k11 d5 tile (178 rows, 51.3 KB) still fits three workgroups per CU (with the constants appended, 53.8 KB, it
+// did not: 593 vs 555 us per stage-1 k11 launch, profiles/r06a_mrfv_*.log)
+constexpr bool CS_IN_PAD = P >= 288;
+constexpr int CS_ROWS = 5 * 128 / 8;
+STZS_DEV float* cs_at(unsigned char* smem, int rows_in, int i) {
+    if constexpr (CS_IN_PAD) return reinterpret_cast<float*>(smem + (i >> 3) * P + 256 + (i & 7) * 4);
+    return reinterpret_cast<float*>(smem + ((rows_in * P + 15) & ~15)) + i;
+}
+// dynamic LDS bytes of a tile of `rows` staged rows
+inline size_t mrfv_lds(int rows) {
+    if (CS_IN_PAD) return (size_t)(rows > CS_ROWS ? rows : CS_ROWS) * P;
+    return (((size_t)rows * P + 15) & ~(size_t)15) + CS_BYTES;
+}
 
 // x[0..N) summed over the 16 lanes of each DPP row, in place, VALU only.  Each step is ONE v_add_f32 with the DPP
 // permutation on its first source (hipcc emitted a v_mov_b32_dpp + v_add_f32 pair per step); the N values go
@@ -68,16 +93,28 @@ STZS_DEV void row_sum16_n(float* x) {
 // BT: time rows per tile, 128 or 64 (r05: small grids -- batch 1 -- where the 128-row tiles leave CUs idle).  The
 // staged operands, the K order of every output element and the 64-row statistics chunks are the same: bit-identical.
 template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int BT = 128>
-__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
+__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a, int stag, int nslot) {
     static_assert(WPW == 1 || (WPW == 2 && NCH != 1), "the wide form is for multi-chunk inputs");
     static_assert(BT == 128 || (BT == 64 && WPW == 1), "64-row tiles: narrow form");
+    // staggered start (r06): the workgroups of the first dispatch round (one per resident slot) start layer x stag x 2 k
+    // cycles late, layer = dispatch index mod 3 -- the co-resident workgroups of a CU get different layers whether the
+    // dispatcher fills the CUs breadth-first (blocks c, c + 256, c + 512) or depth-first (3c .. 3c + 2).  Equal tiles keep
+    // equal phase offsets afterwards (a freed slot is refilled at once), so one workgroup's staging and epilogue run
+    // beside the others' K loops instead of all of a CU's workgroups loading, computing and storing in phase.
+    if (stag > 0) {
+        const int ld = blockIdx.y * gridDim.x + blockIdx.x;
+        if (ld < nslot) {
+            const int n = (ld % 3) * stag;
+            for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);
+        }
+    }
     constexpr int NA = 2 * WPW;  // A fragments (16 output channels each) per wave and K-step
     constexpr int MT = BT / 16;  // 16-row B fragments per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NKC = KS * 4;  // 32-wide K-steps per 128-channel chunk
     const int dil = a.dil;
     const int rows_in = BT + (KS - 1) * dil;
-    float* cs = reinterpret_cast<float*>(smem + ((rows_in * P + 15) & ~15));
+    auto cs = [&](int i) { return cs_at(smem, rows_in, i); };
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tpb = (a.T_out + BT - 1) / BT;
     const int nx = gridDim.x;
@@ -174,14 +211,14 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                     const float al = ok ? a.pro_alpha[ch] : 1.f;
                     const float h = 0.5f / al;
                     const float w = al * 0.318309886183790672f;  // a / pi
-                    cs[tid] = sc * w;
-                    cs[128 + tid] = sh * w;
-                    cs[256 + tid] = sc;
-                    cs[384 + tid] = sh + h;
-                    cs[512 + tid] = -h;
+                    *cs(tid) = sc * w;
+                    *cs(128 + tid) = sh * w;
+                    *cs(256 + tid) = sc;
+                    *cs(384 + tid) = sh + h;
+                    *cs(512 + tid) = -h;
                 } else {
-                    cs[256 + tid] = sc;
-                    cs[384 + tid] = sh;
+                    *cs(256 + tid) = sc;
+                    *cs(384 + tid) = sh;
                 }
             }
             // the tile's rows (+ dilation halo): SB 16-B loads per thread, then the transform in registers, then the
@@ -210,13 +247,13 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 for (int p = 0; p < 4; ++p) {
                     __builtin_amdgcn_sched_barrier(0);  // keep one pair's constants live at a time
                     const int c0 = cv * 8 + 2 * p;
-                    const f32x2 ksc = *reinterpret_cast<const f32x2*>(cs + 256 + c0);
-                    const f32x2 ksh = *reinterpret_cast<const f32x2*>(cs + 384 + c0);
+                    const f32x2 ksc = *reinterpret_cast<const f32x2*>(cs(256 + c0));
+                    const f32x2 ksh = *reinterpret_cast<const f32x2*>(cs(384 + c0));
                     f32x2 ka = {0.f, 0.f}, kbv = {0.f, 0.f}, km = {0.f, 0.f};
                     if constexpr (PACT == STZS_ACT_SNAKE) {
-                        ka = *reinterpret_cast<const f32x2*>(cs + c0);
-                        kbv = *reinterpret_cast<const f32x2*>(cs + 128 + c0);
-                        km = *reinterpret_cast<const f32x2*>(cs + 512 + c0);
+                        ka = *reinterpret_cast<const f32x2*>(cs(c0));
+                        kbv = *reinterpret_cast<const f32x2*>(cs(128 + c0));
+                        km = *reinterpret_cast<const f32x2*>(cs(512 + c0));
                     }
 #pragma unroll
                     for (int i = 0; i < SB; ++i) {
@@ -288,6 +325,13 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
+#ifndef STZS_MRFV_PRIO
+#define STZS_MRFV_PRIO 0
+#endif
+        // the K loop at wave priority 1, staging / epilogue at 0: a co-resident wave's staging VALU (the Snake cosines)
+        // then takes the issue slots the MFMA stream leaves, instead of delaying the next MFMA by age arbitration
+        // (MI355X_MICROARCH.md "Two waves per SIMD" item 2)
+        if constexpr (STZS_MRFV_PRIO) __builtin_amdgcn_s_setprio(1);
         if constexpr (NCH == 1) {
             kloop(std::integral_constant<bool, true>{});
         } else {  // (two K-loop bodies spill the multi-chunk forms: zero the accumulators once instead)
@@ -299,6 +343,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
             }
             kloop(std::integral_constant<bool, false>{});
         }
+        if constexpr (STZS_MRFV_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     if (a.flags & 4) return;
 
@@ -393,7 +438,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 }
 
 template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1, int BT = 128>
-void (*pick_ks(int ks))(stzs_conv_args) {
+void (*pick_ks(int ks))(stzs_conv_args, int, int) {
     switch (ks) {
         case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL, WPW, BT>;
         case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL, WPW, BT>;
@@ -402,7 +447,7 @@ void (*pick_ks(int ks))(stzs_conv_args) {
     }
 }
 template <int PACT, bool HR, bool HA>
-void (*pick(int ks, bool one, bool al, bool wide, bool t64))(stzs_conv_args) {
+void (*pick(int ks, bool one, bool al, bool wide, bool t64))(stzs_conv_args, int, int) {
     if (wide) return al ? pick_ks<PACT, HR, HA, 0, true, 2>(ks) : pick_ks<PACT, HR, HA, 0, false, 2>(ks);
     if (t64) {  // (64-row tiles: the Snake forms of small grids)
         if (al) return one ? pick_ks<PACT, HR, HA, 1, true, 1, 64>(ks) : pick_ks<PACT, HR, HA, 0, true, 1, 64>(ks);
@@ -427,7 +472,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
     if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
-    void (*k)(stzs_conv_args) = nullptr;
+    void (*k)(stzs_conv_args, int, int) = nullptr;
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
     bool blk_wide = false, blk_t64 = false;
     // the wide form (256 output channels per workgroup) for multi-chunk Snake convs whose wide grid still gives every
@@ -443,8 +488,6 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     const bool t64 = !wide && a.pro_act == STZS_ACT_SNAKE && tiles128 < 2 * stzs_cu_count() &&
                      rows64 <= 16 * (a.ks == 3 ? sb_rows64(3) : a.ks == 7 ? sb_rows64(7) : sb_rows64(11)) &&
                      !(a.flags & STZS_CONV_MRFV_T128);
-    const int BT = t64 ? 64 : 128;
-    const size_t lds = ((((size_t)BT + (a.ks - 1) * a.dil) * P + 15) & ~(size_t)15) + CS_BYTES;
     if (a.pro_act == STZS_ACT_SNAKE) {
         const bool one = a.ci_pad == 128;
         const bool al = a.alpha != 1.f;
@@ -477,11 +520,16 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     }
     if (!k) return STZS_ESHAPE;
     const int BTk = (t64 || blk_t64) ? 64 : 128;
-    const size_t ldsk = ((((size_t)BTk + (a.ks - 1) * a.dil) * P + 15) & ~(size_t)15) + CS_BYTES;
-    (void)lds;
+    const size_t ldsk = mrfv_lds(BTk + (a.ks - 1) * a.dil);
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsk);
     dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BTk - 1) / BTk), a.co_pad / (wide || blk_wide ? 2 * BCO : BCO));
-    hipLaunchKernelGGL(k, grid, dim3(NTH), ldsk, s, a);
+    // staggered start of the first round (see the kernel): STZS_MRFV_STAG = sleep units of 2 k cycles per layer
+    static const int stag = [] {
+        const char* e = getenv("STZS_MRFV_STAG");
+        return e ? atoi(e) : 0;
+    }();
+    const int occ = (a.ci_pad == 128 && !(wide || blk_wide)) ? STZS_MRFV_OCC1 : STZS_MRFV_OCC;
+    hipLaunchKernelGGL(k, grid, dim3(NTH), ldsk, s, a, stag, occ * stzs_cu_count());
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

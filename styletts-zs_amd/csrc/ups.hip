@@ -5,7 +5,7 @@
 // general MRF-family kernel gives every 128-column tile its own workgroup, and each of them stages (loads + LeakyReLU
 // + bf16 LDS image) the same input rows again: the stage-1 ConvT (r = 6: 6 tiles) read its 131 MB input 6 times and
 // ran at 0.25 of its HBM roofline (462 us for 917 MB of algorithmic traffic at batch 64).  Here one workgroup:
-//   * stages the 129 input rows of its 128-row tile for EVERY 128-channel chunk once (LDS: chunks x 35 KB), and
+//   * stages the 129 input rows of its 128-row tile for EVERY 128-channel chunk once (LDS: chunks x 37 KB), and
 //   * walks its column tiles (all of them, or a slice for very wide layers) over that resident tile, the
 //     register-direct way of csrc/mrfv.hip: each wave owns 32 output columns, its weight fragments
 //     (STZS_CONV_W_FRAG32 packing) come straight from global memory into VGPRs through a 4-deep register ring that
@@ -21,7 +21,10 @@ namespace {
 
 constexpr int NTH = 256;
 constexpr int BT = 128;
-constexpr int P = 272;                    // staged row pitch, bytes (conflict-free ds_read_b128)
+#ifndef STZS_UPS_P
+#define STZS_UPS_P 288
+#endif
+constexpr int P = STZS_UPS_P;             // staged row pitch, bytes (288: conflict-free ds_read_b128, csrc/mrfv.hip)
 constexpr int ROWS = BT + 1;              // a 2-tap conv at pad 1: rows q0 - 1 .. q0 + 127
 constexpr int TILE = (ROWS * P + 15) & ~15;
 constexpr int SB = 9;                     // 16 row lanes x 9 >= 129 rows

@@ -512,7 +512,7 @@ class StyleTTSZS:
             ntile = (a.T_out + L.CONV_STAT_ROWS - 1) // L.CONV_STAT_ROWS
             defer = self.defer_stats and ntile <= 8
             # (deferred: the partials must outlive this launch until their consumer reads them -- a slab per key)
-            slab = self._scratch("stat_slab." + stats_key, y.B * ntile * Cc * 2) if defer else self._slab(y.B * ntile * Cc * 2)
+            slab = self._scratch("stat_slab." + stats_key, y.B * ntile * Cc * 2, 1024) if defer else self._slab(y.B * ntile * Cc * 2)
             a.stat_part, a.stat_ld = slab.data_ptr(), Cc
             st = (slab, Cc, self.buf(stats_key + ".m", (y.B, Cc), torch.float32),
                   self.buf(stats_key + ".r", (y.B, Cc), torch.float32), defer, ntile)
@@ -588,19 +588,20 @@ class StyleTTSZS:
         nk = cw.ci_pad // 32
         return int(self.small_rows and nk % 4 == 0 and nk // 4 in (1, 2, 4, 8, 16))
 
-    def _scratch(self, name, n):
+    def _scratch(self, name, n, minimum=1 << 20):
         """fp32 scratch shared by consecutive launches of ONE branch (a conv's statistics partials, consumed by
         the finalize launch right behind it; the standalone statistics workspace).  Each forked branch has its
         own (key suffix self._branch): concurrent branches sharing one slab would race on the partials.  A
         grown slab's old storage is retired, not freed: launches already enqueued (or captured) on it --
         possibly on another stream -- still read it, and a freed block could be handed to another stream's
-        allocation while they run."""
+        allocation while they run.  minimum: the smallest storage (the shared slabs start at 4 MB so they rarely grow;
+        the per-key deferred-statistics slabs are sized exactly -- a batch-1 partial is a few KB)."""
         key = name + self._branch
         t = self._bufs.get(key)
         if t is None or t.numel() < n:
             if t is not None:
                 self._retired.append(t)
-            t = self._bufs[key] = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=self.device)
+            t = self._bufs[key] = torch.empty(max(n, minimum), dtype=torch.float32, device=self.device)
         return t
 
     def _counters(self, name, n):
@@ -674,7 +675,7 @@ class StyleTTSZS:
         nch = (x.T + 255) // 256
         defer = self.defer_stats and nch <= 8
         nws = self.lib.stzs_chan_stats_workspace(x.B, x.T, Cc) // 4 + 1
-        ws = self._scratch("stat_ws." + key, nws) if defer else self._scratch("stat_ws", nws)
+        ws = self._scratch("stat_ws." + key, nws, 1024) if defer else self._scratch("stat_ws", nws)
         a = L.StatsArgs()
         a.x, a.mean, a.rstd, a.partial = x.ptr, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr()
         a.ld, a.bs, a.stat_bs, a.B, a.T, a.C, a.dtype, a.eps = x.ld, x.bs, Cc, x.B, x.T, Cc, x.dt, 1e-5

@@ -158,3 +158,27 @@ def test_shard_range_partition():
             assert got[0][0] == 0 and got[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
             assert max(h - l for l, h in got) - min(h - l for l, h in got) <= 1
+
+
+def test_bench_launcher_spawns_ranks():
+    """`python bench.py --gpus 2` with no WORLD_SIZE in the environment starts the 2 rank processes
+    itself (bench.launch_ranks: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* per rank, rendezvous on 127.0.0.1) and the
+    ranks run bench's world-2 set-up (here --dry-run: gloo, CPU, tiny spec, up to the first GPU call) -- rank 0's line
+    says n_gpus 2, every rank holds rank 0's arena, the shards are disjoint; a --gpus / WORLD_SIZE mismatch fails."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["dry_run"] and line["n_gpus"] == 2 and line["weight_broadcast_ms"] > 0
+    ranks = line["ranks"]
+    assert [x["rank"] for x in ranks] == [0, 1]
+    assert ranks[0]["digest"] == ranks[1]["digest"]
+    assert ranks[0]["pid"] != ranks[1]["pid"] and ranks[1]["env"] == dict(LOCAL_RANK="1", MASTER_ADDR="127.0.0.1")
+    assert set(ranks[0]["seeds"]).isdisjoint(ranks[1]["seeds"])
+    bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                         env=dict(env, WORLD_SIZE="1"), capture_output=True, text=True, timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

@@ -340,6 +340,32 @@ def test_latency_engine_deferred_stats_bit_identical(v0):
     assert launches[True] < launches[False]
 
 
+def test_dur_overlap_large_batch(v0):
+    """with durations given every engine pairs the duration LSTM with the shared F0/N LSTM; at B = 129 the
+    paired grid exceeds one workgroup per CU and stzs_lstm_pair falls back to two launches.  The synthesis must run
+    (no STZS_ESHAPE) and give the same bits as the sequential order (1-step sampling: the batch size is the point)."""
+    S, P, eng = v0
+    assert eng.dur_overlap
+    B = 129
+    tok, ref, eps, dur, seeds = bench.rank_inputs(S, B, 13)
+    nf = int(dur[0].sum())
+    dev = eng.device
+    tok_d, ref_d, eps_d, dur_d = (t.to(dev) for t in (tok, ref, eps, dur))
+    keys = ("codes", "F0", "N", "wav", "dur")
+    outs = {}
+    try:
+        for ov in (False, True):
+            eng.dur_overlap = ov
+            o = eng.synth(tok_d, ref_d, steps=1, cfg_scale=bench.CFG, noise=eps_d, durations=dur_d, seeds=seeds,
+                          n_frames=nf, check=False)
+            outs[ov] = {k: (o[k] if torch.is_tensor(o[k]) else o[k].t).detach().clone().cpu() for k in keys}
+    finally:
+        eng.dur_overlap = True
+    eng.check_status()
+    for k in keys:
+        assert torch.equal(outs[True][k], outs[False][k]), k
+
+
 @pytest.mark.parametrize("branch_streams", [False, True])
 def test_dur_overlap_bit_identical(v0, branch_streams):
     """with durations given, the alignment reads them directly and the duration LSTM runs in ONE launch with the

@@ -195,3 +195,25 @@ def test_conv_mfma_splitk(eng, splitk, case):
         print("   stats: mean abs err", em, "rstd rel err", er, "vs unsplit", eu)
         assert em < 1e-4 and er < 3e-4
         assert eu[0] < 1e-4 and eu[1] < 3e-4  # the unsplit conv's bf16 output differs by re-association roundings
+
+
+@pytest.mark.parametrize("splitk", [1, 4, 16])
+def test_conv_rejects_epilogue_act_as_prologue(eng, splitk):
+    """the prologue activation is NONE / LEAKY / SNAKE; an epilogue-only activation (GELU, SILU) passed as
+    pro_act is rejected with STZS_EINVAL before any launch (the DEEP / splitk_epi forms used to route it to the Snake
+    template, which reads pro_alpha -- a null pointer here)."""
+    from stzs import _lib as L
+    from stzs.engine import Act
+    from stzs.weights import Arena, pack_conv
+    B, T, Ci, Co = 1, 80, 512, 512
+    w = torch.randn(Co, Ci, 5) / math.sqrt(Ci * 5)
+    A = Arena()
+    cw = pack_conv(A, "t", w, torch.zeros(Co))
+    A.finalize("cuda:0")
+    cw.w, cw.b = A[cw.w], A[cw.b]
+    x = Act(torch.randn(B, T, Ci, device="cuda:0").to(torch.bfloat16))
+    y = Act(torch.zeros(B, T, Co, dtype=torch.bfloat16, device="cuda:0"))
+    for act in (L.ACT_GELU, L.ACT_SILU):
+        with pytest.raises(L.StzsError, match="rc=-?[0-9]+"):
+            eng.conv(cw, x, y, pad=2, splitk=splitk, pro_act=act)
+    torch.cuda.synchronize()

@@ -275,3 +275,33 @@ def test_decode_chunked_reduces_to_decode(tiny, tiny_params):
     assert ((w3 - full).norm() / full.norm()).item() > 1e-3
     # fixed-length windows (W = chunk + 2 halo = 14), the first and last shifted inward
     assert R.chunk_windows(23, 8, 3) == [(0, 8, 0, 14), (8, 16, 5, 19), (16, 23, 9, 23)]
+
+
+def test_fp64_oracle_path(tiny, tiny_params):
+    """the float64 oracle (tools/oracle_floor.py, DESIGN.md §3 "the oracle's own floor"): fp64 parameters / codes run every
+    op in fp64 -- the BiLSTMs, the iSTFT window, the harmonic source (harmonic_source64: the same phase prefix, counter
+    streams and formula as the fp32 source, no fp32 rounding) -- and land within fp32 rounding of the fp32 oracle."""
+    S, P = tiny, tiny_params
+    g = torch.Generator().manual_seed(5)
+    F0 = 100 + 150 * torch.rand(1, 40, generator=g)
+    F0[:, :4] = 0.0
+    s32 = R.harmonic_source(P, S, F0, [3])
+    s64 = R.harmonic_source(P, S, F0.double(), [3])
+    assert s32.dtype == torch.float32 and s64.dtype == torch.float64
+    assert (s64 - s32.double()).abs().max().item() < 1e-5
+    T = 12
+    tok = torch.randint(1, S.n_symbols, (1, T), generator=g)
+    codes = torch.randn(1, S.L_s, S.code_dim, generator=g) * 0.3
+    dur = torch.tensor([[3, 2] * (T // 2)], dtype=torch.int32)
+    P64 = {k: (v.double() if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in P.items()}
+    with torch.no_grad():
+        out = {}
+        for name, PP, cc in (("32", P, codes), ("64", P64, codes.double())):
+            h = R.text_encoder(PP, S, tok)
+            pro = R.predict_prosody(PP, S, h, cc, dur)
+            out[name] = (R.decode(PP, S, pro["asr"], pro["F0"], pro["N"], cc, [3]), pro["F0"])
+    w32, f32 = out["32"]
+    w64, f64 = out["64"]
+    assert w64.dtype == torch.float64 and f64.dtype == torch.float64
+    assert ((w64 - w32.double()).norm() / w64.norm()).item() < 1e-3
+    assert ((f64 - f32.double()).norm() / f64.norm()).item() < 1e-5
