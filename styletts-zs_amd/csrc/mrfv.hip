@@ -6,7 +6,7 @@
 namespace {
 
 template <int PACT, bool HR, bool HA>
-void (*pick(int ks, bool one, bool al, bool wide, bool t64))(stzs_conv_args, int, int) {
+void (*pick(int ks, bool one, bool al, bool wide, bool t64))(stzs_conv_args) {
     if (wide) return al ? pick_ks<PACT, HR, HA, 0, true, 2>(ks) : pick_ks<PACT, HR, HA, 0, false, 2>(ks);
     static_assert(PACT == STZS_ACT_SNAKE, "the single-chunk forms are the Snake (MRF) convs");
     if (one) return stzs_mrfv_pick_n1(ks, HR, HA, al, t64);  // (csrc/mrfv_n1.hip)
@@ -30,7 +30,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
         return STZS_ESHAPE;
     if (a.pro_act == STZS_ACT_SNAKE && !a.pro_alpha) return STZS_EINVAL;
     if (a.pro_act == STZS_ACT_SNAKE && a.res && a.res_tdiv != 1) return STZS_ESHAPE;  // (TD1 in the kernel)
-    void (*k)(stzs_conv_args, int, int) = nullptr;
+    void (*k)(stzs_conv_args) = nullptr;
     const bool R = a.res != nullptr, A = a.acc_in != nullptr;
     bool blk_wide = false, blk_t64 = false;
     // the wide form (256 output channels per workgroup) for multi-chunk Snake convs whose wide grid still gives every
@@ -81,13 +81,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     const size_t ldsk = mrfv_lds(BTk + (a.ks - 1) * a.dil);
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsk);
     dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BTk - 1) / BTk), a.co_pad / (wide || blk_wide ? 2 * BCO : BCO));
-    // staggered start of the first round (see the kernel): STZS_MRFV_STAG = sleep units of 2 k cycles per layer
-    static const int stag = [] {
-        const char* e = getenv("STZS_MRFV_STAG");
-        return e ? atoi(e) : 0;
-    }();
-    const int occ = (a.ci_pad == 128 && !(wide || blk_wide)) ? STZS_MRFV_OCC1 : STZS_MRFV_OCC;
-    hipLaunchKernelGGL(k, grid, dim3(NTH), ldsk, s, a, stag, occ * stzs_cu_count());
+    hipLaunchKernelGGL(k, grid, dim3(NTH), ldsk, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

@@ -96,21 +96,9 @@ STZS_DEV void row_sum16_n(float* x) {
 // BT: time rows per tile, 128 or 64 (r05: small grids -- batch 1 -- where the 128-row tiles leave CUs idle).  The
 // staged operands, the K order of every output element and the 64-row statistics chunks are the same: bit-identical.
 template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int BT = 128>
-__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a, int stag, int nslot) {
+__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
     static_assert(WPW == 1 || (WPW == 2 && NCH != 1), "the wide form is for multi-chunk inputs");
     static_assert(BT == 128 || (BT == 64 && WPW == 1), "64-row tiles: narrow form");
-    // staggered start (r06): the workgroups of the first dispatch round (one per resident slot) start layer x stag x 2 k
-    // cycles late, layer = dispatch index mod 3 -- the co-resident workgroups of a CU get different layers whether the
-    // dispatcher fills the CUs breadth-first (blocks c, c + 256, c + 512) or depth-first (3c .. 3c + 2).  Equal tiles keep
-    // equal phase offsets afterwards (a freed slot is refilled at once), so one workgroup's staging and epilogue run
-    // beside the others' K loops instead of all of a CU's workgroups loading, computing and storing in phase.
-    if (stag > 0) {
-        const int ld = blockIdx.y * gridDim.x + blockIdx.x;
-        if (ld < nslot) {
-            const int n = (ld % 3) * stag;
-            for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);
-        }
-    }
     constexpr int NA = 2 * WPW;  // A fragments (16 output channels each) per wave and K-step
     constexpr int MT = BT / 16;  // 16-row B fragments per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -328,13 +316,6 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
-#ifndef STZS_MRFV_PRIO
-#define STZS_MRFV_PRIO 0
-#endif
-        // the K loop at wave priority 1, staging / epilogue at 0: a co-resident wave's staging VALU (the Snake cosines)
-        // then takes the issue slots the MFMA stream leaves, instead of delaying the next MFMA by age arbitration
-        // (MI355X_MICROARCH.md "Two waves per SIMD" item 2)
-        if constexpr (STZS_MRFV_PRIO) __builtin_amdgcn_s_setprio(1);
         if constexpr (NCH == 1) {
             kloop(std::integral_constant<bool, true>{});
         } else {  // (two K-loop bodies spill the multi-chunk forms: zero the accumulators once instead)
@@ -346,7 +327,6 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
             }
             kloop(std::integral_constant<bool, false>{});
         }
-        if constexpr (STZS_MRFV_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     if (a.flags & 4) return;
 
@@ -441,7 +421,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 }
 
 template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1, int BT = 128>
-void (*pick_ks(int ks))(stzs_conv_args, int, int) {
+void (*pick_ks(int ks))(stzs_conv_args) {
     switch (ks) {
         case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL, WPW, BT>;
         case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL, WPW, BT>;
@@ -456,5 +436,5 @@ void (*pick_ks(int ks))(stzs_conv_args, int, int) {
 // packed-fp32 VALU ops: beside the K loop's MFMAs a v_pk_fma_f32 costs more issue than two v_fma_f32
 // (MI355X_MICROARCH.md constants table, "packed f32 VALU ... an anti-lever beside MFMAs"); stage-1 k7 / k11 2.5-5 %
 // faster so built (profiles/r06e_mrfv_nopk.log), while the wide stage-0 forms (256 VGPRs) lose 7 % and keep them
-using mrfv_kfn = void (*)(stzs_conv_args, int, int);
+using mrfv_kfn = void (*)(stzs_conv_args);
 mrfv_kfn stzs_mrfv_pick_n1(int ks, bool hr, bool ha, bool al, bool t64);
