@@ -85,6 +85,21 @@ STZS_DEV void row_sum16_n(float* x) {
     for (int i = 0; i < N; ++i) asm volatile("v_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf" : "+v"(x[i]));
 }
 
+// STZS_MRFV_PROF probe build (tools/mrfv_phase.py --build; never in the library build): thread 0 of every workgroup
+// stamps into g_mprof[workgroup][8]: s_memtime at entry (0), after the staging barrier (1), after the K loop (2), after
+// the epilogue's stores issued (3) and drained (4); s_memrealtime (100 MHz) at entry (5) and exit (6); HW_ID | XCC_ID << 32
+// (7).  Workgroup = dispatch index blockIdx.y * gridDim.x + blockIdx.x.  STZS_MRFV_DIAG=2 (probe only): no row loads.
+#ifdef STZS_MRFV_PROF
+__device__ unsigned long long g_mprof[8 * 16384];
+#define MPROF(i, v)                                                                    \
+    if (threadIdx.x == 0) {                                                            \
+        const unsigned wg_ = blockIdx.y * gridDim.x + blockIdx.x;                     \
+        if (wg_ < 16384) g_mprof[wg_ * 8 + (i)] = (v);                                 \
+    }
+#else
+#define MPROF(i, v)
+#endif
+
 // NCH = 1: exactly one 128-channel input chunk (the stage-1 generator convs): the accumulators are not live
 // during the staging, so the kernel fits 3 workgroups per CU; NCH = 0: any number of chunks, 2 per CU.
 // AL: the epilogue scales by a.alpha (alpha != 1; a uniform runtime test was if-converted into a multiply + select
@@ -99,6 +114,10 @@ template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int
 __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
     static_assert(WPW == 1 || (WPW == 2 && NCH != 1), "the wide form is for multi-chunk inputs");
     static_assert(BT == 128 || (BT == 64 && WPW == 1), "64-row tiles: narrow form");
+    MPROF(5, __builtin_amdgcn_s_memrealtime())
+    MPROF(0, __builtin_amdgcn_s_memtime())
+    MPROF(7, (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                 ((unsigned long long)__builtin_amdgcn_s_getreg(0x14 | (3 << 11)) << 32))
     constexpr int NA = 2 * WPW;  // A fragments (16 output channels each) per wave and K-step
     constexpr int MT = BT / 16;  // 16-row B fragments per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -182,6 +201,26 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
             const int c = cc * 128 + cv * 8;
             const bool c_ok = c < a.Ci;  // vectors past Ci (ci_pad > Ci) are zero; weights there are 0
             const int cl = c_ok ? c : 0;
+            // EARLY (r06, the single-chunk stage-1 forms): the tile's rows are loaded BEFORE the per-channel constants
+            // below -- whose own global loads the constants block waits for -- instead of after them: one memory
+            // latency per tile instead of two in series (tools/mrfv_phase.py: the staging phase is the longest phase of a
+            // stage-1 workgroup).  Clamped addresses for every tile (an interior tile's are unchanged).  The multi-chunk
+            // forms keep the old order: raw vectors live across the constants block spill the 256-VGPR wide form.
+            constexpr bool EARLY = NCH == 1 && !PF;
+            uint4 rawe[EARLY ? SB : 1];
+            if constexpr (EARLY) {
+#pragma unroll
+                for (int i = 0; i < SB; ++i) {
+                    int tin = t0 - a.pad + rsub + 16 * i;
+                    tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
+                    const unsigned off = (unsigned)(tin * (int)a.ldx + cl) * 2u;
+#if defined(STZS_MRFV_PROF) && STZS_MRFV_DIAG == 2
+                    rawe[i] = make_uint4(off, off ^ 1u, off ^ 2u, off ^ 3u);  // (probe: no loads, same transform)
+#else
+                    rawe[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(X) + off);
+#endif
+                }
+            }
             // per-channel constants (128 threads):  t = x*ka + kb (revolutions of cos(2 a y)),
             // out = cos(t) * km + (x*ksc + ksh)  [Snake]   or   out = act(x*ksc + ksh)
             if (tid < 128) {
@@ -222,6 +261,8 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 for (int i = 0; i < SB; ++i) {  // 32-bit offsets from the utterance base (SGPR): saddr loads
                     if constexpr (PF) {
                         raw[i] = rawn[i];  // (loaded under the previous chunk's K loop)
+                    } else if constexpr (EARLY) {
+                        raw[i] = rawe[i];  // (loaded ahead of the constants)
                     } else {
                         int tin = t0 - a.pad + rsub + 16 * i;
                         if constexpr (!FULL) tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
@@ -281,6 +322,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
                 stage(std::integral_constant<bool, false>{});
         }
         __syncthreads();
+        MPROF(1, __builtin_amdgcn_s_memtime())
         if constexpr (PF) {
             if (cc + 1 < nchunk && !(a.flags & 1)) prefetch(cc + 1);  // the next chunk flies under this K loop
         }
@@ -328,6 +370,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
             kloop(std::integral_constant<bool, false>{});
         }
     }
+    MPROF(2, __builtin_amdgcn_s_memtime())
     if (a.flags & 4) return;
 
     // ---------------- epilogue: lane (g, n): time t = t0 + mt*16 + n, channels co0 .. co0 + 7
@@ -418,6 +461,12 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
         }
     }
     }
+#ifdef STZS_MRFV_PROF
+    MPROF(3, __builtin_amdgcn_s_memtime())
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    MPROF(4, __builtin_amdgcn_s_memtime())
+    MPROF(6, __builtin_amdgcn_s_memrealtime())
+#endif
 }
 
 template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1, int BT = 128>

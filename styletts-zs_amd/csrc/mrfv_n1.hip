@@ -16,3 +16,15 @@ mrfv_kfn stzs_mrfv_pick_n1(int ks, bool hr, bool ha, bool al, bool t64) {
 #undef STZS_N1
     return nullptr;
 }
+
+#ifdef STZS_MRFV_PROF
+// (probe build only) the stage-1 instances' phase stamps -> host; zero: clear them after the copy
+extern "C" int stzs_mrfv_prof_read(unsigned long long* host, size_t n, int zero) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_mprof)) != hipSuccess) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (host && hipMemcpy(host, p, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (zero && hipMemset(p, 0, sizeof(unsigned long long) * 8 * 16384) != hipSuccess) return -1;
+    return 0;
+}
+#endif
