@@ -34,7 +34,7 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=
 NO_PK = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 FILE_FLAGS = {"source.hip": NO_PK, "conv.hip": NO_PK, "gemm.hip": NO_PK, "convx.hip": NO_PK,
               # (r06, for speed, not the hazard: the stage-1 MRF convs' staging VALU beside MFMAs, csrc/mrfv_n1.hip)
-              "mrfv_n1.hip": NO_PK, "mrfv_n1p.hip": NO_PK}
+              "mrfv_n1.hip": NO_PK}
 
 
 def sources():

@@ -43,30 +43,14 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     // 188 tiles, a stage-0 conv 64); also bit-identical.  STZS_CONV_MRFV_T128 keeps the 128-row tiles (A/B switch).
     const long tiles128 = (long)a.B * ((a.T_out + 127) / 128) * (a.co_pad / BCO);
     const int rows64 = 64 + (a.ks - 1) * a.dil;
-    static const long t64_snake = [] {  // (A/B knob: STZS_MRFV_T64_SNAKE=N moves the threshold to N tiles per CU)
-        const char* e = getenv("STZS_MRFV_T64_SNAKE");
-        return e ? atol(e) : 2L;
-    }();
-    const bool t64 = !wide && a.pro_act == STZS_ACT_SNAKE && tiles128 < t64_snake * stzs_cu_count() &&
+    const bool t64 = !wide && a.pro_act == STZS_ACT_SNAKE && tiles128 < 2 * stzs_cu_count() &&
                      rows64 <= 16 * (a.ks == 3 ? sb_rows64(3) : a.ks == 7 ? sb_rows64(7) : sb_rows64(11)) &&
                      !(a.flags & STZS_CONV_MRFV_T128);
-    // tile runs (mrfv_kernel.hpp PT) for the single-chunk forms: `run` consecutive 128-row tiles per workgroup
-    static const int run_len = [] {
-        const char* e = getenv("STZS_MRFV_RUN");
-        return e ? atoi(e) : 1;
-    }();
-    int runs = 0;  // runs per utterance (0: one tile per workgroup)
     if (a.pro_act == STZS_ACT_SNAKE) {
         const bool one = a.ci_pad == 128;
         const bool al = a.alpha != 1.f;
-        if (one && !t64 && run_len > 1) {
-            const int tpb = (a.T_out + 127) / 128;
-            runs = (tpb + run_len - 1) / run_len;
-            k = stzs_mrfv_pick_n1_run(a.ks, R, A, al);
-        } else {
-            k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide, t64))
-                  : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide, t64));
-        }
+        k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide, t64))
+              : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide, t64));
     } else if (!A && a.ks == 3) {  // the AdaIN residual blocks of the decoder / prosody predictor
         // (r05) the wide form here too where the wide grid gives every CU two workgroups (a decoder conv at 64
         // utterances: 512 wide tiles): each 9-chunk input row staged once per 256 output channels instead of per 128 --
@@ -96,7 +80,7 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
     const int BTk = (t64 || blk_t64) ? 64 : 128;
     const size_t ldsk = mrfv_lds(BTk + (a.ks - 1) * a.dil);
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsk);
-    dim3 grid((unsigned)a.B * (unsigned)(runs ? runs : (a.T_out + BTk - 1) / BTk), a.co_pad / (wide || blk_wide ? 2 * BCO : BCO));
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BTk - 1) / BTk), a.co_pad / (wide || blk_wide ? 2 * BCO : BCO));
     hipLaunchKernelGGL(k, grid, dim3(NTH), ldsk, s, a);
     STZS_LAUNCH_CHECK();
     return STZS_OK;

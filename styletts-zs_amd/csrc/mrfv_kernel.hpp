@@ -28,9 +28,6 @@
 #ifndef STZS_MRFV_OCC1
 #define STZS_MRFV_OCC1 3
 #endif
-#ifndef STZS_MRFV_OCCP
-#define STZS_MRFV_OCCP 2  // (the tile-run forms: the next tile's rows stay live across the K loop -- at 3 they spill)
-#endif
 
 namespace {
 
@@ -113,15 +110,10 @@ __device__ unsigned long long g_mprof[8 * 16384];
 // order per output element either way (bit-identical).
 // BT: time rows per tile, 128 or 64 (r05: small grids -- batch 1 -- where the 128-row tiles leave CUs idle).  The
 // staged operands, the K order of every output element and the 64-row statistics chunks are the same: bit-identical.
-// PT (r06, single-chunk forms): a workgroup walks a run of consecutive row tiles of ONE utterance (gridDim.x = B x
-// runs per utterance; the run length follows from the grid), computing the per-channel constants once and loading the
-// next tile's raw rows into registers right after the current tile's staging, so they fly under its K loop and
-// epilogue instead of being waited for at the next staging.  Same staged operands, same K order: bit-identical.
-template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int BT = 128, bool PT = false>
-__global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OCC1) : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
+template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int BT = 128>
+__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
     static_assert(WPW == 1 || (WPW == 2 && NCH != 1), "the wide form is for multi-chunk inputs");
     static_assert(BT == 128 || (BT == 64 && WPW == 1), "64-row tiles: narrow form");
-    static_assert(!PT || (NCH == 1 && WPW == 1), "tile runs: the single-chunk narrow forms");
     MPROF(5, __builtin_amdgcn_s_memrealtime())
     MPROF(0, __builtin_amdgcn_s_memtime())
     MPROF(7, (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
@@ -139,19 +131,8 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
     const int lin = (a.flags & STZS_CONV_LINEAR_IDS) ? blockIdx.y * nx + blockIdx.x
                                                       : xcd_remap(blockIdx.y * nx + blockIdx.x, nx * gridDim.y);
     const int by = lin / nx, bx = lin - by * nx;  // (co tile, utterance x time tile)
-    int bq, tile0, ntile = 1;
-    if constexpr (PT) {  // (co tile, utterance x run of consecutive tiles)
-        const int nruns = nx / a.B;
-        const int nrun = (tpb + nruns - 1) / nruns;
-        bq = bx / nruns;
-        tile0 = (bx - bq * nruns) * nrun;
-        ntile = min(nrun, tpb - tile0);
-        if (ntile <= 0) return;  // (uniform: before any barrier)
-    } else {
-        bq = bx / tpb;
-        tile0 = bx - bq * tpb;
-    }
-    int t0 = tile0 * BT;
+    const int bq = bx / tpb;
+    const int t0 = (bx - bq * tpb) * BT;
     const int nchunk = NCH ? NCH : a.ci_pad >> 7;
     constexpr int SB = BT == 128 ? sb_rows(KS) : sb_rows64(KS);
     // weights: [co tile][chunk][tap][kq][wave][nt][lane][8] bf16 -> 512 bf16x8 per K-step.  Wide form: wave w takes
@@ -206,24 +187,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
     if constexpr (PF) {
         if (!(a.flags & 1)) prefetch(0);
     }
-    // PT: the raw rows of the tile being staged (the first tile's loaded at its staging, later ones under the previous
-    // tile's K loop); clamped addresses, as the EARLY loads below
-    uint4 rawp[PT ? SB : 1];
-    auto load_rows = [&](int tb) {
-        const int cl = cv * 8 < a.Ci ? cv * 8 : 0;
-#pragma unroll
-        for (int i = 0; i < SB; ++i) {
-            int tin = tb - a.pad + rsub + 16 * i;
-            tin = tin < 0 ? 0 : (tin >= a.T_in ? a.T_in - 1 : tin);
-            rawp[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(X) + (unsigned)(tin * (int)a.ldx + cl) * 2u);
-        }
-    };
 
-    for (int tt = 0; tt < ntile; ++tt) {
-    t0 = (tile0 + tt) * BT;
-    // (PT) the weight stream's per-K-step addresses are loop-invariant: hoisted out of the tile loop they would all stay
-    // live across it (k11: 44 K-steps x 2 fragments -> spills); an opaque base per tile keeps them computed in place
-    if constexpr (PT) asm volatile("" : "+v"(Wf));
     for (int cc = 0; cc < nchunk; ++cc) {
         const int kb = cc * NKC;
 #pragma unroll
@@ -242,11 +206,8 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
             // latency per tile instead of two in series (tools/mrfv_phase.py: the staging phase is the longest phase of a
             // stage-1 workgroup).  Clamped addresses for every tile (an interior tile's are unchanged).  The multi-chunk
             // forms keep the old order: raw vectors live across the constants block spill the 256-VGPR wide form.
-            constexpr bool EARLY = NCH == 1 && !PF && !PT;
+            constexpr bool EARLY = NCH == 1 && !PF;
             uint4 rawe[EARLY ? SB : 1];
-            if constexpr (PT) {
-                if (tt == 0) load_rows(t0);
-            }
             if constexpr (EARLY) {
 #pragma unroll
                 for (int i = 0; i < SB; ++i) {
@@ -262,8 +223,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
             }
             // per-channel constants (128 threads):  t = x*ka + kb (revolutions of cos(2 a y)),
             // out = cos(t) * km + (x*ksc + ksh)  [Snake]   or   out = act(x*ksc + ksh)
-            // (PT: once per run -- they live in the rows' pad bytes, which no staging writes)
-            if (tid < 128 && (!PT || tt == 0)) {
+            if (tid < 128) {
                 const int ch = cc * 128 + tid;
                 const bool ok = ch < a.Ci;
                 float sc = 0.f, sh = 0.f;
@@ -301,8 +261,6 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
                 for (int i = 0; i < SB; ++i) {  // 32-bit offsets from the utterance base (SGPR): saddr loads
                     if constexpr (PF) {
                         raw[i] = rawn[i];  // (loaded under the previous chunk's K loop)
-                    } else if constexpr (PT) {
-                        raw[i] = rawp[i];  // (loaded under the previous tile's K loop, or just above)
                     } else if constexpr (EARLY) {
                         raw[i] = rawe[i];  // (loaded ahead of the constants)
                     } else {
@@ -368,9 +326,6 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
         if constexpr (PF) {
             if (cc + 1 < nchunk && !(a.flags & 1)) prefetch(cc + 1);  // the next chunk flies under this K loop
         }
-        if constexpr (PT) {
-            if (tt + 1 < ntile && !(a.flags & 1)) load_rows(t0 + BT);  // the next tile's rows fly under this K loop
-        }
         // K loop: no barrier.  K-step s = tap*4 + kq reads input rows t + tap*dil, channels kq*32 ..
         // FIRST (the first chunk): K-step 0 takes the MFMA's inline-constant 0 as its C operand instead of 64
         // v_mov zeroings of the accumulators (the same sums: 0 + products either way)
@@ -416,7 +371,7 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
         }
     }
     MPROF(2, __builtin_amdgcn_s_memtime())
-    if (a.flags & 4) continue;  // (probe flag: no epilogue)
+    if (a.flags & 4) return;
 
     // ---------------- epilogue: lane (g, n): time t = t0 + mt*16 + n, channels co0 .. co0 + 7
     const int g = lane >> 4, n = lane & 15;
@@ -506,7 +461,6 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
         }
     }
     }
-    }  // (tile run)
 #ifdef STZS_MRFV_PROF
     MPROF(3, __builtin_amdgcn_s_memtime())
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -515,12 +469,12 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? (PT ? STZS_MRFV_OCCP : STZS_MRFV_OC
 #endif
 }
 
-template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1, int BT = 128, bool PT = false>
+template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1, int BT = 128>
 void (*pick_ks(int ks))(stzs_conv_args) {
     switch (ks) {
-        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL, WPW, BT, PT>;
-        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL, WPW, BT, PT>;
-        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH, AL, WPW, BT, PT>;
+        case 3: return mrfv_conv<PACT, HR, HA, 3, NCH, AL, WPW, BT>;
+        case 7: return mrfv_conv<PACT, HR, HA, 7, NCH, AL, WPW, BT>;
+        case 11: return mrfv_conv<PACT, HR, HA, 11, NCH, AL, WPW, BT>;
         default: return nullptr;
     }
 }
@@ -533,5 +487,3 @@ void (*pick_ks(int ks))(stzs_conv_args) {
 // faster so built (profiles/r06e_mrfv_nopk.log), while the wide stage-0 forms (256 VGPRs) lose 7 % and keep them
 using mrfv_kfn = void (*)(stzs_conv_args);
 mrfv_kfn stzs_mrfv_pick_n1(int ks, bool hr, bool ha, bool al, bool t64);
-// the tile-run (PT) forms of the same instances (csrc/mrfv_n1p.hip, also without packed fp32)
-mrfv_kfn stzs_mrfv_pick_n1_run(int ks, bool hr, bool ha, bool al);
