@@ -22,11 +22,11 @@ __global__ __launch_bounds__(256) void attn_x3(const stzs_attn_args a) {
     constexpr int NKS = DH / 32;
     constexpr int NDT = DH / 16;
     constexpr int KP = DH + 8;
-    constexpr int VP = KC + 8;
-    constexpr int PP = KC + 8;
+    constexpr int VP = DH + 8;  // V rows, row-major: the PV fragments by transposed reads (attn_body.hpp frag_tr)
+    constexpr int PTP = 16 + 4;  // P^T [key][query] per wave
     __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KC * KP];
-    __shared__ __attribute__((aligned(16))) bf16_t Vt[2][DH * VP];
-    __shared__ __attribute__((aligned(16))) bf16_t Ps[2][4][16 * PP];
+    __shared__ __attribute__((aligned(16))) bf16_t Vs[2][KC * VP];
+    __shared__ __attribute__((aligned(16))) bf16_t Ps[2][4][KC * PTP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long r = blockIdx.x;
     const int h = blockIdx.y;
@@ -82,15 +82,8 @@ __global__ __launch_bounds__(256) void attn_x3(const stzs_attn_args a) {
             split8(vf, vh, vl);
             *reinterpret_cast<bf16x8*>(&Ks[0][kr * KP + cv * 8]) = kh;
             *reinterpret_cast<bf16x8*>(&Ks[1][kr * KP + cv * 8]) = kl;
-            const uint4 uh = __builtin_bit_cast(uint4, vh), ul = __builtin_bit_cast(uint4, vl);
-            const uint32_t wh[4] = {uh.x, uh.y, uh.z, uh.w}, wl[4] = {ul.x, ul.y, ul.z, ul.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                Vt[0][(cv * 8 + 2 * j) * VP + kr] = (bf16_t)(wh[j] & 0xFFFF);
-                Vt[0][(cv * 8 + 2 * j + 1) * VP + kr] = (bf16_t)(wh[j] >> 16);
-                Vt[1][(cv * 8 + 2 * j) * VP + kr] = (bf16_t)(wl[j] & 0xFFFF);
-                Vt[1][(cv * 8 + 2 * j + 1) * VP + kr] = (bf16_t)(wl[j] >> 16);
-            }
+            *reinterpret_cast<bf16x8*>(&Vs[0][kr * VP + cv * 8]) = vh;
+            *reinterpret_cast<bf16x8*>(&Vs[1][kr * VP + cv * 8]) = vl;
         }
         __syncthreads();
         f32x4 s[4];
@@ -107,56 +100,60 @@ __global__ __launch_bounds__(256) void attn_x3(const stzs_attn_args a) {
                 s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[ks], kh, s[nt], 0, 0, 0);
             }
         }
-        float alpha[4];
+        float alpha[4], mx[4], sum[4];  // (the row reductions on DPP, as attn_body.hpp)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            float mx = -INFINITY;
+            mx[i] = -INFINITY;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
                 const bool ok = c0 + nt * 16 + (lane & 15) < a.Lk;
                 s[nt][i] = ok ? s[nt][i] * scale : -INFINITY;
-                mx = fmaxf(mx, s[nt][i]);
+                mx[i] = fmaxf(mx[i], s[nt][i]);
             }
+        }
+        stzs_attn::row16_max4(mx);
 #pragma unroll
-            for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-            const float mn = fmaxf(m[i], mx);
+        for (int i = 0; i < 4; ++i) {
+            const float mn = fmaxf(m[i], mx[i]);
             alpha[i] = expf(m[i] - mn);
-            float sum = 0.f;
+            sum[i] = 0.f;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
                 const float pv = expf(s[nt][i] - mn);
                 s[nt][i] = pv;
-                sum += pv;
+                sum[i] += pv;
             }
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
-            l[i] = l[i] * alpha[i] + sum;
             m[i] = mn;
         }
+        stzs_attn::row16_sum4(sum);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) l[i] = l[i] * alpha[i] + sum[i];
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
             for (int i = 0; i < 4; ++i) o[dt][i] *= alpha[i];
+        // P (split) -> P^T images, one 8-B store per key tile and image; A fragments by transposed reads
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
+        for (int nt = 0; nt < 4; ++nt) {
+            float hf[4], lf[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int pi = ((lane >> 4) * 4 + i) * PP + nt * 16 + (lane & 15);
-                const bf16_t ph = f2bf(s[nt][i]);
-                Ps[0][wave][pi] = ph;
-                Ps[1][wave][pi] = f2bf(s[nt][i] - bf2f(ph));
+                hf[i] = bf2f(f2bf(s[nt][i]));
+                lf[i] = s[nt][i] - hf[i];
             }
+            const int pi = (nt * 16 + (lane & 15)) * PTP + 4 * (lane >> 4);
+            *reinterpret_cast<uint2*>(&Ps[0][wave][pi]) = make_uint2(pack2bf(hf[0], hf[1]), pack2bf(hf[2], hf[3]));
+            *reinterpret_cast<uint2*>(&Ps[1][wave][pi]) = make_uint2(pack2bf(lf[0], lf[1]), pack2bf(lf[2], lf[3]));
+        }
         __syncthreads();
 #pragma unroll
         for (int ks = 0; ks < KC / 32; ++ks) {
-            const int po = (lane & 15) * PP + ks * 32 + 8 * (lane >> 4);
-            const bf16x8 ph = *reinterpret_cast<const bf16x8*>(&Ps[0][wave][po]);
-            const bf16x8 pl = *reinterpret_cast<const bf16x8*>(&Ps[1][wave][po]);
+            const bf16x8 ph = stzs_attn::frag_tr(Ps[0][wave], PTP, ks * 32, 0, lane);
+            const bf16x8 pl = stzs_attn::frag_tr(Ps[1][wave], PTP, ks * 32, 0, lane);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) {
-                const int vo = (dt * 16 + (lane & 15)) * VP + ks * 32 + 8 * (lane >> 4);
-                const bf16x8 vh = *reinterpret_cast<const bf16x8*>(&Vt[0][vo]);
-                const bf16x8 vl = *reinterpret_cast<const bf16x8*>(&Vt[1][vo]);
+                const bf16x8 vh = stzs_attn::frag_tr(Vs[0], VP, ks * 32, dt * 16, lane);
+                const bf16x8 vl = stzs_attn::frag_tr(Vs[1], VP, ks * 32, dt * 16, lane);
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vh, o[dt], 0, 0, 0);
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vl, o[dt], 0, 0, 0);
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vh, o[dt], 0, 0, 0);

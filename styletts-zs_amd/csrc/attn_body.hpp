@@ -15,14 +15,57 @@ namespace stzs_attn {
 
 constexpr int KC = 64;  // keys per chunk
 
+template <int CTRL>
+STZS_DEV float dpp16(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+// x[i] reduced over the 16 lanes of each DPP row, the four values step-major (independent DPP reads between dependent
+// ones); every lane of the row gets the result
+STZS_DEV void row16_max4(float* x) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = fmaxf(x[i], dpp16<0xB1>(x[i]));  // quad_perm 1,0,3,2
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = fmaxf(x[i], dpp16<0x4E>(x[i]));  // quad_perm 2,3,0,1
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = fmaxf(x[i], dpp16<0x141>(x[i]));  // row_half_mirror
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = fmaxf(x[i], dpp16<0x140>(x[i]));  // row_mirror
+}
+STZS_DEV void row16_sum4(float* x) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] += dpp16<0xB1>(x[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] += dpp16<0x4E>(x[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] += dpp16<0x141>(x[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] += dpp16<0x140>(x[i]);
+}
+
 template <int DH>
 struct Lds {
     static constexpr int KP = DH + 8;  // K row pitch (bf16)
-    static constexpr int VP = KC + 8;  // V^T row pitch
-    static constexpr int PP = KC + 8;  // P row pitch
-    static constexpr int K_ELEMS = KC * KP, V_ELEMS = DH * VP, P_ELEMS = 4 * 16 * PP;
+    static constexpr int VP = DH + 8;  // V row pitch (row-major: the PV B fragments by transposed reads)
+    static constexpr int PTP = 16 + 4;  // P^T row pitch (a wave's [64 keys][16 queries], 8-B aligned rows)
+    static constexpr int K_ELEMS = KC * KP, V_ELEMS = KC * VP, P_ELEMS = 4 * KC * PTP;
     static constexpr int BYTES = 2 * (K_ELEMS + V_ELEMS + P_ELEMS);
 };
+
+typedef short stzs_v4s __attribute__((ext_vector_type(4)));
+// gfx950 ds_read_b64_tr_b16: per 16-lane group a 4-row x 16-column block of 16-bit elements, lane 4q+p addressing
+// row q, columns 4p..4p+3; lane i receives column i of the 4 rows (row q in element q) -- cdna_hip_programming.md T10
+STZS_DEV uint2 ld_tr16(const bf16_t* p) {
+    const stzs_v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) stzs_v4s*)(p));
+    return __builtin_bit_cast(uint2, v);
+}
+// the 16x16x32 MFMA operand whose lane (n, g) holds elements [k0 + 8g + j][c0 + n], j < 8, of a row-major [k][c] LDS
+// image with pitch `ld` (two transposed reads: rows k0 + 8g + 0..3 and + 4..7).  EXEC must be full.
+STZS_DEV bf16x8 frag_tr(const bf16_t* img, int ld, int k0, int c0, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const bf16_t* a = img + (k0 + 8 * g + q) * ld + c0 + 4 * p;
+    const uint2 lo = ld_tr16(a), hi = ld_tr16(a + 4 * ld);
+    return __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
 
 // operands written by earlier launches
 struct LdPlain {
@@ -37,10 +80,10 @@ STZS_DEV void attn_unit(const stzs_attn_args& a, long r, int h, int qb0, unsigne
     using LY = Lds<DH>;
     constexpr int NKS = DH / 32;  // k-steps of S
     constexpr int NDT = DH / 16;  // d tiles of O
-    constexpr int KP = LY::KP, VP = LY::VP, PP = LY::PP;
+    constexpr int KP = LY::KP, VP = LY::VP, PTP = LY::PTP;
     bf16_t* Ks = reinterpret_cast<bf16_t*>(lds);
-    bf16_t* Vt = Ks + LY::K_ELEMS;
-    bf16_t* Ps = Vt + LY::V_ELEMS;
+    bf16_t* Vs = Ks + LY::K_ELEMS;
+    bf16_t* Ps = Vs + LY::V_ELEMS;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int qb = qb0 + wave * 16;
     const bf16_t* Q = reinterpret_cast<const bf16_t*>(a.q) + r * a.bsq + h * DH;
@@ -64,7 +107,7 @@ STZS_DEV void attn_unit(const stzs_attn_args& a, long r, int h, int qb0, unsigne
         m[i] = -INFINITY;
         l[i] = 0.f;
     }
-    bf16_t* P = Ps + wave * 16 * PP;
+    bf16_t* Pt = Ps + wave * KC * PTP;  // this wave's P^T [key][query]
 
     // K / V chunk loads run one chunk ahead in registers: chunk c + 1's global loads are in flight while chunk c
     // is computed (cross-attention: 3 chunks of 64 keys), the LDS images are written from the registers
@@ -86,19 +129,14 @@ STZS_DEV void attn_unit(const stzs_attn_args& a, long r, int h, int qb0, unsigne
     load_chunk(0);
     for (int c0 = 0; c0 < a.Lk; c0 += KC) {
         __syncthreads();
-        // stage K rows and V^T for keys [c0, c0 + KC) from the registers, then start the next chunk's loads
+        // stage K and V rows for keys [c0, c0 + KC) from the registers (both row-major: V's PV fragments come from
+        // transposed reads, r06 -- it was a scalar transposing store), then start the next chunk's loads
 #pragma unroll
         for (int j = 0; j < NLD; ++j) {
             const int i = tid + j * 256;
             const int kr = i / (DH / 8), cv = i - kr * (DH / 8);
-            const uint4 kv = pk[j], vv = pv[j];
-            *reinterpret_cast<uint4*>(Ks + kr * KP + cv * 8) = kv;
-            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                Vt[(cv * 8 + 2 * q) * VP + kr] = (bf16_t)(w[q] & 0xFFFF);
-                Vt[(cv * 8 + 2 * q + 1) * VP + kr] = (bf16_t)(w[q] >> 16);
-            }
+            *reinterpret_cast<uint4*>(Ks + kr * KP + cv * 8) = pk[j];
+            *reinterpret_cast<uint4*>(Vs + kr * VP + cv * 8) = pv[j];
         }
         if (c0 + KC < a.Lk) load_chunk(c0 + KC);
         __syncthreads();
@@ -113,49 +151,56 @@ STZS_DEV void attn_unit(const stzs_attn_args& a, long r, int h, int qb0, unsigne
                 s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, s[nt], 0, 0, 0);
             }
         }
-        // online softmax; element (row = (lane>>4)*4 + i, key = nt*16 + (lane & 15))
-        float alpha[4];
+        // online softmax; element (row = (lane>>4)*4 + i, key = nt*16 + (lane & 15)).  The 16-lane row max / sum run
+        // on DPP (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror, row_mirror) instead of xor shuffles through
+        // ds_bpermute: after the two quad steps every lane of a quad holds the same value, so the mirror partners
+        // contribute exactly what the xor-4 / xor-8 partners did -- the same bits, at VALU latency (r06)
+        float alpha[4], mx[4], sum[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            float mx = -INFINITY;
+            mx[i] = -INFINITY;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
                 const bool ok = c0 + nt * 16 + (lane & 15) < a.Lk;
                 s[nt][i] = ok ? s[nt][i] * scale : -INFINITY;
-                mx = fmaxf(mx, s[nt][i]);
+                mx[i] = fmaxf(mx[i], s[nt][i]);
             }
+        }
+        row16_max4(mx);
 #pragma unroll
-            for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-            const float mn = fmaxf(m[i], mx);
+        for (int i = 0; i < 4; ++i) {
+            const float mn = fmaxf(m[i], mx[i]);
             alpha[i] = __expf(m[i] - mn);
-            float sum = 0.f;
+            sum[i] = 0.f;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
                 const float pv = __expf(s[nt][i] - mn);
                 s[nt][i] = pv;
-                sum += pv;
+                sum[i] += pv;
             }
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
-            l[i] = l[i] * alpha[i] + sum;
             m[i] = mn;
         }
+        row16_sum4(sum);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) l[i] = l[i] * alpha[i] + sum[i];
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
             for (int i = 0; i < 4; ++i) o[dt][i] *= alpha[i];
-        // P -> LDS (C layout) -> A fragments
+        // P -> LDS as P^T (lane (n, g) holds queries 4g..4g+3 of key nt*16 + n: one 8-B store per key tile) -> A
+        // fragments by transposed reads (lane (n, g): query n, keys ks*32 + 8g + j); the same bf16 values as before
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) P[((lane >> 4) * 4 + i) * PP + nt * 16 + (lane & 15)] = f2bf(s[nt][i]);
+        for (int nt = 0; nt < 4; ++nt) {
+            const uint2 pq = make_uint2(pack2bf(s[nt][0], s[nt][1]), pack2bf(s[nt][2], s[nt][3]));
+            *reinterpret_cast<uint2*>(Pt + (nt * 16 + (lane & 15)) * PTP + 4 * (lane >> 4)) = pq;
+        }
         __syncthreads();
 #pragma unroll
         for (int ks = 0; ks < KC / 32; ++ks) {
-            const bf16x8 pf = *reinterpret_cast<const bf16x8*>(P + (lane & 15) * PP + ks * 32 + 8 * (lane >> 4));
+            const bf16x8 pf = frag_tr(Pt, PTP, ks * 32, 0, lane);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) {
-                const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vt + (dt * 16 + (lane & 15)) * VP + ks * 32 + 8 * (lane >> 4));
+                const bf16x8 vf = frag_tr(Vs, VP, ks * 32, dt * 16, lane);
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[dt], 0, 0, 0);
             }
         }
