@@ -116,14 +116,41 @@ STZS_DEV float act_apply(int act, float x, float slope, float alpha) {
     }
 }
 
+// Cross-lane butterflies without ds_bpermute (r06).  xor 32 / xor 16: v_permlane32_swap / v_permlane16_swap with both
+// operands = v (lanes 32-63 of one copy trade places with lanes 0-31 of the other, resp. the odd 16-lane rows with the
+// even ones), whose two results are {own, partner} in some order -- their sum / max is the xor partner's, bit for bit
+// (commutative).  xor 8 / 4 / 2 / 1 after those: DPP row rotations (row_ror 8 is xor 8; after it every value has period
+// 8 within its row, so row_ror 4 fetches the xor-4 partner's value, likewise 2 and 1).  Same bits as the xor shuffles.
+template <int CTRL>
+STZS_DEV float dpp_f32(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+STZS_DEV float xor32_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+STZS_DEV float xor16_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 STZS_DEV float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v = xor32_sum(v);
+    v = xor16_sum(v);
+    v += dpp_f32<0x128>(v);  // row_ror:8
+    v += dpp_f32<0x124>(v);
+    v += dpp_f32<0x122>(v);
+    v += dpp_f32<0x121>(v);
     return v;
 }
 STZS_DEV float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    v = fmaxf(v, dpp_f32<0x128>(v));
+    v = fmaxf(v, dpp_f32<0x124>(v));
+    v = fmaxf(v, dpp_f32<0x122>(v));
+    v = fmaxf(v, dpp_f32<0x121>(v));
     return v;
 }
 

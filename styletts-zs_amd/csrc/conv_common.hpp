@@ -159,10 +159,8 @@ STZS_DEV void epilogue(const stzs_conv_args& a, const float* ep, const float* c_
     auto stat_flush = [&](int half) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            st_s[j] += __shfl_xor(st_s[j], 16, 64);
-            st_s[j] += __shfl_xor(st_s[j], 32, 64);
-            st_q[j] += __shfl_xor(st_q[j], 16, 64);
-            st_q[j] += __shfl_xor(st_q[j], 32, 64);
+            st_s[j] = xor32_sum(xor16_sum(st_s[j]));  // (common.hpp: the xor-16 / xor-32 shuffles' bits)
+            st_q[j] = xor32_sum(xor16_sum(st_q[j]));
         }
         const int wv = tid >> 6;
         if ((tid & 63) < 16) {

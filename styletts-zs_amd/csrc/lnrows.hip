@@ -22,10 +22,14 @@ namespace {
 
 constexpr int LR_ROWS = 16;  // rows per workgroup (one 16-row MFMA tile; 4 rows per wave in the LayerNorm)
 
-// sum over the 16 lanes of a lane group (xor 8, 4, 2, 1)
+// sum over the 16 lanes of a lane group: the xor-8, 4, 2, 1 butterfly on DPP row rotations (r06; it ran on ds_bpermute
+// shuffles).  After the xor-8 step every value has period 8 within the row (x_j + x_(j^8) == x_(j^8) + x_j bitwise),
+// so rotating by 4 fetches exactly the xor-4 partner's value, and likewise by 2 and 1: the same bits as the shuffles.
 STZS_DEV float sum16(float v) {
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v += dpp_f32<0x128>(v);  // row_ror:8 (= xor 8)
+    v += dpp_f32<0x124>(v);  // row_ror:4
+    v += dpp_f32<0x122>(v);  // row_ror:2
+    v += dpp_f32<0x121>(v);  // row_ror:1
     return v;
 }
 
