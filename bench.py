@@ -297,12 +297,13 @@ def stage_roofline(eng, S, tok_d, ref_d, eps_d, dur_d, seeds, n_frames):
                 stages=out, families=fams, top_tags=top)
 
 
-def precise_mode(S, P, dev, B=64, steps=5, nstream=2, stagger=1):
+def precise_mode(S, P, dev, B=64, steps=5, nstream=2, stagger=1, schedule="pipe"):
     """throughput of the PRECISE mode -- the whole pipeline (text encoder, style diffusion, predictor, decoder) on
     fp32 activations and split-operand bf16x3 products, the mode that meets the north-star log-mel L1 <= 1e-3
     END TO END (tests/test_gpu_precise.py: 4.2e-4 at configs[1]) -- on the throughput workload (batch 64, 5-s
-    targets, 2-step CFG 5): replayed as the main leg is, `nstream` shards on their own streams (shard_runner), and as one graph
-    on one stream beside it."""
+    targets, 2-step CFG 5): replayed as the main leg is (schedule "pipe": pipe_runner, the front of batch i + 1 beside
+    the decoder of batch i; "shards": `nstream` shards on their own streams, shard_runner), and as one graph on one
+    stream beside it."""
     from stzs.engine import StyleTTSZS
     ep = StyleTTSZS(S, P, device=dev, precise=True)
     host_src = make_inputs(S, B, 7)
@@ -322,7 +323,11 @@ def precise_mode(S, P, dev, B=64, steps=5, nstream=2, stagger=1):
     torch.cuda.synchronize()
     el1 = (time.perf_counter() - t0) / steps
     del g
-    run_steps, twins, _ = shard_runner(ep, S, dev, tok, ref, eps, dur, seeds, nf, nstream, stagger, None, host_src, nwav)
+    if schedule == "pipe":
+        run_steps, twins, _ = pipe_runner(ep, S, dev, tok, ref, eps, dur, seeds, nf, None, host_src, nwav)
+    else:
+        run_steps, twins, _ = shard_runner(ep, S, dev, tok, ref, eps, dur, seeds, nf, nstream, stagger, None, host_src,
+                                           nwav)
     run_steps(1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -336,8 +341,9 @@ def precise_mode(S, P, dev, B=64, steps=5, nstream=2, stagger=1):
     del run_steps, twins, ep
     torch.cuda.empty_cache()
     return dict(config=f"batch {B}, 5-s targets, 2-step CFG-5, precise mode (fp32 activations, split-operand "
-                       f"bf16x3 convs / linears / LSTM / attention in every stage); {nstream} shards on {nstream} "
-                       f"streams (stagger {stagger})",
+                       f"bf16x3 convs / linears / LSTM / attention in every stage); " +
+                       ("front of batch i + 1 beside the decoder of batch i (pipe_runner)" if schedule == "pipe" else
+                        f"{nstream} shards on {nstream} streams (stagger {stagger})"),
                 audio_s_per_s=round(B * TARGET_S / el, 1), ms_per_step=round(el * 1e3, 2),
                 single_stream_audio_s_per_s=round(B * TARGET_S / el1, 1), lstm_status=lstm_to, stages=st)
 
@@ -431,6 +437,75 @@ def shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstre
     return run_steps, twins, host
 
 
+def pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, pidx, host_src, nwav, nback=1,
+                steps=STEPS_THROUGHPUT, cfg=CFG):
+    """the per-GPU batch as a two-stage pipeline: the front graph (text, prompt, style diffusion, prosody) of the WHOLE
+    batch on one stream, the back graphs (decoder; `nback` utterance shards, each on its own stream) on others, so batch
+    i's decoder runs beside batch i + 1's front (the latency-bound recurrences and small GEMMs of the front fill what
+    the decoder convs leave).  Two front twins and two sets of back twins alternate by step parity (front i + 2 waits
+    for every back of step i, the readers of its outputs).  Every step is one front + the backs of the full batch; the
+    first front of a timed run is not overlapped (pipeline fill).  Host-to-host steps: the inputs go in on the front
+    stream before each front, each back shard's waveform comes out on its stream after it.
+    -> (run_steps(k, h2h=False), twins, host buffers {tok, ref, eps, dur, wav} (pinned))"""
+    B = tok_d.shape[0]
+    sizes = [B // nback + (1 if i < B % nback else 0) for i in range(nback)]
+    offs = [sum(sizes[:j]) for j in range(nback)]
+    fr, st, twins, graphs = [eng.twin(), eng.twin()], [{}, {}], [], []
+    for p in range(2):
+        def front(tw=fr[p], s=st[p]):
+            h, pr = tw.encode_inputs(tok_d, ref_d, pidx)
+            codes = tw.sample_style(h, pr, eps_d, steps, cfg)
+            s["codes"], s["pro"] = codes, tw.predict_prosody(h, codes, dur_d, n_frames)
+        front()
+        backs = []
+        for j in range(nback):
+            tw, b0, nb = eng.twin(), offs[j], sizes[j]
+            twins.append(tw)
+
+            def back(tw=tw, s=st[p], b0=b0, nb=nb):
+                pro = s["pro"]
+                if nb < B:  # this shard's utterances of the front's outputs
+                    pro = dict(pro, asr_buf=pro["asr_buf"].rows(b0, nb), F0=pro["F0"][b0:b0 + nb],
+                               N=pro["N"][b0:b0 + nb])
+                return tw.decode(pro, s["codes"][b0:b0 + nb], seeds[b0:b0 + nb])
+            back()
+            gb, wv = tw.capture(back)
+            backs.append((gb, wv, b0, nb))
+        ga = fr[p].capture(front)[0]
+        graphs.append((ga, backs))
+    sF, sD = torch.cuda.Stream(dev), [torch.cuda.Stream(dev) for _ in range(nback)]
+    host = dict(zip(("tok", "ref", "eps", "dur"), (t.pin_memory() for t in host_src)))
+    host["wav"] = torch.empty(B, nwav, dtype=torch.float32).pin_memory()
+
+    def run_steps(k, h2h=False):
+        cur = torch.cuda.current_stream(dev)
+        for x in [sF] + sD:
+            x.wait_stream(cur)
+        fdone = [torch.cuda.Event() for _ in range(k)]
+        bdone = [[torch.cuda.Event() for _ in range(nback)] for _ in range(k)]
+        for i in range(k):
+            ga, backs = graphs[i & 1]
+            with torch.cuda.stream(sF):
+                if i >= 2:  # this twin's codes / prosody were read by the backs of step i - 2
+                    for e in bdone[i - 2]:
+                        sF.wait_event(e)
+                if h2h:
+                    for d_, h_ in ((tok_d, host["tok"]), (ref_d, host["ref"]), (eps_d, host["eps"]), (dur_d, host["dur"])):
+                        d_.copy_(h_, non_blocking=True)
+                ga.replay()
+                fdone[i].record(sF)
+            for j, (gb, wv, b0, nb) in enumerate(backs):
+                with torch.cuda.stream(sD[j]):
+                    sD[j].wait_event(fdone[i])
+                    gb.replay()
+                    if h2h:
+                        host["wav"][b0:b0 + nb].copy_(wv, non_blocking=True)
+                    bdone[i][j].record(sD[j])
+        for x in [sF] + sD:
+            cur.wait_stream(x)
+    return run_steps, fr + twins, host
+
+
 def _free_port():
     import socket
     with socket.socket() as so:
@@ -517,6 +592,12 @@ def main():
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage roofline pass")
     ap.add_argument("--streams", type=int, default=4,
                     help="split the per-GPU batch over this many concurrently replayed graphs (engine twins)")
+    ap.add_argument("--schedule", choices=("shards", "pipe"), default="pipe",
+                    help="shards: --streams concurrent front+back graphs of batch shards (shard_runner); pipe: the whole "
+                         "batch's front beside the previous batch's decoder (pipe_runner)")
+    ap.add_argument("--pipe-backs", type=int, default=1, help="--schedule pipe: decoder shards (streams) per step")
+    ap.add_argument("--precise-schedule", choices=("shards", "pipe"), default="pipe",
+                    help="the precise leg's schedule (shards: 2 shards, stagger 1)")
     ap.add_argument("--stagger", type=int, default=2,
                     help="1: shards j > 0 start one front phase late; 2: shard j starts after shard j - 1's first front")
     ap.add_argument("--branch-streams", default="0",
@@ -600,7 +681,13 @@ def main():
     run = graph.replay if graph is not None else step
     nstream = min(args.streams, B) if (graph is not None and args.streams > 1) else 1
     twins = [eng]
-    if nstream > 1:
+    pipe = graph is not None and args.schedule == "pipe"
+    if pipe:
+        nstream = 1 + args.pipe_backs
+        run_steps, tws, host = pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, pidx,
+                                           (tok, ref, eps, dur), out["wav"].shape[1], nback=args.pipe_backs)
+        twins += tws
+    elif nstream > 1:
         run_steps, tws, host = shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstream,
                                             int(args.stagger), pidx, (tok, ref, eps, dur), out["wav"].shape[1])
         twins += tws
@@ -733,7 +820,8 @@ def main():
         lstm_timeouts += lf.pop("lstm_timeouts")
     pr = None
     if not args.no_precise and world == 1:
-        pr = precise_mode(S, P, dev)  # 2 shards: 4 measured slower in the fp32-activation mode (r05_j 6 491 vs 7 756)
+        # (shards: 2 -- 4 measured slower in the fp32-activation mode, r05_j 6 491 vs 7 756)
+        pr = precise_mode(S, P, dev, schedule=args.precise_schedule)
         lstm_timeouts += int(pr["lstm_status"] != 0)
 
     cpu = None
@@ -761,7 +849,8 @@ def main():
             "config": {"workload": "configs[2]: batch 64/GPU, 5-s targets, 2-step distilled style diffusion, CFG 5",
                        "global_batch": world * B, "seq_len": n_frames, "parallelism": f"dp{world} (utterance shards)",
                        "spec": S.name, "graph": graph is not None, "branch_streams": bs if isinstance(bs, bool) else sorted(bs), "streams": nstream,
-                       "stagger": int(args.stagger) if nstream > 1 else 0, "shared_speaker": bool(args.shared_speaker)},
+                       "schedule": "pipe" if pipe else ("shards" if nstream > 1 else "one"),
+                       "stagger": int(args.stagger) if nstream > 1 and not pipe else 0, "shared_speaker": bool(args.shared_speaker)},
             "audio_s_per_s_per_gpu": round(value / world, 2),
             "latency": lat,
             "roofline": roof,

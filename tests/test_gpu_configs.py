@@ -300,6 +300,32 @@ def test_bench_shard_runner_matches_eager(v0, c2, nstream, stagger):
     assert ok1 and ok3
 
 
+@pytest.mark.parametrize("nback", [1, 2])
+def test_bench_pipe_runner_matches_eager(v0, c2, nback):
+    """bench.pipe_runner, the headline schedule since r06: the whole batch's front graph on one stream, the previous
+    batch's decoder (`nback` utterance shards) on others, two twin sets alternating by step parity, host-to-host copies
+    on the front / back streams -> every waveform the same bits as the eager single-stream batch, after device-resident
+    steps and after host-to-host steps (odd and even step counts: both twin sets)."""
+    S, P, eng = v0
+    (tok, ref, eps, dur, seeds), g = c2
+    dev = eng.device
+    tok_d, ref_d, eps_d, dur_d = (t.to(dev) for t in (tok, ref, eps, dur))
+    run_steps, tws, host = bench.pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, int(dur[0].sum()), None,
+                                             (tok, ref, eps, dur), g["wav"].shape[1], nback=nback)
+    run_steps(3)
+    run_steps(1, h2h=True)
+    torch.cuda.synchronize()
+    ok1 = torch.equal(host["wav"], g["wav"])
+    host["wav"].zero_()
+    run_steps(4, h2h=True)
+    torch.cuda.synchronize()
+    ok4 = torch.equal(host["wav"], g["wav"])
+    st = [tw.check_status() for tw in tws]
+    print(f"pipe, {nback} decoder shard(s): h2h x1 {ok1}, h2h x4 {ok4}, max |dwav| "
+          f"{(host['wav'] - g['wav']).abs().max().item():.3e}, status {st}")
+    assert ok1 and ok4
+
+
 def test_latency_engine_batch_invariant(v0):
     """the latency engine (whole-chip small-M denoiser linears, split-K) keeps utterances independent: three
     utterances synthesized as one batch == each synthesized alone, bit for bit (the K structure of every linear is a
