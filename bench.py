@@ -438,7 +438,7 @@ def shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstre
 
 
 def pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, pidx, host_src, nwav, nback=1,
-                steps=STEPS_THROUGHPUT, cfg=CFG, cut="dec"):
+                steps=STEPS_THROUGHPUT, cfg=CFG):
     """the per-GPU batch as a two-stage pipeline: the front graph (text, prompt, style diffusion, prosody) of the WHOLE
     batch on one stream, the back graphs (decoder; `nback` utterance shards, each on its own stream) on others, so batch
     i's decoder runs beside batch i + 1's front (the latency-bound recurrences and small GEMMs of the front fill what
@@ -446,10 +446,9 @@ def pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, pidx, 
     for every back of step i, the readers of its outputs).  Every step is one front + the backs of the full batch; the
     first front of a timed run is not overlapped (pipeline fill).  Host-to-host steps: the inputs go in on the front
     stream before each front, each back shard's waveform comes out on its stream after it.
-    cut: where the front ends -- "dec": before the decoder (prosody out); "gen": before the generator (the decoder
-    pre-blocks and the harmonic source in the front; nback = 1 only).
+    The front ends at the prosody: moving the decoder pre-blocks + harmonic source into it measured slower (18.3k vs
+    19.2k audio-s/s), the harmonic source alone flat (profiles/r06y, r06z).
     -> (run_steps(k, h2h=False), twins, host buffers {tok, ref, eps, dur, wav} (pinned))"""
-    assert cut == "dec" or nback == 1
     B = tok_d.shape[0]
     sizes = [B // nback + (1 if i < B % nback else 0) for i in range(nback)]
     offs = [sum(sizes[:j]) for j in range(nback)]
@@ -459,9 +458,6 @@ def pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, pidx, 
             h, pr = tw.encode_inputs(tok_d, ref_d, pidx)
             codes = tw.sample_style(h, pr, eps_d, steps, cfg)
             s["codes"], s["pro"] = codes, tw.predict_prosody(h, codes, dur_d, n_frames)
-            if cut == "gen":
-                s["gen"] = tw.decoder_pre(s["pro"], codes)
-                s["har"] = tw.sine_gen(s["pro"]["F0"], seeds)
         front()
         backs = []
         for j in range(nback):
@@ -469,9 +465,6 @@ def pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, pidx, 
             twins.append(tw)
 
             def back(tw=tw, s=st[p], b0=b0, nb=nb):
-                if cut == "gen":
-                    (gen_in, gbd), har = s["gen"], s["har"]
-                    return tw.generator(gen_in, s["pro"]["F0"], seeds, gbd, har=har)
                 pro = s["pro"]
                 if nb < B:  # this shard's utterances of the front's outputs
                     pro = dict(pro, asr_buf=pro["asr_buf"].rows(b0, nb), F0=pro["F0"][b0:b0 + nb],
@@ -607,8 +600,6 @@ def main():
                     help="shards: --streams concurrent front+back graphs of batch shards (shard_runner); pipe: the whole "
                          "batch's front beside the previous batch's decoder (pipe_runner)")
     ap.add_argument("--pipe-backs", type=int, default=1, help="--schedule pipe: decoder shards (streams) per step")
-    ap.add_argument("--pipe-cut", choices=("dec", "gen"), default="dec",
-                    help="--schedule pipe: the front ends before the decoder (dec) or before the generator (gen)")
     ap.add_argument("--precise-schedule", choices=("shards", "pipe"), default="pipe",
                     help="the precise leg's schedule (shards: 2 shards, stagger 1)")
     ap.add_argument("--stagger", type=int, default=2,
@@ -698,8 +689,7 @@ def main():
     if pipe:
         nstream = 1 + args.pipe_backs
         run_steps, tws, host = pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, pidx,
-                                           (tok, ref, eps, dur), out["wav"].shape[1], nback=args.pipe_backs,
-                                           cut=args.pipe_cut)
+                                           (tok, ref, eps, dur), out["wav"].shape[1], nback=args.pipe_backs)
         twins += tws
     elif nstream > 1:
         run_steps, tws, host = shard_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, nstream,
