@@ -659,6 +659,8 @@ size_t stzs_denoiser_fwd_workspace(const stzs_tensor_t* inputs, int n_in, const 
  *     stride), codes f32 [B, L_s, code], F0 conv f32 [4] (w0 w1 w2 bias), N conv f32 [4], asr_res w, b, AdaIN norm
  *     group w [total x style_ac], b, then 5 blocks (encode, decode0..3) x 7: conv1 w, conv1 b, conv2 w, conv2 b,
  *     sc w (data NULL when din == dout), pool w f32 [din x 3], pool b f32 [din] (decode3 only, else NULL)} ->
+ *     [the block convs packed STZS_PACK_FRAG32 when din > 64 and Co % 32 == 0 (conv1, conv2 and the 1x1 shortcut),
+ *     else conv1 / conv2 STZS_PACK_LANE16 when Co % 16 == 0 and STZS_PACK_KSTEP otherwise -- stzs/weights.py pack_blk]
  *     out {generator input bf16 [B, T80, >= dec_out]}; i[0] = dec_enc, i[1] = dec_asr_res, i[2] = dec_out,
  *     i[3] = style_ac (acoustic code channels pooled for AdaIN), i[4] = columns of the norm group (its first ones:
  *     norm1 | norm2 gamma-beta of the 5 blocks in order).  (stzs/engine.py decoder_pre) */

@@ -48,8 +48,9 @@ extern "C" size_t stzs_pack_conv_size(int Co, int Ci, int ks, int ups, int form)
     switch (form) {
         case STZS_PACK_KSTEP: return (size_t)g.ks * g.co_pad * g.ci_pad * 2;
         case STZS_PACK_LANE16: return (g.cic == 128 && Co % 16 == 0) ? (size_t)g.ks * g.co_pad * g.ci_pad * 2 : 0;
-        case STZS_PACK_FRAG32:  // MRF convs (k 3 / 7 / 11) and the polyphase ConvTranspose (csrc/ups.hip)
-            return (g.cic == 128 && (ups ? Co % 32 == 0 : (Co % 8 == 0 && (ks == 3 || ks == 7 || ks == 11))))
+        case STZS_PACK_FRAG32:  // MRF / AdaIN-block convs (k 3 / 7 / 11), the blocks' 1x1 shortcuts, the polyphase
+                                // ConvTranspose (csrc/ups.hip)
+            return (g.cic == 128 && (ups ? Co % 32 == 0 : (Co % 8 == 0 && (ks == 1 || ks == 3 || ks == 7 || ks == 11))))
                        ? (size_t)g.ks * g.co_pad * g.ci_pad * 2 : 0;
         case STZS_PACK_NARROW32: return (!ups && g.cic == 128 && Co <= 32) ? (size_t)g.ks * 32 * g.ci_pad * 2 : 0;
         case STZS_PACK_X3: return 2 * (size_t)g.ks * g.co_pad * g.ci_pad * 2;

@@ -91,6 +91,8 @@ struct CW {
 inline int blk_form(int Co, int Ci) {
     return (Ci > 64 && Co % 32 == 0) ? STZS_PACK_FRAG32 : (Ci > 64 && Co % 16 == 0) ? STZS_PACK_LANE16 : STZS_PACK_KSTEP;
 }
+// ... and for the blocks' 1x1 shortcut (r06): the register-direct form under the same condition, else the K-step one
+inline int sc_form(int Co, int Ci) { return (Ci > 64 && Co % 32 == 0) ? STZS_PACK_FRAG32 : STZS_PACK_KSTEP; }
 
 struct Ctx {
     Carve cv;
@@ -317,7 +319,7 @@ int blk(Ctx& c, const BlkIn& bw, const Act& x, const Act& out, const float* gb, 
     if (bw.t[4].data) {
         Act scb;
         CK(c.act(scb, B, T, bw.dout, dt));
-        CK(conv(c, CW{&bw.t[4], nullptr, bw.dout, bw.din, 1, STZS_PACK_KSTEP}, x, scb));
+        CK(conv(c, CW{&bw.t[4], nullptr, bw.dout, bw.din, 1, sc_form(bw.dout, bw.din)}, x, scb));
         res = scb;
     }
     const Pro p2{s2, gb + off2, gbs, bw.dout};

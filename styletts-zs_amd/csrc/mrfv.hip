@@ -23,7 +23,7 @@ int stzs_ups_conv_launch(const stzs_conv_args& a, hipStream_t s);   // csrc/ups.
 __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_args& a, hipStream_t s) {
     if (a.ups > 0) return stzs_ups_conv_launch(a, s);
     const int rows_in = 128 + (a.ks - 1) * a.dil;
-    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || rows_in > 16 * (a.ks == 3 ? sb_rows(3) : a.ks == 7 ? sb_rows(7) : SB_MAX) ||
+    if (a.stride != 1 || a.cic != 128 || a.ci_pad % 128 || a.Co % 8 || a.co_pad % BCO || rows_in > 16 * sb_rows(a.ks) ||
         a.in_dtype != STZS_BF16 || a.out_dtype != STZS_BF16 || a.gate || a.epi_act != STZS_ACT_NONE || a.ups ||
         a.refl || a.ldy % 8 || a.bsy % 8 || (a.res && (a.ldr % 8 || a.bsr % 8 || a.res_tdiv <= 0)) ||
         (a.acc_in && (a.lda % 8 || a.bsa % 8)) || (a.stat_part && a.stat_ld < a.Co))
@@ -51,6 +51,15 @@ __attribute__((visibility("hidden"))) int stzs_mrfv_conv_launch(const stzs_conv_
         const bool al = a.alpha != 1.f;
         k = R ? (A ? pick<STZS_ACT_SNAKE, true, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, true, false>(a.ks, one, al, wide, t64))
               : (A ? pick<STZS_ACT_SNAKE, false, true>(a.ks, one, al, wide, t64) : pick<STZS_ACT_SNAKE, false, false>(a.ks, one, al, wide, t64));
+    } else if (!A && a.ks == 1 && a.pro_act == STZS_ACT_NONE && a.pro_mode == STZS_PRO_NONE && !a.stat_part) {
+        // (r06) the AdaIN blocks' 1x1 shortcut convs (1090 -> 1024 at the decoder): the block convs' data movement with
+        // one tap -- as a FLAT LDS-DMA GEMM they ran at 0.11 of their roofline, streaming A and B tiles through LDS
+        blk_wide = a.ci_pad > 128 && a.co_pad % (2 * BCO) == 0 && wide_tiles >= 2 * stzs_cu_count() &&
+                   !(a.flags & STZS_CONV_MRFV_NARROW);
+        blk_t64 = !blk_wide && tiles128 < 4 * stzs_cu_count() && !(a.flags & STZS_CONV_MRFV_T128);
+        k = blk_wide ? (R ? mrfv_conv<STZS_ACT_NONE, true, false, 1, 0, true, 2> : mrfv_conv<STZS_ACT_NONE, false, false, 1, 0, true, 2>)
+          : blk_t64 ? (R ? mrfv_conv<STZS_ACT_NONE, true, false, 1, 0, true, 1, 64> : mrfv_conv<STZS_ACT_NONE, false, false, 1, 0, true, 1, 64>)
+                     : (R ? mrfv_conv<STZS_ACT_NONE, true, false, 1, 0, true> : mrfv_conv<STZS_ACT_NONE, false, false, 1, 0, true>);
     } else if (!A && a.ks == 3) {  // the AdaIN residual blocks of the decoder / prosody predictor
         // (r05) the wide form here too where the wide grid gives every CU two workgroups (a decoder conv at 64
         // utterances: 512 wide tiles): each 9-chunk input row staged once per 256 output channels instead of per 128 --

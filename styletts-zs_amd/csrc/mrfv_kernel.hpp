@@ -47,9 +47,10 @@ constexpr int P = STZS_MRFV_P;
 // staged 16-B vectors per thread (16 rows each): rows_in = 128 + (KS - 1) dil <= 16 SB.  Sized per kernel width
 // (k3: dil <= 8; k7 / k11: dil <= 5), not for the widest: every staged vector costs its transform (the cosines
 // of the Snake) whether or not its row is used, and a k3 tile with SB = 12 transformed 192 rows for 130-138
-constexpr int sb_rows(int ks) { return ks == 3 ? 9 : (ks == 7 ? 10 : 12); }
+// (ks 1, r06: the AdaIN blocks' 1x1 shortcut convs -- no halo)
+constexpr int sb_rows(int ks) { return ks == 1 ? 8 : ks == 3 ? 9 : (ks == 7 ? 10 : 12); }
 // the 64-row tiles (BT 64, small grids): 64 + (ks - 1) dil rows
-constexpr int sb_rows64(int ks) { return ks == 3 ? 5 : (ks == 7 ? 6 : 8); }
+constexpr int sb_rows64(int ks) { return ks == 1 ? 4 : ks == 3 ? 5 : (ks == 7 ? 6 : 8); }
 constexpr int SB_MAX = 12;
 constexpr int CS_BYTES = 5 * 128 * 4;  // per-channel prologue constants
 // At pitch >= 288 the constants live in the rows' 32 pad bytes (bytes 256..287, never read or written by the tile's

@@ -432,6 +432,7 @@ class StyleTTSZS:
             assert x.t.dtype == torch.float8_e4m3fn and x_scale is not None, what
             a.x_scale, a.w_scale = x_scale.data_ptr(), self._t(cw.wscale).data_ptr()
         if (cw.ks == 1 and stride == 1 and pad == 0 and not cw.ups and pro is None and pro_act == L.ACT_NONE
+                and not getattr(cw, "frag32", False)  # (the 1x1 block shortcuts on the register-direct form)
                 and cscale == 1.0 and x.t.dtype in (torch.bfloat16, torch.float8_e4m3fn)
                 and x.c0 + cw.ci_pad <= x.ld and a.T_out == x.T):
             flags |= 8  # STZS_CONV_A_DMA: every row readable over ci_pad channels -> LDS-DMA GEMM path
@@ -1253,7 +1254,7 @@ class StyleTTSZS:
                                          what=key + ".conv1")
         if bw.sc is not None:
             scb = self.act(key + ".sc", B, T, bw.dout, dt)
-            self.conv(bw.sc, x, scb, splitk=sk, what=key + ".sc")
+            self.conv(bw.scs if (sk and bw.scs is not None) else bw.sc, x, scb, splitk=sk, what=key + ".sc")
             res = scb
         else:
             res = x

@@ -226,7 +226,7 @@ def pack_conv(A: Arena, name, w, b=None, ups=0, lane16=False, narrow32=False, f3
             fx3 = A.add(name + ".wfx3", frag32x3_stream(wf))
         return ConvW(wn, bn, Ci, Co, ks, ci_pad, co_pad, cic, ups, False, True, w32=w32, wx3=wx3, fx3=fx3)
     if frag32:  # register-direct MRF convs (csrc/mrfv.hip) and the polyphase ConvTranspose (csrc/ups.hip, ups > 0)
-        assert cic == 128 and ((not ups and Co % 8 == 0 and ks in (3, 7, 11)) or (ups and Co % 32 == 0)), \
+        assert cic == 128 and ((not ups and Co % 8 == 0 and ks in (1, 3, 7, 11)) or (ups and Co % 32 == 0)), \
             (name, Ci, Co, ks, ups)
         wp = wp.view(ks, co_pad // 128, 128, ci_pad)[:, :, frag32_perm()].reshape(ks, co_pad, ci_pad)
         wn = A.add(name + ".wfr", frag32_stream(wp).to(torch.bfloat16))
@@ -421,6 +421,7 @@ class BlkW:
     # over input-channel chunks (StyleTTSZS(blk_splitk=...)): a 5-s utterance's decoder conv is 16 tiles otherwise
     conv1s: Optional[ConvW] = None
     conv2s: Optional[ConvW] = None
+    scs: Optional[ConvW] = None  # (the shortcut likewise, when it is on the register-direct form)
 
 
 def _lane16_ok(w) -> bool:
@@ -443,7 +444,13 @@ def pack_blk(A: Arena, P, name, up=False, x3=False) -> BlkW:
     f1, f2 = _frag32_ok(w1), _frag32_ok(w2)
     c1 = pack_conv(A, name + ".conv1", w1, P[name + ".conv1.b"], lane16=_lane16_ok(w1) and not f1, frag32=f1, x3=x3)
     c2 = pack_conv(A, name + ".conv2", w2, P[name + ".conv2.b"], lane16=_lane16_ok(w2) and not f2, frag32=f2, x3=x3)
-    sc = pack_conv(A, name + ".sc", P[name + ".sc.w"], x3=x3) if name + ".sc.w" in P else None
+    # the 1x1 shortcut on the register-direct form too (r06, tools/sc_bench.py: the decoder's 1090 -> 1024 shortcut
+    # 100 us on the generic conv -- its 1090-channel rows are too narrow for the LDS-DMA GEMM -- vs 52 us; the
+    # encode block's 514 -> 1024 68 vs 33 us; the same bits as the GEMM forms)
+    wsc = P.get(name + ".sc.w")
+    fs = wsc is not None and not x3 and wsc.shape[1] > 64 and wsc.shape[0] % 32 == 0
+    sc = pack_conv(A, name + ".sc", wsc, x3=x3, frag32=fs) if wsc is not None else None
+    scs = pack_conv(A, name + ".scs", wsc) if fs else None
     c1s = pack_conv(A, name + ".conv1s", w1, P[name + ".conv1.b"]) if f1 and not x3 else None
     c2s = pack_conv(A, name + ".conv2s", w2, P[name + ".conv2.b"]) if f2 and not x3 else None
     pw = pb = None
@@ -452,7 +459,7 @@ def pack_blk(A: Arena, P, name, up=False, x3=False) -> BlkW:
         pb = A.add(name + ".poolb", P[name + ".pool.b"].float())
     din = P[name + ".conv1.w"].shape[1]
     dout = P[name + ".conv1.w"].shape[0]
-    return BlkW(name, din, dout, up, c1, c2, sc, pw, pb, c1s, c2s)
+    return BlkW(name, din, dout, up, c1, c2, sc, pw, pb, c1s, c2s, scs)
 
 
 class PackedModel:

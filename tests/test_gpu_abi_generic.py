@@ -288,7 +288,7 @@ class _Weights:
         form = lambda cw: L.PACK_FRAG32 if cw.frag32 else (L.PACK_LANE16 if cw.lane16 else L.PACK_KSTEP)
         f1, f2 = form(bw.conv1), form(bw.conv2)
         out = self.conv(bw.conv1, n + ".conv1", form=f1) + self.conv(bw.conv2, n + ".conv2", form=f2)
-        out.append(self.conv(bw.sc, n + ".sc")[0] if bw.sc is not None else _none_tensor())
+        out.append(self.conv(bw.sc, n + ".sc", form=form(bw.sc))[0] if bw.sc is not None else _none_tensor())
         out += [self.raw(bw.pool_w), self.raw(bw.pool_b)] if bw.up else [_none_tensor(), _none_tensor()]
         return out
 
