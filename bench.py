@@ -476,7 +476,8 @@ def pipe_runner(eng, S, dev, tok_d, ref_d, eps_d, dur_d, seeds, n_frames, pidx, 
         ga = fr[p].capture(front)[0]
         graphs.append((ga, backs))
     # (equal priorities: a high-priority decoder stream measured 12.7k audio-s/s, a high-priority front stream 15.6k,
-    # against 19.0k -- profiles/r06y_*prio*)
+    # against 19.0k -- profiles/r06y_*prio*; the front on a CU-masked stream (every 2nd / 4th / 8th CU) 13.4-14.4k
+    # against 19.3k -- profiles/r06af: the front is not latency-bound enough to live on a fraction of the chip)
     sF, sD = torch.cuda.Stream(dev), [torch.cuda.Stream(dev) for _ in range(nback)]
     host = dict(zip(("tok", "ref", "eps", "dur"), (t.pin_memory() for t in host_src)))
     host["wav"] = torch.empty(B, nwav, dtype=torch.float32).pin_memory()
