@@ -20,22 +20,26 @@
 namespace {
 
 constexpr int NTH = 256;
-constexpr int BT = 128;
 #ifndef STZS_UPS_P
 #define STZS_UPS_P 288
 #endif
 constexpr int P = STZS_UPS_P;             // staged row pitch, bytes (288: conflict-free ds_read_b128, csrc/mrfv.hip)
-constexpr int ROWS = BT + 1;              // a 2-tap conv at pad 1: rows q0 - 1 .. q0 + 127
-constexpr int TILE = (ROWS * P + 15) & ~15;
-constexpr int SB = 9;                     // 16 row lanes x 9 >= 129 rows
+// BT: q rows per tile, 128 or 64 (r06: the 512-channel first stage -- 4 chunks x 37 KB of staged rows held ONE
+// workgroup per CU at 128 rows, and its 401-row utterances filled 4 x 128 tiles to 78 %); the same K order per output
+// element either way: bit-identical
+constexpr int rows_of(int bt) { return bt + 1; }  // a 2-tap conv at pad 1: rows q0 - 1 .. q0 + bt - 1
+constexpr int tile_of(int bt) { return (rows_of(bt) * P + 15) & ~15; }
 constexpr int RING = 4;                   // weight K-steps in flight (3 ahead); divides every NK (8 per chunk)
 
 // NZ (STZS_CONV_UPS_NOISE): the 1x1 noise conv fused as one more K-step per column tile whose B operand is the
 // harmonic-source rows of the tile's output rows (loaded at the tile's start, as the residual rows were) and whose
 // weights follow the tile's ConvTranspose K-steps in the stream; there is then no residual operand.
-template <int NCH, bool HR, bool NZ>
-__global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_conv_args a, int ctw) {
+template <int NCH, bool HR, bool NZ, int BT = 128>
+__global__ __launch_bounds__(NTH, NCH * tile_of(BT) <= 80 * 1024 ? 2 : 1) void ups_conv(const stzs_conv_args a, int ctw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int ROWS = rows_of(BT), TILE = tile_of(BT);
+    constexpr int SB = (ROWS + 15) / 16;  // staged 16-B vectors per thread (16 row lanes)
+    constexpr int MT = BT / 16;           // 16-row input fragments per wave
     constexpr int NK = NCH * 8;  // K-steps per column tile: chunks x 2 taps x 4
     constexpr int NKW = NK + (NZ ? 1 : 0);  // weight-stream K-steps per column tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -104,8 +108,8 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
     const int t_hi = a.T_final + a.refl - 1;
     const bf16_t* Rb = reinterpret_cast<const bf16_t*>(a.res) + (long)bq * a.bsr;
     bf16_t* Y = reinterpret_cast<bf16_t*>(a.y) + (long)bq * a.bsy;
-    f32x4 acc[2][8];
-    bf16x8 xf[8];
+    f32x4 acc[2][MT];
+    bf16x8 xf[MT];
     for (int ct = ct0; ct < ct1; ++ct) {
         const int jb = (ct - ct0) * NK;
         // this tile's output rows / channels and its residual rows, loaded now (consumed after the K loop)
@@ -113,10 +117,10 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
         const int ph = col0 / a.Co, cof = col0 - ph * a.Co;
         const bool col_ok = col0 < ncol;
         const int cofc = col_ok ? cof : 0;
-        uint4 rr[8];  // residual rows (HR) or, fused noise conv (NZ), the harmonic-source B fragments
-        int trow[8];
+        uint4 rr[MT];  // residual rows (HR) or, fused noise conv (NZ), the harmonic-source B fragments
+        int trow[MT];
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
+        for (int mt = 0; mt < MT; ++mt) {
             const int q = q0 + mt * 16 + n;
             const int t = q * a.ups + ph - a.ups_pad + a.refl;
             trow[mt] = t;
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
 #pragma unroll
         for (int i = 0; i < 8; ++i) bias[i] = a.bias ? a.bias[cofc + i] : 0.f;
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
+        for (int mt = 0; mt < MT; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + mt * 16 * P);
         const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < NK; ++s) {
@@ -142,14 +146,14 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
             const int sn = s + 1;  // next K-step's input fragments: chunk sn / 8, tap (sn / 4) & 1, kq sn & 3
             const int offn = (sn >> 3) * TILE + ((sn >> 2) & 1) * P + (sn & 3) * 64;
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
+            for (int mt = 0; mt < MT; ++mt) {
                 acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % RING][0], xf[mt], s == 0 ? zero : acc[0][mt], 0, 0, 0);
                 acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s % RING][1], xf[mt], s == 0 ? zero : acc[1][mt], 0, 0, 0);
                 if (sn < NK) xf[mt] = *reinterpret_cast<const bf16x8*>(smem + xoff0 + offn + mt * 16 * P);
             }
             __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // the two weight loads first
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
+            for (int mt = 0; mt < MT; ++mt) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                 if (sn < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
         }
         if constexpr (NZ) {  // the fused noise conv: one more K-step on the harmonic-source rows
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
+            for (int mt = 0; mt < MT; ++mt) {
                 const bf16x8 hf = __builtin_bit_cast(bf16x8, rr[mt]);
                 acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wn[0], hf, acc[0][mt], 0, 0, 0);
                 acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wn[1], hf, acc[1][mt], 0, 0, 0);
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(NTH, NCH <= 2 ? 2 : 1) void ups_conv(const stzs_con
         }
         // epilogue: row q -> t = q ups + p - pad_up (+ refl), valid for q < T_out and t in [0, T_final)
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
+        for (int mt = 0; mt < MT; ++mt) {
             const int q = q0 + mt * 16 + n;
             const int t = trow[mt];
             const int tp = t - a.refl;
@@ -236,6 +240,13 @@ __attribute__((visibility("hidden"))) int stzs_ups_conv_launch(const stzs_conv_a
         return STZS_ESHAPE;
     const int nch = a.ci_pad / 128;
     const int nct = (a.ups * a.Co + 127) / 128;
+    // 64-row q tiles where the 128-row form's staged chunks hold one workgroup per CU (more than two chunks);
+    // STZS_UPS_BT=128 / 64 forces a form (A/B)
+    static const int bt_env = [] {
+        const char* e = getenv("STZS_UPS_BT");
+        return e ? atoi(e) : 0;
+    }();
+    const int BT = bt_env == 64 || bt_env == 128 ? bt_env : (nch > 2 ? 64 : 128);
     const int nqt = a.B * ((a.T_out + BT - 1) / BT);
     // column tiles per workgroup: all of them (input staged once), unless the q-tile grid alone leaves most of the
     // chip idle (the 40-fps first stage: 128 q tiles at batch 64) -- then slices, ~4 workgroups per CU in total
@@ -244,16 +255,23 @@ __attribute__((visibility("hidden"))) int stzs_ups_conv_launch(const stzs_conv_a
     while (groups < nct && (long)nqt * groups < target) ++groups;
     const int ctw = (nct + groups - 1) / groups;
     groups = (nct + ctw - 1) / ctw;
-    const size_t lds = (size_t)nch * TILE;
+    const size_t lds = (size_t)nch * (BT == 64 ? tile_of(64) : tile_of(128));
     void (*k)(stzs_conv_args, int) = nullptr;
     const bool R = a.res != nullptr;
-    switch (nch) {
-        case 1: k = nz ? ups_conv<1, false, true> : R ? ups_conv<1, true, false> : ups_conv<1, false, false>; break;
-        case 2: k = nz ? ups_conv<2, false, true> : R ? ups_conv<2, true, false> : ups_conv<2, false, false>; break;
-        case 3: k = nz ? ups_conv<3, false, true> : R ? ups_conv<3, true, false> : ups_conv<3, false, false>; break;
-        case 4: k = nz ? ups_conv<4, false, true> : R ? ups_conv<4, true, false> : ups_conv<4, false, false>; break;
+#define STZS_UPS_PICK(N, B_)                                                                                    \
+    k = nz ? ups_conv<N, false, true, B_> : R ? ups_conv<N, true, false, B_> : ups_conv<N, false, false, B_>;
+    switch (nch * (BT == 64 ? -1 : 1)) {
+        case 1: STZS_UPS_PICK(1, 128) break;
+        case 2: STZS_UPS_PICK(2, 128) break;
+        case 3: STZS_UPS_PICK(3, 128) break;
+        case 4: STZS_UPS_PICK(4, 128) break;
+        case -1: STZS_UPS_PICK(1, 64) break;
+        case -2: STZS_UPS_PICK(2, 64) break;
+        case -3: STZS_UPS_PICK(3, 64) break;
+        case -4: STZS_UPS_PICK(4, 64) break;
         default: return STZS_ESHAPE;
     }
+#undef STZS_UPS_PICK
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, dim3((unsigned)nqt, (unsigned)groups), dim3(NTH), lds, s, a, ctw);
     STZS_LAUNCH_CHECK();
