@@ -434,6 +434,28 @@ def test_mrf_t64_bit_identical(eng, case):
         assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
 
 
+@pytest.mark.parametrize("B,T,Ci,Co,ld", [(64, 200, 1090, 1024, 1096), (2, 37, 514, 1024, 520), (3, 131, 1090, 512, 1160),
+                                         (1, 200, 512, 256, 512), (200, 700, 512, 128, 512)])
+def test_block_shortcut_frag32(eng, B, T, Ci, Co, ld):
+    """the AdaIN blocks' 1x1 shortcut on the register-direct block-conv form (STZS_CONV_W_FRAG32, ks 1; the wide form at
+    B = 64, the narrow 128-row form last, the 64-row form between) vs the same weights on the K-step path (the LDS-DMA GEMM where the rows
+    are wide enough, else the generic conv): the same bits, and within 1e-2 of max|ref| of the fp32 product."""
+    g = torch.Generator().manual_seed(Ci + T)
+    x = bf(torch.randn(B, T, Ci, generator=g))
+    w = torch.randn(Co, Ci, 1, generator=g) / math.sqrt(Ci)
+    ref = torch.einsum("btc,oc->bto", x, w[:, :, 0])
+    xd = _act(_dev_ntc(x, ld), Ci)
+    outs = []
+    for frag in (False, True):
+        cw, _A = _pack(w, None, frag32=frag)
+        yd = _act(torch.zeros(B, T, Co, dtype=torch.bfloat16, device="cuda:0"))
+        eng.conv(cw, xd, yd)
+        torch.cuda.synchronize()
+        outs.append(yd.t.float().cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert max_rel(outs[1], ref) < 1e-2
+
+
 @pytest.mark.parametrize("B,T,Ci,Co,k", [(2, 3001, 128, 22, 7), (1, 300, 256, 32, 3), (3, 257, 128, 8, 7)])
 def test_narrow_conv(eng, B, T, Ci, Co, k):
     """narrow conv (conv_post form: LeakyReLU(0.01) prologue, Co <= 32, fp32 out, csrc/mrf.hip
