@@ -1208,11 +1208,13 @@ class StyleTTSZS:
         Nn = self.buf("pr.N", (B, T80, 1), torch.float32)
         c0, c1, c2 = S.f0n_ch
 
+        s0 = self.stats(xs, "pr.xs.s1")  # (both branches' first AdaIN normalise xs: its statistics once, r06)
+
         def branch(br, out):
             y0 = self.act(f"pr.{br}.y0", B, T40, c0, self.adt)
             y1 = self.act(f"pr.{br}.y1", B, T80, c1, self.adt)
             y2 = self.act(f"pr.{br}.y2", B, T80, c2, self.adt)
-            self.blk(W.pr_blk[f"pr.{br}0"], xs, y0, ng, gbp, f"pr.{br}0", self.adt)
+            self.blk(W.pr_blk[f"pr.{br}0"], xs, y0, ng, gbp, f"pr.{br}0", self.adt, s1=s0)
             self.blk(W.pr_blk[f"pr.{br}1"], y0, y1, ng, gbp, f"pr.{br}1", self.adt)
             self.blk(W.pr_blk[f"pr.{br}2"], y1, y2, ng, gbp, f"pr.{br}2", self.adt)
             self.conv(W.pr_blk[f"pr.{br}_proj"], y2, Act(out, 0, 1), what=f"pr.{br}_proj")
@@ -1226,13 +1228,14 @@ class StyleTTSZS:
         a.B, a.Tsrc, a.Tdst, a.C, a.xc0, a.yc0, a.dtype = x.B, x.T, y.T, Cn, x.c0, y.c0, x.dt
         self._call(self.lib.stzs_gather_rows, a, "gather")
 
-    def blk(self, bw, x: Act, out: Act, ng, gb: torch.Tensor, key, dt=torch.bfloat16):
-        """AdainResBlk1d: out = (conv2(act(AdaIN(conv1(up(act(AdaIN(x))))))) + sc(x)) / sqrt 2."""
+    def blk(self, bw, x: Act, out: Act, ng, gb: torch.Tensor, key, dt=torch.bfloat16, s1=None):
+        """AdainResBlk1d: out = (conv2(act(AdaIN(conv1(up(act(AdaIN(x))))))) + sc(x)) / sqrt 2.
+        s1: x's statistics when the caller already has them (self.stats(x, ...))."""
         B, T = x.B, x.T
         off1, n1 = ng.offsets[bw.name + ".norm1"]
         off2, n2 = ng.offsets[bw.name + ".norm2"]
         gbase, gbs = gb.data_ptr(), ng.total
-        m1, r1, sb1 = self.stats(x, key + ".s1")
+        m1, r1, sb1 = s1 if s1 is not None else self.stats(x, key + ".s1")
         # batch-1 engine: the generic-layout copies split-K (blk_splitk), else the register-direct convs
         sk = self.blk_splitk if dt == torch.bfloat16 else 0
         c1 = bw.conv1s if (sk and bw.conv1s is not None) else bw.conv1
