@@ -200,6 +200,15 @@ size_t stzs_conv_splitk_workspace(int64_t rows, int32_t co_pad, int32_t splitk);
  * csrc/rows.hip form (STZS_CONV_ROWS) and the 16-row K-slice form of stzs_ln_linear (ln = NULL, splitk in {2, 4}) */
 size_t stzs_conv_rows_workspace(int64_t rows, int32_t Co, int32_t kgroups);
 int stzs_conv1d(const stzs_conv_args* a, void* stream);
+/* n in 1..3 independent stzs_conv1d problems (no one reads another's output) in as few launches as the library can:
+ * the k3 / k7 / k11 convs of one generator MRF layer (a[0..2]: STZS_CONV_W_FRAG32, ks 3, 7, 11, Snake AdaIN prologue,
+ * no acc_in, alpha 1, same B / T_out / Ci / Co / ci_pad / co_pad, all with or all without a residual, small grids --
+ * each taking the 64-row tiles on its own, e.g. batch 1) run as ONE launch whose workgroups execute each problem's own
+ * kernel body; anything else runs one stzs_conv1d after the other.  Outputs (and fused statistics partials) are
+ * bit-identical to n stzs_conv1d calls either way.  Returns the number of kernel launches issued (1 or n), or a
+ * negative STZS_E* code (from the first failing problem's checks).  (r06: no reference counterpart -- the
+ * reference's generator runs its resblocks one conv at a time) */
+int stzs_conv1d_group(const stzs_conv_args* a, int n, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------
  * x [B, T, ld] (bf16|f32), channels [0, C).  `partial` is caller workspace of
@@ -222,6 +231,9 @@ int stzs_chan_stats_partial(const stzs_stats_args* a, void* stream);
 /* second pass only: mean / rstd from a partial slab already holding ceil(T / chunk_rows) chunks
  * (written by stzs_conv1d's stat_part epilogue with chunk_rows = STZS_CONV_STAT_ROWS); x unused. */
 int stzs_chan_stats_final(const stzs_stats_args* a, int chunk_rows, void* stream);
+/* n in 1..3 stzs_chan_stats_final problems (same chunk_rows) in ONE launch; each mean / rstd bit-identical to its own
+ * stzs_chan_stats_final call.  (r06: the three MRF resblocks' statistics at batch 1, beside stzs_conv1d_group) */
+int stzs_chan_stats_final_group(const stzs_stats_args* a, int n, int chunk_rows, void* stream);
 
 /* ---- row LayerNorm + modulation (+activation), one wave per row -------------------------
  * y[r, c] = act((x - mu_r) * rstd_r * (gadd + G[(r/gdiv)*gs + c]) + Bt[(r/gdiv)*bs + c])

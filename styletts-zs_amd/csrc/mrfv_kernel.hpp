@@ -111,8 +111,10 @@ __device__ unsigned long long g_mprof[8 * 16384];
 // order per output element either way (bit-identical).
 // BT: time rows per tile, 128 or 64 (r05: small grids -- batch 1 -- where the 128-row tiles leave CUs idle).  The
 // staged operands, the K order of every output element and the 64-row statistics chunks are the same: bit-identical.
+// (r06) the body as an always-inlined device function: the kernel mrfv_conv below is this body alone (same code
+// object), mrfv_trio runs three of them in one launch.
 template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int BT = 128>
-__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
+STZS_DEV void mrfv_body(const stzs_conv_args a) {
     static_assert(WPW == 1 || (WPW == 2 && NCH != 1), "the wide form is for multi-chunk inputs");
     static_assert(BT == 128 || (BT == 64 && WPW == 1), "64-row tiles: narrow form");
     MPROF(5, __builtin_amdgcn_s_memrealtime())
@@ -470,6 +472,29 @@ __global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) voi
 #endif
 }
 
+template <int PACT, bool HR, bool HA, int KS, int NCH, bool AL, int WPW = 1, int BT = 128>
+__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_conv(const stzs_conv_args a) {
+    mrfv_body<PACT, HR, HA, KS, NCH, AL, WPW, BT>(a);
+}
+
+// (r06) the three resblocks' convs of one MRF layer (k 3 / 7 / 11, same input, same shape and form) in ONE launch: grid
+// z = 0, 1, 2 runs the k11, k7, k3 problem (the longest workgroups dispatched first), each with its own arguments --
+// every workgroup executes exactly the body of the single-problem kernel, so the outputs are bit-identical.  At batch 1
+// a single conv fills 63 (stage 0) or 376 (stage 1) workgroups of 256 CUs and its time is latency, not throughput:
+// side by side the three take little more than the k11 alone.  Snake prologue, no accumulate input, alpha 1, the narrow
+// 64-row tiles (the small-grid form); csrc/mrfv.hip stzs_mrfv_trio_launch checks the rest.
+template <bool HR, int NCH, int BT>
+__global__ __launch_bounds__(NTH, NCH == 1 ? STZS_MRFV_OCC1 : STZS_MRFV_OCC) void mrfv_trio(const stzs_conv_args a3,
+                                                                                        const stzs_conv_args a7,
+                                                                                        const stzs_conv_args a11) {
+    if (blockIdx.z == 0)
+        mrfv_body<STZS_ACT_SNAKE, HR, false, 11, NCH, false, 1, BT>(a11);
+    else if (blockIdx.z == 1)
+        mrfv_body<STZS_ACT_SNAKE, HR, false, 7, NCH, false, 1, BT>(a7);
+    else
+        mrfv_body<STZS_ACT_SNAKE, HR, false, 3, NCH, false, 1, BT>(a3);
+}
+
 template <int PACT, bool HR, bool HA, int NCH, bool AL, int WPW = 1, int BT = 128>
 void (*pick_ks(int ks))(stzs_conv_args) {
     switch (ks) {
@@ -488,3 +513,5 @@ void (*pick_ks(int ks))(stzs_conv_args) {
 // faster so built (profiles/r06e_mrfv_nopk.log), while the wide stage-0 forms (256 VGPRs) lose 7 % and keep them
 using mrfv_kfn = void (*)(stzs_conv_args);
 mrfv_kfn stzs_mrfv_pick_n1(int ks, bool hr, bool ha, bool al, bool t64);
+using mrfv_trio_kfn = void (*)(stzs_conv_args, stzs_conv_args, stzs_conv_args);
+mrfv_trio_kfn stzs_mrfv_trio_pick_n1(bool hr);  // (the single-chunk trio forms, 64-row tiles)

@@ -17,6 +17,8 @@ mrfv_kfn stzs_mrfv_pick_n1(int ks, bool hr, bool ha, bool al, bool t64) {
     return nullptr;
 }
 
+mrfv_trio_kfn stzs_mrfv_trio_pick_n1(bool hr) { return hr ? mrfv_trio<true, 1, 64> : mrfv_trio<false, 1, 64>; }
+
 #ifdef STZS_MRFV_PROF
 // (probe build only) the stage-1 instances' phase stamps -> host; zero: clear them after the copy
 extern "C" int stzs_mrfv_prof_read(unsigned long long* host, size_t n, int zero) {

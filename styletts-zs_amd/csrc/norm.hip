@@ -79,10 +79,10 @@ __global__ __launch_bounds__(256) void chan_stats_partial(const stzs_stats_args 
 // pass 2: block = (utterance, 32 channels); 8 chunk groups stride over the chunks with coalesced
 // 8-B (sum, sumsq) loads, fp64 sums, combined in fixed group order -> deterministic.
 constexpr int FIN_CH = 32;
-__global__ __launch_bounds__(256) void chan_stats_final(const stzs_stats_args a, int nchunk) {
+STZS_DEV void stats_final_body(const stzs_stats_args a, int nchunk, int b, int by) {
     __shared__ double red[8][FIN_CH][2];
     const int tid = threadIdx.x, cl = tid & (FIN_CH - 1), g = tid >> 5;
-    const int b = blockIdx.x, c = blockIdx.y * FIN_CH + cl;
+    const int c = by * FIN_CH + cl;
     double s = 0.0, q = 0.0;
     if (c < a.C) {
         const float2* P = reinterpret_cast<const float2*>(a.partial) + (long)b * nchunk * a.C + c;
@@ -118,6 +118,23 @@ __global__ __launch_bounds__(256) void chan_stats_final(const stzs_stats_args a,
         a.mean[(long)b * a.stat_bs + c] = mu;
         a.rstd[(long)b * a.stat_bs + c] = rs;
     }
+}
+
+__global__ __launch_bounds__(256) void chan_stats_final(const stzs_stats_args a, int nchunk) {
+    stats_final_body(a, nchunk, blockIdx.x, blockIdx.y);
+}
+
+// (r06) up to three independent finalisations in one launch (grid z = problem): each block runs the body above for
+// its own problem, so every mean / rstd has the bits of its own chan_stats_final launch
+struct StatsGroup {
+    stzs_stats_args a[3];
+    int nchunk[3];
+};
+__global__ __launch_bounds__(256) void chan_stats_final_group(const StatsGroup g) {
+    const int z = blockIdx.z;
+    const stzs_stats_args& a = z == 0 ? g.a[0] : (z == 1 ? g.a[1] : g.a[2]);
+    if ((int)blockIdx.x >= a.B || (int)blockIdx.y * FIN_CH >= a.C) return;  // (uniform per block)
+    stats_final_body(a, z == 0 ? g.nchunk[0] : (z == 1 ? g.nchunk[1] : g.nchunk[2]), blockIdx.x, blockIdx.y);
 }
 
 
@@ -198,6 +215,24 @@ extern "C" int stzs_chan_stats_final(const stzs_stats_args* a, int chunk_rows, v
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int nchunk = (a->T + chunk_rows - 1) / chunk_rows;
     hipLaunchKernelGGL(chan_stats_final, dim3(a->B, (a->C + FIN_CH - 1) / FIN_CH), dim3(256), 0, s, *a, nchunk);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
+extern "C" int stzs_chan_stats_final_group(const stzs_stats_args* a, int n, int chunk_rows, void* stream) {
+    if (!a || n < 1 || n > 3 || chunk_rows <= 0) return STZS_EINVAL;
+    StatsGroup g = {};
+    int gx = 0, gy = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!a[i].mean || !a[i].rstd || !a[i].partial) return STZS_EINVAL;
+        if (a[i].B <= 0 || a[i].T <= 0 || a[i].C <= 0) return STZS_ESHAPE;
+        g.a[i] = a[i];
+        g.nchunk[i] = (a[i].T + chunk_rows - 1) / chunk_rows;
+        gx = a[i].B > gx ? a[i].B : gx;
+        const int ny = (a[i].C + FIN_CH - 1) / FIN_CH;
+        gy = ny > gy ? ny : gy;
+    }
+    hipLaunchKernelGGL(chan_stats_final_group, dim3(gx, gy, n), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), g);
     STZS_LAUNCH_CHECK();
     return STZS_OK;
 }

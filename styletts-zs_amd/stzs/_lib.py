@@ -205,10 +205,10 @@ def params(ints=(), floats=()) -> Params:
 
 
 # every exported symbol of include/stzs.h (tests check the .so exports exactly these)
-EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_conv_splitk_workspace",
+EXPORTS = ["stzs_init", "stzs_strerror", "stzs_version", "stzs_conv1d", "stzs_conv1d_group", "stzs_conv_splitk_workspace",
            "stzs_conv_rows_workspace",
            "stzs_chan_stats_workspace",
-           "stzs_chan_stats", "stzs_chan_stats_partial", "stzs_chan_stats_final", "stzs_row_layernorm", "stzs_ln_linear", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_lstm_pair",
+           "stzs_chan_stats", "stzs_chan_stats_partial", "stzs_chan_stats_final", "stzs_chan_stats_final_group", "stzs_row_layernorm", "stzs_ln_linear", "stzs_quant_rows", "stzs_attention", "stzs_lstm_workspace", "stzs_lstm", "stzs_lstm_pair",
            "stzs_lstm_state_reset", "stzs_predictor_prep",
            "stzs_durations", "stzs_alignment", "stzs_gather_rows", "stzs_adain_dwup", "stzs_f0n_down",
            "stzs_harmonic_source", "stzs_istft", "stzs_istft_stream", "stzs_istft_stream_span",
@@ -239,12 +239,14 @@ def load():
         "stzs_strerror": ([i32], C.c_char_p),
         "stzs_version": ([], i32),
         "stzs_conv1d": ([P(ConvArgs), vp], i32),
+        "stzs_conv1d_group": ([P(ConvArgs), i32, vp], i32),
         "stzs_conv_splitk_workspace": ([i64, i32, i32], C.c_size_t),
         "stzs_conv_rows_workspace": ([i64, i32, i32], C.c_size_t),
         "stzs_chan_stats_workspace": ([i32, i32, i32], C.c_size_t),
         "stzs_chan_stats": ([P(StatsArgs), vp], i32),
         "stzs_chan_stats_partial": ([P(StatsArgs), vp], i32),
         "stzs_chan_stats_final": ([P(StatsArgs), i32, vp], i32),
+        "stzs_chan_stats_final_group": ([P(StatsArgs), i32, i32, vp], i32),
         "stzs_row_layernorm": ([P(RowLNArgs), vp], i32),
         "stzs_ln_linear": ([P(ConvArgs), P(RowLNArgs), vp], i32),
         "stzs_quant_rows": ([P(QuantArgs), vp], i32),

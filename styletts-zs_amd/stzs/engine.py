@@ -269,6 +269,9 @@ class StyleTTSZS:
         # (stzs_conv_args.pro_part: the prologue finalises them, bit-identical, one launch less per statistics) --
         # the engines whose AdaIN-block convs run the generic path (blk_splitk); STZS_DEFER_STATS=0|1 overrides
         self.defer_stats = os.environ.get("STZS_DEFER_STATS", "1" if self.blk_splitk else "0") != "0"
+        # (r06) small batches (<= 4 utterances): the generator MRF's three resblocks advanced side by side, each layer's
+        # three convs in one launch (stzs_conv1d_group, csrc/mrfv.hip mrfv_trio) -- bit-identical; STZS_MRF_TRIO=0: off
+        self.mrf_trio = os.environ.get("STZS_MRF_TRIO", "1") != "0"
         # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
         # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
@@ -384,9 +387,12 @@ class StyleTTSZS:
              pro_slope=0.0, pro_alpha=None, cscale=1.0, res: Act = None, res_tdiv=1, acc_in: Act = None,
              alpha=1.0, beta=0.0, gate=None, gate_bs=0, epi_act=L.ACT_NONE, epi_slope=0.0, ups_pad=0,
              T_final=0, refl=0, flags=0, stats_key=None, x_scale=None, post_ln=None, pre_ln=None, splitk=0, rows=0,
-             attn=None, what="conv"):
+             attn=None, collect=None, what="conv"):
         """-> y, or (y, (mean, rstd, stat_bs)) with stats_key: InstanceNorm statistics of the stored
         output fused into the conv epilogue (per-tile partials) + one small finalize launch.
+        collect (a list): append the conv's stzs_conv_args to it instead of launching (the caller launches the
+        collected problems with stzs_conv1d_group, and finalises their statistics -- returned unfinalised, per-key
+        slabs -- with _finalize_group).
         post_ln (stzs_rowln_args) / attn ((q, k, v, o) Acts): the LayerNorm / attention that consumes y, launched
         behind the linear.  (r03 also ran them, and the sampler's CFG + Euler step, inside the small-M linear's launch
         by its last-arriving workgroups: bit-identical but slower at batch 1, removed in r04 -- DESIGN.md §5.)
@@ -511,7 +517,7 @@ class StyleTTSZS:
         if stats_key is not None:
             Cc = _rup(cw.Co, 8)
             ntile = (a.T_out + L.CONV_STAT_ROWS - 1) // L.CONV_STAT_ROWS
-            defer = self.defer_stats and ntile <= 8
+            defer = collect is not None or (self.defer_stats and ntile <= 8)
             # (deferred: the partials must outlive this launch until their consumer reads them -- a slab per key)
             slab = self._scratch("stat_slab." + stats_key, y.B * ntile * Cc * 2, 1024) if defer else self._slab(y.B * ntile * Cc * 2)
             a.stat_part, a.stat_ld = slab.data_ptr(), Cc
@@ -545,7 +551,10 @@ class StyleTTSZS:
             if not r16_split:
                 a.splitk = 0
             launch = lambda: self.lib.stzs_ln_linear(C.byref(a), None, self.stream())
-        if tm is not None and (tm["all"] or what in tm["tags"]):
+        if collect is not None:
+            assert not fused and not r16 and pre_ln is None and post_ln is None and attn is None, what
+            collect.append(a)
+        elif tm is not None and (tm["all"] or what in tm["tags"]):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -1595,8 +1604,84 @@ class StyleTTSZS:
             f0 += Fc
             i += 1
 
+    def _launch_group(self, args, what):
+        """the collected stzs_conv_args (conv(collect=...)) as ONE stzs_conv1d_group call"""
+        arr = (L.ConvArgs * len(args))(*args)
+        rc = self.lib.stzs_conv1d_group(arr, len(args), self.stream())
+        if rc < 0:
+            L.check(rc, what)
+        self.launches += rc
+
+    def _finalize_group(self, refs):
+        """the statistics of up to three collected convs finalised in one launch (stzs_chan_stats_final_group)"""
+        arr = (L.StatsArgs * len(refs))()
+        for s, r in zip(arr, refs):
+            s.mean, s.rstd, s.partial = r.mean.data_ptr(), r.rstd.data_ptr(), r.part.data_ptr()
+            s.stat_bs, s.B, s.T, s.C, s.eps = r.ld, r.B, r.T, r.ld, 1e-5
+        assert len({r.chunk_rows for r in refs}) == 1
+        self.launches += 1
+        L.check(self.lib.stzs_chan_stats_final_group(arr, len(refs), refs[0].chunk_rows, self.stream()),
+                "chan_stats_final_group")
+        for r in refs:
+            r.done = True
+
+    def _mrf_trio(self, x: Act, i, gbd, ng):
+        """mrf() with the three resblocks (k 3 / 7 / 11) advanced layer by layer side by side: each layer's c1 convs in
+        ONE launch (stzs_conv1d_group -> mrfv_trio at small batch), their statistics in one, the non-last c2 convs and
+        their statistics likewise; the last layer's c2 convs stay one after the other (each adds the previous
+        resblocks' sum, acc_in).  Per-resblock buffers; every value bit-identical to mrf()'s order."""
+        S, W = self.spec, self.W
+        B, T, c = x.B, x.T, x.C
+        gbase, gbs = gbd.data_ptr(), ng.total
+        dt = x.t.dtype
+        nk = len(S.rb_kernels)
+        xs = self.act(f"gen.xs{i}", B, T, c, dt)
+        t1 = [self.act(f"gen.t1_{i}.{j}", B, T, c, dt) for j in range(nk)]
+        bufs = [(self.act(f"gen.ba{i}.{j}", B, T, c, dt), self.act(f"gen.bb{i}.{j}", B, T, c, dt)) for j in range(nk)]
+        mx, rx, sb = self.stats(x, f"gen.sx{i}")
+        cur, cm, cr = [x] * nk, [mx] * nk, [rx] * nk
+        nl = len(W.rb[i][0])
+        for m in range(nl):
+            grp, st1 = [], []
+            for j, res in enumerate(W.rb[i]):
+                lw = res[m]
+                k, dil = lw["k"], lw["dil"]
+                o1, c1 = ng.offsets[lw["n1"]]
+                _, st = self.conv(lw["c1"], cur[j], t1[j], pad=dil * (k - 1) // 2, dil=dil,
+                                  pro=(cm[j], cr[j], sb, gbase + o1 * 4, gbs, c1), pro_act=L.ACT_SNAKE,
+                                  pro_alpha=lw["a1"], stats_key=f"gen.st{i}.{j}", collect=grp, what="rb.c1")
+                st1.append(st)
+            self._launch_group(grp, "rb.c1")
+            self._finalize_group([st[0].ref for st in st1])
+            last = m == nl - 1
+            grp, st2, outs = [], [], []
+            for j, res in enumerate(W.rb[i]):
+                lw = res[m]
+                k = lw["k"]
+                o2, c2 = ng.offsets[lw["n2"]]
+                tm, tr, _ = st1[j]
+                kw = dict(pad=(k - 1) // 2, pro=(tm, tr, sb, gbase + o2 * 4, gbs, c2), pro_act=L.ACT_SNAKE,
+                          pro_alpha=lw["a2"], res=cur[j], what="rb.c2")
+                if last:  # xs = c2 / nk + cur (+ xs): the resblocks' sum in resblock order, one launch each
+                    self.conv(lw["c2"], t1[j], xs, alpha=1.0 / nk, acc_in=(xs if j > 0 else None), beta=1.0, **kw)
+                else:
+                    out = bufs[j][0] if cur[j] is not bufs[j][0] else bufs[j][1]
+                    _, st = self.conv(lw["c2"], t1[j], out, stats_key=f"gen.sc{i}.{j}.{m % 2}", collect=grp, **kw)
+                    st2.append(st)
+                    outs.append(out)
+            if not last:
+                self._launch_group(grp, "rb.c2")
+                self._finalize_group([st[0].ref for st in st2])
+                for j in range(nk):
+                    cur[j], (cm[j], cr[j], _) = outs[j], st2[j]
+        return xs
+
     def mrf(self, x: Act, i, gbd, ng):
         S, W = self.spec, self.W
+        if (self.mrf_trio and self.timer is None and x.B <= 4 and tuple(S.rb_kernels) == (3, 7, 11) and
+                len({len(res) for res in W.rb[i]}) == 1 and all(r["k"] == k for res, k in zip(W.rb[i], (3, 7, 11))
+                                                               for r in res)):
+            return self._mrf_trio(x, i, gbd, ng)
         B, T, c = x.B, x.T, x.C
         gbase, gbs = gbd.data_ptr(), ng.total
         dt = x.t.dtype

@@ -166,6 +166,29 @@ def test_entry_points_reject_before_launch(name, struct, extra):
     assert fn(C.byref(a), *extra, None) == _lib.ESHAPE  # sizes all 0: rejected, nothing dereferenced
 
 
+def test_groups_reject_before_launch():
+    """stzs_conv1d_group / stzs_chan_stats_final_group: NULL arrays and n outside 1..3 -> STZS_EINVAL; problems with
+    NULL pointers or empty shapes are rejected by their own checks (the grouped form is only taken after every
+    problem passes stzs_conv1d's checks) -- all before any HIP call."""
+    from stzs import _lib
+    L = _lib.load()
+    E, S = _lib.EINVAL, _lib.ESHAPE
+    a = (_lib.ConvArgs * 3)()
+    assert L.stzs_conv1d_group(None, 3, None) == E
+    assert L.stzs_conv1d_group(a, 0, None) == E and L.stzs_conv1d_group(a, 4, None) == E
+    assert L.stzs_conv1d_group(a, 3, None) == E  # NULL x / w / y
+    for p in a:
+        p.x, p.w, p.y, p.flags = 0x1000, 0x2000, 0x3000, _lib.CONV_W_FRAG32
+    assert L.stzs_conv1d_group(a, 3, None) == S  # empty shapes: the first problem's own checks
+    st = (_lib.StatsArgs * 2)()
+    assert L.stzs_chan_stats_final_group(None, 2, 64, None) == E
+    assert L.stzs_chan_stats_final_group(st, 0, 64, None) == E and L.stzs_chan_stats_final_group(st, 2, 0, None) == E
+    assert L.stzs_chan_stats_final_group(st, 2, 64, None) == E  # NULL mean / rstd / partial
+    for p in st:
+        p.mean, p.rstd, p.partial = 0x1000, 0x2000, 0x3000
+    assert L.stzs_chan_stats_final_group(st, 2, 64, None) == S
+
+
 def test_lstm_pair_rejects_before_launch():
     """stzs_lstm_pair: each recurrence validated as stzs_lstm validates it, then the pair -- one shape class (B, H,
     ndir, precise) and separate exchange state -- all before any HIP call."""

@@ -430,6 +430,46 @@ def test_dur_overlap_bit_identical(v0, branch_streams):
     e.check_status()
 
 
+@pytest.mark.parametrize("B", [1, 2])
+def test_mrf_trio_synth_bit_identical(v0, B):
+    """small batches advance the generator MRF's three resblocks side by side (engine.mrf_trio: each layer's k3 / k7 /
+    k11 convs in one stzs_conv1d_group launch, their statistics in one stzs_chan_stats_final_group): the waveform of
+    an eager and of a graph-replayed synthesis must be the same bits as the resblock-by-resblock order."""
+    from stzs.engine import latency_engine
+    S, P, eng = v0
+    e = latency_engine(S, eng.W, eng.device)
+    assert e.mrf_trio
+    tok, ref, eps, dur, seeds = bench.rank_inputs(S, B, 5)
+    nf = int(dur[0].sum())
+    dev = e.device
+    tok_d, ref_d, eps_d, dur_d = (t.to(dev) for t in (tok, ref, eps, dur))
+    host = lambda v: (v if torch.is_tensor(v) else v.t).detach().clone().cpu()
+
+    def fn():
+        return e.synth(tok_d, ref_d, steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG, noise=eps_d, durations=dur_d,
+                       seeds=seeds, n_frames=nf, check=False)
+    outs = {}
+    try:
+        for trio in (False, True):
+            e.mrf_trio = trio
+            e.launches = 0
+            outs[trio] = host(fn()["wav"])
+            if trio:
+                n_trio = e.launches
+            else:
+                n_seq = e.launches
+        assert torch.equal(outs[True], outs[False])
+        assert n_trio < n_seq - 30, (n_trio, n_seq)  # (2 stages x (4 x 3 - 4) convs + 2 x (5 x 3 - 4) statistics fewer)
+        g, o = e.capture(fn)
+        for rep in range(3):
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(host(o["wav"]), outs[False]), rep
+    finally:
+        e.mrf_trio = True
+    e.check_status()
+
+
 def test_latency_engine_enc_fork_bit_identical(v0):
     """the latency engine forks the text encoder and the prompt encoder onto two branches of its captured graph
     (stzs.engine.LATENCY_FORKS = {"enc"}: each branch on its own scratch): eager and graph-replayed synthesis must be

@@ -787,3 +787,52 @@ def test_abi_rejects_bad_shapes(eng):
     assert eng.lib.stzs_conv1d(C.byref(a), None) == -1
     a.ups, a.ks, a.pad, a.T_out, a.T_final = 0, 1, 0, 4, 0
     assert eng.lib.stzs_conv1d(C.byref(a), None) == -1
+
+
+@pytest.mark.parametrize("B,T,C,dil,res,trio", [(1, 1000, 256, 1, False, True), (1, 1000, 256, 5, True, True),
+                                               (1, 3001, 128, 3, False, True), (2, 700, 128, 5, True, True),
+                                               (1, 77, 128, 1, True, True), (48, 1400, 128, 1, False, False)])
+def test_mrf_trio_group_bit_identical(eng, B, T, C, dil, res, trio):
+    """stzs_conv1d_group on the k3 / k7 / k11 convs of one MRF layer (Snake AdaIN prologue, fused statistics, with and
+    without the residual; stage-0 256-channel and stage-1 128-channel inputs) vs three stzs_conv1d calls: outputs, the
+    statistics partials and their grouped finalisation (stzs_chan_stats_final_group) bit-identical.  Small batches run
+    as ONE launch (mrfv_trio; the library returns 1); at 48 utterances the 64-row form does not apply and the group
+    runs the three convs one after the other (returns 3), same bits."""
+    from stzs import _lib as L
+    g = torch.Generator().manual_seed(T + C + dil)
+    x = _act(torch.randn(B, T, C, generator=g).to("cuda:0", torch.bfloat16))
+    mean = (torch.randn(B, C, generator=g) * 0.1).cuda()
+    rstd = (torch.rand(B, C, generator=g) + 0.5).cuda()
+    gb = (torch.randn(B, 2 * C, generator=g) * 0.2).cuda()
+    al = (torch.rand(C, generator=g) + 0.5).cuda()
+    keep, convs = [], []
+    for k in (3, 7, 11):
+        w = torch.randn(C, C, k, generator=g) / math.sqrt(C * k)
+        cw, A = _pack(w, torch.randn(C, generator=g) * 0.1, frag32=True)
+        keep.append(A)
+        convs.append((cw, k))
+
+    def run(group):
+        ys, grp, sts = [], [], []
+        for cw, k in convs:
+            y = _act(torch.zeros(B, T, C, device="cuda:0", dtype=torch.bfloat16))
+            _, st = eng.conv(cw, x, y, pad=dil * (k - 1) // 2, dil=dil, pro=(mean, rstd, C, gb.data_ptr(), 2 * C, C),
+                             pro_act=L.ACT_SNAKE, pro_alpha=al, res=x if res else None,
+                             stats_key=f"trio.{group}.{k}", collect=grp if group else None)
+            ys.append(y)
+            sts.append(st)
+        if group:
+            arr = (L.ConvArgs * 3)(*grp)
+            n = eng.lib.stzs_conv1d_group(arr, 3, eng.stream())
+            assert n == (1 if trio else 3), n
+            eng._finalize_group([st[0].ref for st in sts])
+        torch.cuda.synchronize()
+        tens = lambda v: (v.tensor() if hasattr(v, "tensor") else v).clone()
+        return [y.t.clone() for y in ys], [(tens(st[0]), tens(st[1])) for st in sts]
+
+    y0, s0 = run(False)
+    y1, s1 = run(True)
+    for a, b in zip(y0, y1):
+        assert torch.equal(a, b)
+    for (m0, r0), (m1, r1) in zip(s0, s1):
+        assert torch.equal(m0, m1) and torch.equal(r0, r1)

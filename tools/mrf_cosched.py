@@ -1,7 +1,8 @@
 """Does running the three resblocks' convs of one MRF layer SIDE BY SIDE pay?  The stage-1 c1 convs of the k3 / k7 / k11
 resblocks (B = 64, T 24 001, 128 channels, dilation d) timed one after another on one stream vs. each on its own
 stream at once (the hardware queues interleave their workgroups on the CUs) -- an upper-bound probe for a one-launch
-"trio" form.  python tools/mrf_cosched.py   (env: B, D, REPS, STAGE=1|0)"""
+"trio" form.  python tools/mrf_cosched.py   (env: B, D, REPS, STAGE=1|0, GRAPH=1: both orders captured in a HIP graph
+-- at batch 1 the eager launches are host-bound)"""
 import math
 import os
 import sys
@@ -50,6 +51,51 @@ def run(i):
 for i in range(3):
     run(i)
 torch.cuda.synchronize()
+if os.environ.get("GRAPH", "0") == "1":
+    cur = torch.cuda.current_stream()
+    streams = [torch.cuda.Stream() for _ in range(3)]
+
+    def seq_body():
+        for i in range(3):
+            run(i)
+
+    def conc_body():
+        c = torch.cuda.current_stream()
+        for s in streams:
+            s.wait_stream(c)
+        for i, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                run(i)
+        for s in streams:
+            c.wait_stream(s)
+
+    def timed(body):
+        g = torch.cuda.CUDAGraph()
+        sg = torch.cuda.Stream()
+        sg.wait_stream(cur)
+        with torch.cuda.stream(sg):
+            with torch.cuda.graph(g, stream=sg):
+                for _ in range(REPS):
+                    body()
+        cur.wait_stream(sg)
+        g.replay()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(5):
+            g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / (5 * REPS) * 1e3
+
+    singles = []
+    for i in range(3):
+        singles.append(timed(lambda i=i: run(i)))
+    tseq, tconc = timed(seq_body), timed(conc_body)
+    print(f"[graph] stage T={T} C={C} B={B} d={D}: k3 / k7 / k11 alone {singles[0]:.1f} / {singles[1]:.1f} / "
+          f"{singles[2]:.1f} us (conv + statistics); one stream {tseq:.1f} us per layer; three branches {tconc:.1f} us "
+          f"({tseq / tconc:.3f}x)", flush=True)
+    sys.exit(0)
 ev = lambda: torch.cuda.Event(enable_timing=True)
 single = []
 for i in range(3):
