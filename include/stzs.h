@@ -204,10 +204,13 @@ int stzs_conv1d(const stzs_conv_args* a, void* stream);
  * the k3 / k7 / k11 convs of one generator MRF layer (a[0..2]: STZS_CONV_W_FRAG32, ks 3, 7, 11, Snake AdaIN prologue,
  * no acc_in, alpha 1, same B / T_out / Ci / Co / ci_pad / co_pad, all with or all without a residual, small grids --
  * each taking the 64-row tiles on its own, e.g. batch 1) run as ONE launch whose workgroups execute each problem's own
- * kernel body; anything else runs one stzs_conv1d after the other.  Outputs (and fused statistics partials) are
- * bit-identical to n stzs_conv1d calls either way.  Returns the number of kernel launches issued (1 or n), or a
- * negative STZS_E* code (from the first failing problem's checks).  (r06: no reference counterpart -- the
- * reference's generator runs its resblocks one conv at a time) */
+ * kernel body; two generic-path bf16 convs that would each take the DEEP split-K form with its combine launch (splitk
+ * = ci_pad / cic, same shape / slice count / prologue activation: the prosody predictor's F0 and N branches at batch 1,
+ * each with its OWN splitk_ws) share one conv launch and one combine launch; anything else runs one stzs_conv1d after
+ * the other.  Outputs (and fused statistics partials) are bit-identical to n stzs_conv1d calls either way.  Returns 1
+ * when the problems shared their launches, n when they ran one after the other, or a negative STZS_E* code (from the
+ * first failing problem's checks; the problems before it have been launched).  (r06: no reference counterpart -- the
+ * reference runs these convs one at a time) */
 int stzs_conv1d_group(const stzs_conv_args* a, int n, void* stream);
 
 /* ---- InstanceNorm statistics over time, per (b, c): mean and 1/sqrt(var + eps) -----------

@@ -35,8 +35,10 @@ namespace {
 // SKE (with DEEP): the slice stores its fp32 partial tile row-major into its slab and ends; the combine and the fused
 // epilogue run in splitk_epi, a second launch spread over 8 workgroups per tile (the last-arriver combine read every
 // other slice's 64-KB slab through ONE workgroup: 7.5 us of a 24-us batch-1 decoder conv, tools/conv_phase.py).
+// (r06) the body as an always-inlined device function of (arguments by value, split-K slice zs): conv_mfma is this
+// body with zs = grid z, conv_mfma_pair two problems' bodies in one launch.
 template <typename TIn, typename TOut, bool FLAT, int PACT, bool DEEP = false, bool SKE = false>
-__global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_args a) {
+STZS_DEV void conv_body(const stzs_conv_args a, const int zs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int cic = a.cic;
     const int pitch = cic * 2 + 16;
@@ -80,8 +82,8 @@ __global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_
     // Slice z takes chunks [z n / S, (z+1) n / S): equal slices when S divides n, otherwise sizes differing by one
     // (the decoder / predictor AdaIN convs of the batch-1 engine: 9 chunks in 3 or 4 slices)
     const int SKr = a.splitk > 1 ? a.splitk : 1;
-    const int cc_lo = SKr > 1 ? (int)blockIdx.z * nchunk / SKr : 0;
-    const int cc_hi = SKr > 1 ? ((int)blockIdx.z + 1) * nchunk / SKr : nchunk;
+    const int cc_lo = SKr > 1 ? zs * nchunk / SKr : 0;
+    const int cc_hi = SKr > 1 ? (zs + 1) * nchunk / SKr : nchunk;
     const int k_lo = cc_lo * ks * kpc, k_hi = cc_hi * ks * kpc;
 
     auto fill = [&](int k) {
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_
                     ep[(wt * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP_PITCH + wc * 64 + nt * 16 + (lane & 15)] = acc[mt][nt][r];
         __syncthreads();
         const long tile = (long)by * gridDim.x + bx;
-        float* slab = reinterpret_cast<float*>(a.splitk_ws) + (tile * SKr + blockIdx.z) * (long)(BT * BCO);
+        float* slab = reinterpret_cast<float*>(a.splitk_ws) + (tile * SKr + zs) * (long)(BT * BCO);
         const long rows_left = FLAT ? (long)a.B * a.T_out - row0 : (long)(a.T_out - t0);
         const int nrow = rows_left < BT ? (int)rows_left : BT;
         for (int e = tid; e < nrow * (BCO / 4); e += NTHR) {
@@ -283,7 +285,7 @@ __global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_
         CPROF_RT(14)
         return;
     }
-    if (SKr > 1 && !splitk_combine_rt<BT, DEEP ? 4 : 1>(a, acc, smem, SKr)) {
+    if (SKr > 1 && !splitk_combine_rt<BT, DEEP ? 4 : 1>(a, acc, smem, SKr, zs)) {
         CPROF_RT(14)
         return;
     }
@@ -299,17 +301,33 @@ __global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_
 #endif
 }
 
+template <typename TIn, typename TOut, bool FLAT, int PACT, bool DEEP = false, bool SKE = false>
+__global__ __launch_bounds__(NTHR, DEEP ? 1 : 2) void conv_mfma(const stzs_conv_args a) {
+    conv_body<TIn, TOut, FLAT, PACT, DEEP, SKE>(a, blockIdx.z);
+}
+
+// (r06) two independent DEEP split-K convs of one shape (the prosody predictor's F0 and N branches at batch 1) in one
+// launch: grid z < splitk runs problem 0's slice z, the rest problem 1's -- each workgroup the single-problem body, so
+// every slab holds the bits of its own launch; splitk_epi_pair combines them.
+template <typename TIn, typename TOut, int PACT>
+__global__ __launch_bounds__(NTHR, 1) void conv_mfma_pair(const stzs_conv_args a0, const stzs_conv_args a1) {
+    const int SK = a0.splitk;
+    if ((int)blockIdx.z < SK)
+        conv_body<TIn, TOut, false, PACT, true, true>(a0, blockIdx.z);
+    else
+        conv_body<TIn, TOut, false, PACT, true, true>(a1, (int)blockIdx.z - SK);
+}
+
 // splitk_combine with the slice count at run time (conv_mfma): the same slabs, ticket and slice-order sum, the
 // slices loaded one at a time (no [SK][NV] register block).
 template <int BTM, int RB>
-STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK) {
+STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK, int z) {
     constexpr int NV = BTM / 32 * 4;
     constexpr int SLAB = NV * NTHR * 16;
     const int tid = threadIdx.x;
     const long tile = blockIdx.x + (long)gridDim.x * blockIdx.y;
     unsigned char* base = reinterpret_cast<unsigned char*>(a.splitk_ws) + tile * (long)SK * SLAB;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(base, 0, SK * SLAB, 0x00020000);
-    const int z = blockIdx.z;
 #pragma unroll
     for (int i = 0; i < NV; ++i)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i >> 2][i & 3]), wr,
@@ -357,7 +375,7 @@ STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][
 // stored values per 64-row half (one deterministic fp32 partial per (utterance, 64-row chunk, channel), reduced
 // lanes -> waves in a fixed order).
 template <typename TOut, bool FLAT>
-__global__ __launch_bounds__(NTHR) void splitk_epi(const stzs_conv_args a, int SK) {
+STZS_DEV void splitk_epi_body(const stzs_conv_args a, const int SK) {
     __shared__ float red[4][2][8][2];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int bx = blockIdx.x, by = blockIdx.y >> 3, cg = blockIdx.y & 7;
@@ -490,6 +508,20 @@ __global__ __launch_bounds__(NTHR) void splitk_epi(const stzs_conv_args a, int S
     }
 }
 
+template <typename TOut, bool FLAT>
+__global__ __launch_bounds__(NTHR) void splitk_epi(const stzs_conv_args a, int SK) {
+    splitk_epi_body<TOut, FLAT>(a, SK);
+}
+
+// (r06) the combines of a conv_mfma_pair launch: grid z picks the problem
+template <typename TOut>
+__global__ __launch_bounds__(NTHR) void splitk_epi_pair(const stzs_conv_args a0, const stzs_conv_args a1, int SK) {
+    if (blockIdx.z == 0)
+        splitk_epi_body<TOut, false>(a0, SK);
+    else
+        splitk_epi_body<TOut, false>(a1, SK);
+}
+
 size_t lds_bytes(int rows_in, int cic, int nslot = NSLOT) {
     const size_t main = (((size_t)rows_in * (cic * 2 + 16) + 15) & ~(size_t)15) + (size_t)nslot * SLOT_BYTES + 4 * 128 * 4;
     const size_t epi = (size_t)BT * EP_PITCH * 4 + 2 * BCO * 4 + 2 * 4 * BCO * 2 * 4;
@@ -566,13 +598,51 @@ int launch_dt(const stzs_conv_args& a, hipStream_t s) {
     }
 }
 
+// (r06) two problems as ONE conv_mfma_pair + ONE splitk_epi_pair launch where each would take the DEEP split-K form with
+// the splitk_epi combine on its own (not flat; the batch-1 predictor / decoder AdaIN-block convs) with the same
+// prologue activation, grid, slice count and LDS; otherwise STZS_ESHAPE (nothing launched).
+template <typename TIn, typename TOut>
+int launch_pair_dt(const stzs_conv_args* p, hipStream_t s) {
+    size_t lds = 0;
+    for (int i = 0; i < 2; ++i) {
+        const stzs_conv_args& a = p[i];
+        const bool flat = (a.ks == 1 && a.stride == 1 && a.pad == 0 && a.ups == 0 && a.pro_mode == STZS_PRO_NONE &&
+                           a.pro_act == STZS_ACT_NONE && a.T_in == a.T_out);
+        const int rows_in = (BT - 1) * a.stride + (a.ks - 1) * a.dil + 1;
+        const int nslot_deep = a.ks * (a.cic >> 5);
+        const bool deep = !flat && a.splitk > 1 && a.splitk == a.ci_pad / a.cic && !(a.flags & STZS_CONV_RING) &&
+                          lds_bytes(rows_in, a.cic, nslot_deep) <= 160 * 1024;
+        const bool ske = deep && epi_vec(a) && a.ups == 0 && !(a.flags & (STZS_CONV_SK_TICKET | STZS_CONV_A_DMA));
+        if (!ske || a.splitk > 16 || !a.splitk_ws || !a.splitk_ctr || !stzs_aligned(a.splitk_ws, 16) ||
+            !stzs_aligned(a.splitk_ctr, 4))
+            return STZS_ESHAPE;
+        const size_t l = lds_bytes(rows_in, a.cic, nslot_deep);
+        if (i == 0) lds = l;
+        if (i == 1 && (l != lds || a.splitk != p[0].splitk || a.pro_act != p[0].pro_act || a.B != p[0].B ||
+                       a.T_out != p[0].T_out || a.co_pad != p[0].co_pad))
+            return STZS_ESHAPE;
+    }
+    const stzs_conv_args& a = p[0];
+    void (*k)(stzs_conv_args, stzs_conv_args) = a.pro_act == STZS_ACT_LEAKY ? conv_mfma_pair<TIn, TOut, STZS_ACT_LEAKY>
+                                               : a.pro_act == STZS_ACT_SNAKE ? conv_mfma_pair<TIn, TOut, STZS_ACT_SNAKE>
+                                                                             : conv_mfma_pair<TIn, TOut, STZS_ACT_NONE>;
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dim3 grid((unsigned)a.B * (unsigned)((a.T_out + BT - 1) / BT), a.co_pad / BCO, 2 * a.splitk);
+    hipLaunchKernelGGL(k, grid, dim3(NTHR), lds, s, p[0], p[1]);
+    STZS_LAUNCH_CHECK();
+    hipLaunchKernelGGL(splitk_epi_pair<TOut>, dim3(grid.x, grid.y * 8, 2), dim3(NTHR), 0, s, p[0], p[1], (int)a.splitk);
+    STZS_LAUNCH_CHECK();
+    return STZS_OK;
+}
+
 }  // namespace
 
 int stzs_mrf_conv_launch(const stzs_conv_args& a, hipStream_t s);     // csrc/mrf.hip
 int stzs_narrow_conv_launch(const stzs_conv_args& a, hipStream_t s);  // csrc/mrf.hip
 
-// the dispatcher proper; csrc/dispatch.hip routes the register-direct MRF form before it
-__attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args* a, void* stream) {
+namespace {
+
+int core_checks(const stzs_conv_args* a) {
     if (!a || !a->x || !a->w || !a->y) return STZS_EINVAL;
     if (a->cic != 32 && a->cic != 64 && a->cic != 128) return STZS_EINVAL;
     if (a->B <= 0 || a->T_in <= 0 || a->T_out <= 0 || a->Ci <= 0 || a->Co <= 0 || a->ks <= 0 || a->dil <= 0 ||
@@ -605,6 +675,31 @@ __attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args*
     if (a->pro_act == STZS_ACT_SNAKE && !a->pro_alpha) return STZS_EINVAL;
     if (a->stat_part && (a->ups > 0 || !epi_vec(*a) || a->stat_ld < a->Co || !stzs_aligned(a->stat_part, 8)))
         return STZS_EINVAL;
+    return STZS_OK;
+}
+
+}  // namespace
+
+// (r06) two generic-path problems in one conv_mfma_pair + splitk_epi_pair launch (stzs_conv1d_group, n = 2): each must
+// pass stzs_conv1d's checks, be bf16 -> bf16 without a W_* / ROWS / A_DMA flag and take the DEEP split-K form with the
+// splitk_epi combine on its own; STZS_ESHAPE otherwise (nothing launched: the caller runs them one at a time).
+__attribute__((visibility("hidden"))) int stzs_conv_pair_launch(const stzs_conv_args* p, hipStream_t s) {
+    constexpr int WF = STZS_CONV_W_X3 | STZS_CONV_W_F32 | STZS_CONV_W_LANE16 | STZS_CONV_W_NARROW32 | STZS_CONV_W_FRAG32 |
+                       STZS_CONV_W_FRAG32X3 | STZS_CONV_ROWS | STZS_CONV_A_DMA | STZS_CONV_UPS_NOISE;
+    for (int i = 0; i < 2; ++i) {
+        const int rc = core_checks(&p[i]);
+        if (rc != STZS_OK) return rc;
+        if ((p[i].flags & WF) || p[i].in_dtype != STZS_BF16 || p[i].out_dtype != STZS_BF16) return STZS_ESHAPE;
+    }
+    return launch_pair_dt<bf16_t, bf16_t>(p, s);
+}
+
+// the dispatcher proper; csrc/dispatch.hip routes the register-direct MRF form before it
+__attribute__((visibility("hidden"))) int stzs_conv1d_core(const stzs_conv_args* a, void* stream) {
+    {
+        const int rc = core_checks(a);
+        if (rc != STZS_OK) return rc;
+    }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (a->in_dtype == STZS_F8) {
         const bool lin = a->ks == 1 && a->stride == 1 && a->pad == 0 && a->ups == 0 && a->T_in == a->T_out &&

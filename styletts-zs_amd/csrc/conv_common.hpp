@@ -341,7 +341,7 @@ STZS_DEV void epilogue_act(const stzs_conv_args& a, const float* ep, const float
 }
 
 template <int BTM, int RB = 1>
-STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK);
+STZS_DEV bool splitk_combine_rt(const stzs_conv_args& a, f32x4 (&acc)[BTM / 32][4], unsigned char* smem, int SK, int z);
 // EP: the epilogue variant compiled into the calling kernel.  -1: all of them behind runtime tests (the conv kernels);
 // 0..15: ONE vectorised variant, HR = bit 0, HA = bit 1, activation index (ep_act) = bits 2-3 (the GEMM kernels:
 // with all twenty variants inlined a gemm_glds instance was ~73 k instructions and its epilogue ran from a cold

@@ -10,6 +10,7 @@ int stzs_rows_gemm_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/ro
 int stzs_mrfx_conv_launch(const stzs_conv_args& a, hipStream_t s);    // csrc/mrfx.hip
 
 int stzs_mrfv_trio_launch(const stzs_conv_args* a, hipStream_t s);   // csrc/mrfv.hip
+int stzs_conv_pair_launch(const stzs_conv_args* a, hipStream_t s);    // csrc/conv.hip
 
 namespace {
 
@@ -38,6 +39,11 @@ extern "C" int stzs_conv1d_group(const stzs_conv_args* a, int n, void* stream) {
         a[2].ups <= 0 && frag32_checks(&a[0]) == STZS_OK && frag32_checks(&a[1]) == STZS_OK &&
         frag32_checks(&a[2]) == STZS_OK) {
         const int rc = stzs_mrfv_trio_launch(a, reinterpret_cast<hipStream_t>(stream));
+        if (rc == STZS_OK) return 1;
+        if (rc != STZS_ESHAPE) return rc;
+    }
+    if (n == 2 && !a[0].pro_part == !a[1].pro_part) {  // (pro_part: both or neither, as the body reads it uniformly)
+        const int rc = stzs_conv_pair_launch(a, reinterpret_cast<hipStream_t>(stream));
         if (rc == STZS_OK) return 1;
         if (rc != STZS_ESHAPE) return rc;
     }

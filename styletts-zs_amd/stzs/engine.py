@@ -272,6 +272,9 @@ class StyleTTSZS:
         # (r06) small batches (<= 4 utterances): the generator MRF's three resblocks advanced side by side, each layer's
         # three convs in one launch (stzs_conv1d_group, csrc/mrfv.hip mrfv_trio) -- bit-identical; STZS_MRF_TRIO=0: off
         self.mrf_trio = os.environ.get("STZS_MRF_TRIO", "1") != "0"
+        # (r06) the batch-1 engine (blk_splitk): the prosody predictor's F0 and N branches in lockstep, each conv pair
+        # in one launch pair (stzs_conv1d_group -> conv_mfma_pair) -- bit-identical; STZS_F0N_PAIR=0: off
+        self.f0n_pair = os.environ.get("STZS_F0N_PAIR", "1") != "0"
         # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
         # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
@@ -503,12 +506,13 @@ class StyleTTSZS:
             # per tile (grid.x is at most B x ceil(T_out / 128))
             tiles = x.B * ((a.T_out + 127) // 128) * (cw.co_pad // 128)
             a.splitk = splitk
-            a.splitk_ws = self._scratch("csk_ws", tiles * splitk * 16384).data_ptr()
-            a.splitk_ctr = self._counters("csk_ctr", tiles).data_ptr()
+            gs = f".g{len(collect)}" if collect is not None else ""  # (a collected problem: its own slabs)
+            a.splitk_ws = self._scratch("csk_ws" + gs, tiles * splitk * 16384).data_ptr()
+            a.splitk_ctr = self._counters("csk_ctr" + gs, tiles).data_ptr()
         if pro_ref is not None:
             generic = not (a.flags & (8 | L.CONV_ROWS | L.CONV_W_X3 | L.CONV_W_F32 | L.CONV_W_FRAG32 |
                                       L.CONV_W_LANE16 | L.CONV_W_NARROW32 | L.CONV_W_FRAG32X3)) and not cw.f8
-            if generic and pre_ln is None:  # the prologue finalises the partials itself
+            if generic and pre_ln is None and pro_ref.nch <= 8:  # the prologue finalises the partials itself
                 a.pro_part, a.pro_ld, a.pro_nch, a.pro_T, a.pro_eps = pro_ref.part.data_ptr(), pro_ref.ld, pro_ref.nch, \
                     pro_ref.T, 1e-5
             else:
@@ -1218,6 +1222,21 @@ class StyleTTSZS:
         c0, c1, c2 = S.f0n_ch
 
         s0 = self.stats(xs, "pr.xs.s1")  # (both branches' first AdaIN normalise xs: its statistics once, r06)
+        bs = self.branch_streams
+        forked = bs is True or (isinstance(bs, (set, frozenset)) and "f0n" in bs)
+        if self.f0n_pair and self.blk_splitk and not forked:
+            # (r06) the two branches in lockstep, each block's two convs of both branches as one launch pair
+            # (stzs_conv1d_group -> conv_mfma_pair / splitk_epi_pair): same bits as branch after branch
+            ys = {br: (self.act(f"pr.{br}.y0", B, T40, c0, self.adt), self.act(f"pr.{br}.y1", B, T80, c1, self.adt),
+                       self.act(f"pr.{br}.y2", B, T80, c2, self.adt)) for br in ("f0", "n")}
+            ins = {"f0": xs, "n": xs}
+            for i in range(3):
+                self._blk_pair([(W.pr_blk[f"pr.{br}{i}"], ins[br], ys[br][i], f"pr.{br}{i}", s0 if i == 0 else None)
+                                for br in ("f0", "n")], ng, gbp, self.adt)
+                ins = {br: ys[br][i] for br in ("f0", "n")}
+            for br, out in (("f0", F0), ("n", Nn)):
+                self.conv(W.pr_blk[f"pr.{br}_proj"], ys[br][2], Act(out, 0, 1), what=f"pr.{br}_proj")
+            return F0[:, :, 0], Nn[:, :, 0]
 
         def branch(br, out):
             y0 = self.act(f"pr.{br}.y0", B, T40, c0, self.adt)
@@ -1274,6 +1293,54 @@ class StyleTTSZS:
                   pro_slope=0.2, res=res, res_tdiv=2 if bw.up else 1, alpha=1.0 / math.sqrt(2.0), splitk=sk,
                   what=key + ".conv2")
         return out
+
+    def _blk_pair(self, items, ng, gb: torch.Tensor, dt):
+        """blk() for two independent blocks of the same shape (items: (bw, x, out, key, s1) each), advanced side by
+        side: statistics, upsampling and shortcuts one block after the other, each conv pair collected into one
+        stzs_conv1d_group call (the library pairs the batch-1 DEEP split-K convs, else runs them in turn)."""
+        gbase, gbs = gb.data_ptr(), ng.total
+        sk = self.blk_splitk if dt == torch.bfloat16 else 0
+        st = []
+        for bw, x, out, key, s1 in items:
+            m1, r1, sb1 = s1 if s1 is not None else self.stats(x, key + ".s1")
+            st.append((m1, r1, sb1))
+        grp, st2, rs = [], [], []
+        for (bw, x, out, key, _), (m1, r1, sb1) in zip(items, st):
+            off1, n1 = ng.offsets[bw.name + ".norm1"]
+            c1 = bw.conv1s if (sk and bw.conv1s is not None) else bw.conv1
+            To = 2 * x.T if bw.up else x.T
+            r = self.act(key + ".r", x.B, To, bw.dout, dt)
+            rs.append(r)
+            if bw.up:
+                u = self.act(key + ".u", x.B, To, bw.din, dt)
+                a = L.DwupArgs()
+                a.x, a.y, a.mean, a.rstd, a.gb = x.ptr, u.ptr, m1.data_ptr(), r1.data_ptr(), gbase + off1 * 4
+                a.w, a.wb = self.W.t(bw.pool_w).data_ptr(), self.W.t(bw.pool_b).data_ptr()
+                a.ldx, a.bsx, a.ldy, a.bsy, a.stat_bs, a.gb_bs, a.gb_beta_off = x.ld, x.bs, u.ld, u.bs, sb1, gbs, n1
+                a.B, a.T, a.C, a.slope, a.dtype = x.B, x.T, bw.din, 0.2, x.dt
+                self._call(self.lib.stzs_adain_dwup, a, key + ".dwup")
+                _, s2 = self.conv(c1, u, r, pad=1, stats_key=key + ".s2", splitk=sk, collect=grp, what=key + ".conv1")
+            else:
+                _, s2 = self.conv(c1, x, r, pad=1, pro=(m1, r1, sb1, gbase + off1 * 4, gbs, n1), pro_act=L.ACT_LEAKY,
+                                  pro_slope=0.2, stats_key=key + ".s2", splitk=sk, collect=grp, what=key + ".conv1")
+            st2.append(s2)
+        self._launch_group(grp, "blk.conv1")
+        res = []
+        for bw, x, out, key, _ in items:
+            if bw.sc is not None:
+                scb = self.act(key + ".sc", x.B, x.T, bw.dout, dt)
+                self.conv(bw.scs if (sk and bw.scs is not None) else bw.sc, x, scb, splitk=sk, what=key + ".sc")
+                res.append(scb)
+            else:
+                res.append(x)
+        grp = []
+        for (bw, x, out, key, _), (m2, r2, sb2), r, rr in zip(items, st2, rs, res):
+            off2, n2 = ng.offsets[bw.name + ".norm2"]
+            c2 = bw.conv2s if (sk and bw.conv2s is not None) else bw.conv2
+            self.conv(c2, r, out, pad=1, pro=(m2, r2, sb2, gbase + off2 * 4, gbs, n2), pro_act=L.ACT_LEAKY,
+                      pro_slope=0.2, res=rr, res_tdiv=2 if bw.up else 1, alpha=1.0 / math.sqrt(2.0), splitk=sk,
+                      collect=grp, what=key + ".conv2")
+        self._launch_group(grp, "blk.conv2")
 
     # ------------------------------------------------------------------ (c) decoder
     def decode(self, pro: dict, codes: torch.Tensor, seeds, istft=True) -> torch.Tensor:

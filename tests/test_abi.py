@@ -176,7 +176,7 @@ def test_groups_reject_before_launch():
     a = (_lib.ConvArgs * 3)()
     assert L.stzs_conv1d_group(None, 3, None) == E
     assert L.stzs_conv1d_group(a, 0, None) == E and L.stzs_conv1d_group(a, 4, None) == E
-    assert L.stzs_conv1d_group(a, 3, None) == E  # NULL x / w / y
+    assert L.stzs_conv1d_group(a, 3, None) == E and L.stzs_conv1d_group(a, 2, None) == E  # NULL x / w / y
     for p in a:
         p.x, p.w, p.y, p.flags = 0x1000, 0x2000, 0x3000, _lib.CONV_W_FRAG32
     assert L.stzs_conv1d_group(a, 3, None) == S  # empty shapes: the first problem's own checks

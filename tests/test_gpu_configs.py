@@ -470,6 +470,46 @@ def test_mrf_trio_synth_bit_identical(v0, B):
     e.check_status()
 
 
+def test_f0n_pair_synth_bit_identical(v0):
+    """the batch-1 engine runs the prosody predictor's F0 and N branches in lockstep (engine.f0n_pair: each block's
+    conv pair as one conv_mfma_pair + splitk_epi_pair launch): F0, N and the waveform of an eager and of a
+    graph-replayed synthesis must be the same bits as branch after branch."""
+    from stzs.engine import latency_engine
+    S, P, eng = v0
+    e = latency_engine(S, eng.W, eng.device)
+    assert e.f0n_pair and e.blk_splitk
+    tok, ref, eps, dur, seeds = bench.rank_inputs(S, 1, 9)
+    nf = int(dur[0].sum())
+    dev = e.device
+    tok_d, ref_d, eps_d, dur_d = (t.to(dev) for t in (tok, ref, eps, dur))
+    keys = ("F0", "N", "wav")
+    host = lambda v: (v if torch.is_tensor(v) else v.t).detach().clone().cpu()
+
+    def fn():
+        return e.synth(tok_d, ref_d, steps=bench.STEPS_LATENCY, cfg_scale=bench.CFG, noise=eps_d, durations=dur_d,
+                       seeds=seeds, n_frames=nf, check=False)
+    outs, nl = {}, {}
+    try:
+        for pair in (False, True):
+            e.f0n_pair = pair
+            e.launches = 0
+            o = fn()
+            outs[pair] = {k: host(o[k]) for k in keys}
+            nl[pair] = e.launches
+        for k in keys:
+            assert torch.equal(outs[True][k], outs[False][k]), k
+        assert nl[True] <= nl[False] - 6, nl  # (6 block-conv pairs)
+        g, o = e.capture(fn)
+        for rep in range(3):
+            g.replay()
+            torch.cuda.synchronize()
+            for k in keys:
+                assert torch.equal(host(o[k]), outs[False][k]), (rep, k)
+    finally:
+        e.f0n_pair = True
+    e.check_status()
+
+
 def test_latency_engine_enc_fork_bit_identical(v0):
     """the latency engine forks the text encoder and the prompt encoder onto two branches of its captured graph
     (stzs.engine.LATENCY_FORKS = {"enc"}: each branch on its own scratch): eager and graph-replayed synthesis must be

@@ -836,3 +836,55 @@ def test_mrf_trio_group_bit_identical(eng, B, T, C, dil, res, trio):
         assert torch.equal(a, b)
     for (m0, r0), (m1, r1) in zip(s0, s1):
         assert torch.equal(m0, m1) and torch.equal(r0, r1)
+
+
+@pytest.mark.parametrize("B,T,Ci,Co,res,pair", [(1, 100, 512, 512, False, True), (1, 200, 512, 256, True, True),
+                                               (2, 130, 256, 512, True, True), (1, 100, 512, 512, False, False)])
+def test_conv_pair_group_bit_identical(eng, B, T, Ci, Co, res, pair):
+    """stzs_conv1d_group on two independent DEEP split-K convs (AdaIN + LeakyReLU prologue, k 3, fused statistics,
+    with and without the residual; the prosody predictor's F0 / N block convs at batch 1) vs two stzs_conv1d calls:
+    outputs and statistics bit-identical.  One conv_mfma_pair + one splitk_epi_pair launch (the library returns 1);
+    with different slice counts (last case: 4 vs 2 slices) the two run one after the other (returns 2), same bits."""
+    from stzs import _lib as L
+    g = torch.Generator().manual_seed(T + Ci + Co)
+    xs = [_act(torch.randn(B, T, Ci, generator=g).to("cuda:0", torch.bfloat16)) for _ in range(2)]
+    rs = [_act(torch.randn(B, T, Co, generator=g).to("cuda:0", torch.bfloat16)) if res else None for _ in range(2)]
+    pros = []
+    for _ in range(2):
+        mean = (torch.randn(B, Ci, generator=g) * 0.1).cuda()
+        rstd = (torch.rand(B, Ci, generator=g) + 0.5).cuda()
+        gb = (torch.randn(B, 2 * Ci, generator=g) * 0.2).cuda()
+        pros.append((mean, rstd, gb))
+    keep, convs = [], []
+    for _ in range(2):
+        w = torch.randn(Co, Ci, 3, generator=g) / math.sqrt(Ci * 3)
+        cw, A = _pack(w, torch.randn(Co, generator=g) * 0.1)
+        keep.append(A)
+        convs.append(cw)
+    sks = (16, 16) if pair else (16, 2)
+
+    def run(group):
+        ys, grp, sts = [], [], []
+        for i in range(2):
+            mean, rstd, gb = pros[i]
+            y = _act(torch.zeros(B, T, Co, device="cuda:0", dtype=torch.bfloat16))
+            _, st = eng.conv(convs[i], xs[i], y, pad=1, pro=(mean, rstd, Ci, gb.data_ptr(), 2 * Ci, Ci),
+                             pro_act=L.ACT_LEAKY, pro_slope=0.2, res=rs[i], alpha=0.7, stats_key=f"pair.{group}.{i}",
+                             splitk=sks[i], collect=grp if group else None)
+            ys.append(y)
+            sts.append(st)
+        if group:
+            arr = (L.ConvArgs * 2)(*grp)
+            n = eng.lib.stzs_conv1d_group(arr, 2, eng.stream())
+            assert n == (1 if pair else 2), n
+            eng._finalize_group([st[0].ref for st in sts])
+        torch.cuda.synchronize()
+        tens = lambda v: (v.tensor() if hasattr(v, "tensor") else v).clone()
+        return [y.t.clone() for y in ys], [(tens(st[0]), tens(st[1])) for st in sts]
+
+    y0, s0 = run(False)
+    y1, s1 = run(True)
+    for a, b in zip(y0, y1):
+        assert torch.equal(a, b)
+    for (m0, r0), (m1, r1) in zip(s0, s1):
+        assert torch.equal(m0, m1) and torch.equal(r0, r1)
