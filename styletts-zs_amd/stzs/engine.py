@@ -1304,6 +1304,9 @@ class StyleTTSZS:
         for bw, x, out, key, s1 in items:
             m1, r1, sb1 = s1 if s1 is not None else self.stats(x, key + ".s1")
             st.append((m1, r1, sb1))
+        refs = [m.ref for m, _, _ in st if isinstance(m, _StatPtr) and not m.ref.done]
+        if len(refs) == len(items) and len({id(r) for r in refs}) == len(refs) and all(it[0].up for it in items):
+            self._finalize_group(refs)  # (the upsampling blocks' dwup reads mean / rstd: both finalised in one launch)
         grp, st2, rs = [], [], []
         for (bw, x, out, key, _), (m1, r1, sb1) in zip(items, st):
             off1, n1 = ng.offsets[bw.name + ".norm1"]
