@@ -1124,8 +1124,9 @@ class StyleTTSZS:
         return self.duration_head(d, ov)
 
     def duration_encoder(self, h_txt: Act, codes: torch.Tensor, durations=None):
-        """a5: DurationEncoder (LSTM + AdaLN layers) -> (d [B, T, pr_in], the given durations as the int32
-        device buffer pr.dur_ov, or None)."""
+        """a5: DurationEncoder (LSTM + AdaLN layers) -> (d [B, T, pr_in], the given durations as an int32 device
+        tensor -- the caller's own when it is one (contiguous [B, T]: read in place, stream-ordered), else the copy
+        pr.dur_ov -- or None)."""
         S, W = self.spec, self.W
         B, T = h_txt.B, h_txt.T
         pin = S.pr_in
@@ -1147,11 +1148,15 @@ class StyleTTSZS:
                        bs=2 * S.pr_hid, gdiv=1, gadd=1.0, what=f"pr.adaln{i}")
         ov = None
         if durations is not None:
-            ov = self.buf("pr.dur_ov", (B, T), torch.int32)
-            if durations.device.type == "cpu":
-                ov.copy_(durations.to(torch.int32))
-            elif durations.data_ptr() != ov.data_ptr():
-                ov.copy_(durations)
+            if (durations.device.type != "cpu" and durations.dtype == torch.int32 and durations.is_contiguous() and
+                    tuple(durations.shape) == (B, T)):
+                ov = durations  # (read only by the alignment and the durations kernel: no device copy, r06)
+            else:
+                ov = self.buf("pr.dur_ov", (B, T), torch.int32)
+                if durations.device.type == "cpu":
+                    ov.copy_(durations.to(torch.int32))
+                elif durations.data_ptr() != ov.data_ptr():
+                    ov.copy_(durations)
         return xin, ov
 
     def duration_head(self, d: Act, ov=None, hd: Act = None) -> dict:
