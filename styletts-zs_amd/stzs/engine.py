@@ -275,6 +275,8 @@ class StyleTTSZS:
         # (r06) the batch-1 engine (blk_splitk): the prosody predictor's F0 and N branches in lockstep, each conv pair
         # in one launch pair (stzs_conv1d_group -> conv_mfma_pair) -- bit-identical; STZS_F0N_PAIR=0: off
         self.f0n_pair = os.environ.get("STZS_F0N_PAIR", "1") != "0"
+        # (r06) the denoiser layers' cross-attention K / V projections as one stacked linear; STZS_KV_FUSE=0: per layer
+        self.kv_fuse = os.environ.get("STZS_KV_FUSE", "1") != "0"
         # the per-utterance linears (one row per utterance or per sigma step: the sigma-embedding MLP, the pooled-
         # prompt projection, the decoder / predictor AdaIN gamma-beta GEMMs) on the whole-chip small-M form at every
         # batch size (a per-weight choice: batch-invariant); on the tiled GEMM they ran on 1-4 workgroups each.
@@ -960,10 +962,18 @@ class StyleTTSZS:
             a.B, a.R, a.C, a.in_dtype, a.out_dtype = B, 1, d, L.F32, L.F32
             self._call(self.lib.stzs_copy2d, a, "pool_null")
         kv = []
-        for l, lw in enumerate(W.dn_layers):
-            kvl = self.act(f"dn.kv{l}", R, Lc, 2 * d, self.sdt)
-            self.conv(lw["kv"], ctx, kvl, what=f"dn.kv{l}")
-            kv.append(kvl)
+        if getattr(W, "dn_kv_all", None) is not None and self.kv_fuse:
+            # (r06) all layers' K / V of the shared context in one linear (weights.py dn_kv_all); layer l's [K | V] are
+            # channels [2 d l, 2 d (l + 1)) of its rows
+            nl = len(W.dn_layers)
+            kva = self.act("dn.kv_all", R, Lc, 2 * d * nl, self.sdt)
+            self.conv(W.dn_kv_all, ctx, kva, what="dn.kv")
+            kv = [Act(kva.t, 2 * d * l, 2 * d) for l in range(nl)]
+        else:
+            for l, lw in enumerate(W.dn_layers):
+                kvl = self.act(f"dn.kv{l}", R, Lc, 2 * d, self.sdt)
+                self.conv(lw["kv"], ctx, kvl, what=f"dn.kv{l}")
+                kv.append(kvl)
         # sigma embeddings for all steps
         fkey = ("dn.four", tuple(float(v) for v in sigmas))
         fo = self._consts.get(fkey)

@@ -529,6 +529,13 @@ class PackedModel:
             for key, n in (("qkv", ".sa_qkv"), ("o", ".sa_o"), ("q", ".ca_q"), ("co", ".ca_o"), ("ff1", ".ff1"),
                            ("ff2", ".ff2")):
                 self.dn_layers[-1][key + "8"] = pack_conv_f8(A, p + n + ".f8", P[p + n + ".w"], P[p + n + ".b"])
+        # (r06) every layer's cross-attention K / V projection of the one shared context as ONE linear: the layers'
+        # [2 d, d] weights stacked along the output channels (2 d is a multiple of the 128-column tile, so each tile is
+        # the K-step stream of its own layer's linear: the same bits, one launch instead of dn_layers)
+        kvw = [P[f"dn.l{l}.ca_kv.w"] for l in range(S.dn_layers)]
+        kvb = [P[f"dn.l{l}.ca_kv.b"] for l in range(S.dn_layers)]
+        self.dn_kv_all = pack_conv(A, "dn.ca_kv_all", torch.cat(kvw), torch.cat(kvb), x3=xdn) \
+            if (2 * d) % 128 == 0 else None
         # --- predictor ---
         self.pr_de = [pack_lstm(A, f"pr.de{i}", P, x3=xa) for i in range(S.pr_layers)]
         self.pr_aln = [L(f"pr.de{i}.aln") for i in range(S.pr_layers)]
