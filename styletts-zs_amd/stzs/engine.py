@@ -1150,12 +1150,22 @@ class StyleTTSZS:
         a.f32 = int(self.adt == torch.float32)
         self._call(self.lib.stzs_predictor_prep, a, "pr_prep")
         hout = self.act("pr.hout", B, T, S.pr_hid, self.adt)
-        gb = self.act("pr.gb", B, T, 2 * S.pr_hid, torch.float32)
-        for i in range(S.pr_layers):
+        nl = S.pr_layers
+        if getattr(W, "pr_aln_all", None) is not None and self.kv_fuse:
+            # (r06) every layer's AdaLN gamma / beta from the style columns (never rewritten by the layers: d_txt ==
+            # pr_hid) in one stacked linear, layer i's at channels [2 pr_hid i, 2 pr_hid (i + 1))
+            gb = self.act("pr.gb_all", B, T, 2 * S.pr_hid * nl, torch.float32)
+            self.conv(W.pr_aln_all, xin.sl(S.d_txt, S.style_pr), gb, what="pr.aln")
+            g_at, gs = (lambda i: gb.ptr + 2 * S.pr_hid * i * 4), 2 * S.pr_hid * nl
+        else:
+            gb = self.act("pr.gb", B, T, 2 * S.pr_hid, torch.float32)
+            g_at, gs = (lambda i: gb.ptr), 2 * S.pr_hid
+        for i in range(nl):
             self.lstm(W.pr_de[i], xin, hout, f"pr.de{i}")
-            self.conv(W.pr_aln[i], xin.sl(S.d_txt, S.style_pr), gb, what=f"pr.aln{i}")
-            self.rowln(hout, Act(xin.t, 0, S.pr_hid), G=gb.ptr, gs=2 * S.pr_hid, Bt=gb.ptr + S.pr_hid * 4,
-                       bs=2 * S.pr_hid, gdiv=1, gadd=1.0, what=f"pr.adaln{i}")
+            if gs == 2 * S.pr_hid:
+                self.conv(W.pr_aln[i], xin.sl(S.d_txt, S.style_pr), gb, what=f"pr.aln{i}")
+            self.rowln(hout, Act(xin.t, 0, S.pr_hid), G=g_at(i), gs=gs, Bt=g_at(i) + S.pr_hid * 4,
+                       bs=gs, gdiv=1, gadd=1.0, what=f"pr.adaln{i}")
         ov = None
         if durations is not None:
             if (durations.device.type != "cpu" and durations.dtype == torch.int32 and durations.is_contiguous() and

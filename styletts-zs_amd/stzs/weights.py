@@ -539,6 +539,11 @@ class PackedModel:
         # --- predictor ---
         self.pr_de = [pack_lstm(A, f"pr.de{i}", P, x3=xa) for i in range(S.pr_layers)]
         self.pr_aln = [L(f"pr.de{i}.aln") for i in range(S.pr_layers)]
+        # (r06) the duration encoder's AdaLN projections all read the same style columns: one stacked linear (each
+        # 128-column tile its own layer's K-step stream -- same bits, one launch instead of pr_layers)
+        self.pr_aln_all = pack_conv(A, "pr.de.aln_all", torch.cat([P[f"pr.de{i}.aln.w"] for i in range(S.pr_layers)]),
+                                    torch.cat([P[f"pr.de{i}.aln.b"] for i in range(S.pr_layers)]), x3=xa) \
+            if (2 * S.pr_hid) % 128 == 0 else None
         self.pr_dur_lstm = pack_lstm(A, "pr.dur_lstm", P, x3=xa)
         self.pr_dur_proj = L("pr.dur_proj")
         self.pr_shared = pack_lstm(A, "pr.shared", P, x3=xa)
